@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training throughput of the reference toy CNN on MI355X.
+
+Metric (BASELINE.json): images/sec for the whole node, toy CNN (``Net``, /root/reference/mnist/
+main.py:130-147) on synthetic MNIST, DDP at 1/2/4/8 GPUs (weak scaling: 128 images per GPU per
+step, the reference's default ``--batch-size``), fp32 (the reference's dtype), Adam(lr=1e-3).
+
+One timed "step" is the full reference step (main.py:84-99): forward, cross-entropy, backward,
+gradient all-reduce + average over ranks (RCCL, bucketed, overlapped with the conv backward),
+Adam update, loss/accuracy meters.  Each rank trains on its DistributedSampler shard of a
+60,000-sample synthetic set (random-init weights, synthetic data: no network on the box).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...)
+
+W untimed warm-up steps, then exactly K steps bracketed by barrier + device synchronize on both
+sides; the elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_METRIC = "images/sec (whole node) + DDP scaling eff, toy CNN synthetic MNIST 1/2/4/8 GPU"
+STOCK_TORCH_W1 = 121442.1   # same-hardware stock-PyTorch reference loop, W=1 (profiles/baseline/)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--batch-size", type=int, default=128, help="per-GPU batch (reference default 128)")
+    ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
+    ap.add_argument("--train-size", type=int, default=60000)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_distributed_example_amd import dist
+    from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_mnist
+    from pytorch_distributed_example_amd.engine import LeNetTrainStep
+    from pytorch_distributed_example_amd.models import build_net
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    comm = None
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
+        comm = dist.engine_comm()
+
+    net = build_net(seed=args.seed, device=dev)
+    if comm is not None:
+        dist.broadcast_parameters(net)            # DDP semantics: replicas start identical
+    eng = LeNetTrainStep(net, batch_size=args.batch_size, lr=1e-3, comm=comm, overlap=not args.no_overlap)
+    train = synthetic_mnist(args.train_size, seed=args.seed, device=dev, kind="fashion")
+    eng.bind_dataset(train.images, train.labels)
+    sampler = DistributedSampler(train, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
+    idx = sampler.indices_tensor()
+    nfull = idx.numel() // args.batch_size
+    eng.set_epoch_indices(idx[: nfull * args.batch_size])   # full batches only: every timed step is B=128
+
+    def run(n):
+        if args.mode == "graph":
+            for _ in range(n):
+                eng.replay()
+        else:
+            for _ in range(n):
+                eng.step()
+
+    if args.mode == "graph":
+        eng.capture()
+    run(args.warmup)
+    torch.cuda.synchronize()
+    eng.read_meters(reset=True)                    # meters cover the timed steps only
+    if comm is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if comm is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if comm is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_sum, correct, _ = eng.read_meters()
+    n_img = args.steps * args.batch_size * world
+    ips = n_img / elapsed
+    if rank == 0:
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(ips, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (class-conditional MNIST-shaped, device resident), random-init weights",
+            "config": {
+                "model": "toy CNN Net (conv5x5 20 -> conv5x5 50 -> fc 500 -> fc 10), 431,080 params",
+                "global_batch": args.batch_size * world,
+                "per_gpu_batch": args.batch_size,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "optimizer": "Adam(lr=1e-3)",
+                "mode": args.mode,
+                "grad_allreduce": "none" if world == 1 else ("bucketed-overlap" if not args.no_overlap else "flat"),
+            },
+            "stock_torch_same_hw_w1_images_per_s": STOCK_TORCH_W1,
+            "speedup_vs_stock_torch_per_gpu": round(ips / world / STOCK_TORCH_W1, 2),
+            "train_loss_mean_timed_rank0": round(loss_sum / max(1, args.steps * args.batch_size), 5),
+            "train_acc_timed_rank0": round(correct / max(1, args.steps * args.batch_size), 5),
+        }
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

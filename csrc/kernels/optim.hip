@@ -1,0 +1,173 @@
+// Fused optimizers over flat fp32 buffers (one launch per step for ALL parameters).
+//
+// Adam / AdamW reproduce torch.optim.Adam's single-tensor math (torch/optim/adam.py:347-460):
+//   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g
+//   p -= (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+// The step counter lives on the device: every block reads t = *step + 1 and the last block to
+// arrive publishes *step = t (arrival counter reset in the same block), so the whole optimizer
+// step is capturable in a hipGraph and replayable without host involvement.  `bump` = number of
+// consecutive int64 counters advanced by the last block (0: none; [0] is the optimizer step).
+// grad_scale folds the DDP 1/world_size average (or any loss scale) into the update.
+// Optional epilogue: repack the LeNet conv2 weight [50][20][5][5] into the [k'][64] layout the
+// conv2 forward kernel streams (k' = (kh*5+kw)*20+ci), so no separate repack launch exists.
+#include "pde_hip.h"
+#include "pde_kernels.h"
+
+namespace {
+
+struct Pack {
+  long long off;   // flat offset of conv2.weight, -1 = no repack
+  float* dst;      // [500][64]
+};
+
+__device__ __forceinline__ void pack_store(const Pack& pk, long long i, float v) {
+  const long long e = i - pk.off;
+  if (pk.off >= 0 && e >= 0 && e < 25000) {
+    const int co = (int)(e / 500), k = (int)(e % 500), ci = k / 25, r = k % 25;
+    pk.dst[(r * 20 + ci) * 64 + co] = v;
+  }
+}
+
+// The arrival add carries a data dependency on the step value this block read, so it cannot be
+// issued before that read returned: no block can observe the bumped counter.
+__device__ __forceinline__ bool last_block(unsigned* arrive, long long t) {
+  __shared__ int is_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(arrive, t > 0 ? 1u : 2u);
+    is_last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  return is_last != 0;
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v, long long n4,
+                                              float lr, float b1, float b2, float eps, float wd, int decoupled,
+                                              float grad_scale, long long* __restrict__ step,
+                                              unsigned* __restrict__ arrive, int bump, Pack pk) {
+  const long long t = *step + 1;
+  const float bc1 = 1.f - powf(b1, (float)t);
+  const float bc2 = 1.f - powf(b2, (float)t);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float omb1 = 1.f - b1, omb2 = 1.f - b2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
+    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = ga[j] * grad_scale;
+      if (wd != 0.f) {
+        if (decoupled) pa[j] = pa[j] * (1.f - lr * wd);
+        else gr = gr + wd * pa[j];
+      }
+      ma[j] = ma[j] + omb1 * (gr - ma[j]);
+      va[j] = va[j] * b2 + omb2 * gr * gr;
+      const float denom = sqrtf(va[j]) / bc2s + eps;
+      pa[j] = pa[j] - step_size * (ma[j] / denom);
+      pack_store(pk, 4 * i + j, pa[j]);
+    }
+    p4[i] = pp; m4[i] = mm; v4[i] = vv;
+  }
+  if (bump > 0 && last_block(arrive, t) && threadIdx.x == 0) {
+    step[0] = t;
+    for (int c = 1; c < bump; ++c) step[c] += 1;   // extra device counters (e.g. batch position)
+    *arrive = 0u;
+  }
+}
+
+// torch.optim.SGD semantics (torch/optim/sgd.py): d_p = g + wd*p; buf = momentum*buf + (1-dampening)*d_p
+// (buf = d_p on the first step); d_p = nesterov ? d_p + momentum*buf : buf; p -= lr*d_p.
+__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                             long long n4, float lr, float momentum, float dampening, float wd,
+                                             int nesterov, float grad_scale, long long* __restrict__ step,
+                                             unsigned* __restrict__ arrive, int bump, Pack pk) {
+  const long long t = *step + 1;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* b4 = reinterpret_cast<float4*>(buf);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 pp = p4[i], gg = g4[i];
+    float4 bb = momentum != 0.f ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* pa = &pp.x; float* ga = &gg.x; float* ba = &bb.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = ga[j] * grad_scale;
+      if (wd != 0.f) d = d + wd * pa[j];
+      if (momentum != 0.f) {
+        ba[j] = (t == 1) ? d : momentum * ba[j] + (1.f - dampening) * d;
+        d = nesterov ? d + momentum * ba[j] : ba[j];
+      }
+      pa[j] = pa[j] - lr * d;
+      pack_store(pk, 4 * i + j, pa[j]);
+    }
+    p4[i] = pp;
+    if (momentum != 0.f) b4[i] = bb;
+  }
+  if (bump > 0 && last_block(arrive, t) && threadIdx.x == 0) {
+    step[0] = t;
+    for (int c = 1; c < bump; ++c) step[c] += 1;   // extra device counters (e.g. batch position)
+    *arrive = 0u;
+  }
+}
+
+__global__ void k_lenet_pack_w2(const float* __restrict__ w2, float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 500 * 64) {
+    const int kp = i >> 6, co = i & 63, r = kp / 20, ci = kp % 20;
+    dst[i] = co < 50 ? w2[co * 500 + ci * 25 + r] : 0.f;
+  }
+}
+
+__global__ void k_scale(float* __restrict__ x, long long n, float s) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] *= s;
+}
+
+inline int grid_for(long long n4) {
+  long long blocks = (n4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t pde_adam_flat(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2,
+                         float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
+                         int bump, long long pack_off, float* pack_dst, hipStream_t st) {
+  if (n % 4) return hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n4)), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps, wd, decoupled,
+                     grad_scale, step, arrive, bump, Pack{pack_off, pack_dst});
+  return hipGetLastError();
+}
+
+hipError_t pde_sgd_flat(float* p, const float* g, float* buf, long long n, float lr, float momentum, float dampening,
+                        float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
+                        long long pack_off, float* pack_dst, hipStream_t st) {
+  if (n % 4) return hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4)), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
+                     nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst});
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_pack_w2(const float* w2, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_lenet_pack_w2, dim3((500 * 64 + 255) / 256), dim3(256), 0, st, w2, dst);
+  return hipGetLastError();
+}
+
+hipError_t pde_scale(float* x, long long n, float s, hipStream_t st) {
+  hipLaunchKernelGGL(k_scale, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, x, n, s);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,230 @@
+// torch <-> HIP kernel binding layer for the `_kernels` extension.
+//
+// Every function takes preallocated tensors (the Python engine owns all workspaces so the whole
+// training step is capturable in a hipGraph), validates device / dtype / contiguity / size, and
+// launches on the caller's current HIP stream.  Device code lives in csrc/kernels/*.hip and is
+// reached through the extern "C" launchers of pde_kernels.h.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <optional>
+
+#include "pde_kernels.h"
+
+namespace {
+
+using OptT = std::optional<at::Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t min_numel = 0) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.numel() >= min_numel, name, " has ", t.numel(), " elements, needs >= ", min_numel);
+}
+
+template <typename T>
+T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+template <typename T>
+T* optr(const OptT& t, const char* name, at::ScalarType dt, int64_t min_numel = 0) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cuda(*t, name, dt, min_numel);
+  return ptr<T>(*t);
+}
+
+void hip_check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e));
+}
+
+constexpr auto F32 = at::kFloat;
+constexpr auto I32 = at::kInt;
+constexpr auto I64 = at::kLong;
+constexpr auto U8 = at::kByte;
+constexpr auto F64 = at::kDouble;
+
+// ------------------------------------------------------------------------------------------------
+void lenet_conv1_fwd(const at::Tensor& X, const OptT& idx, const OptT& step, int64_t nbatches, int64_t stride,
+                     const OptT& labels_all,
+                     int64_t B, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& P1,
+                     const at::Tensor& A1, const OptT& cur_row, const OptT& cur_lbl, const OptT& zero) {
+  TORCH_CHECK(B >= 1, "batch must be >= 1");
+  check_cuda(X, "X", F32);
+  TORCH_CHECK(X.numel() % 784 == 0, "X must be [N,1,28,28]");
+  if (!idx.has_value()) TORCH_CHECK(X.numel() >= B * 784, "X smaller than batch");
+  check_cuda(w, "conv1.weight", F32, 500);
+  check_cuda(bias, "conv1.bias", F32, 20);
+  check_cuda(P1, "P1", F32, B * 2880);
+  check_cuda(A1, "A1", U8, B * 2880);
+  const int* ip = optr<int>(idx, "idx", I32, B);
+  const long long* sp = optr<long long>(step, "step", I64, 1);
+  const int64_t st = stride > 0 ? stride : B;
+  if (sp) TORCH_CHECK(ip && nbatches >= 1 && idx->numel() >= (nbatches - 1) * st + B, "step-indexed batches need idx");
+  float* zp = optr<float>(zero, "zero", F32);
+  hip_check(pde_lenet_conv1_fwd(ptr<float>(X), ip, sp, (int)nbatches, (int)st, optr<long long>(labels_all, "labels", I64), (int)B,
+                                ptr<float>(w), ptr<float>(bias), ptr<float>(P1), ptr<uint8_t>(A1),
+                                optr<int>(cur_row, "cur_row", I32, B), optr<long long>(cur_lbl, "cur_lbl", I64, B), zp,
+                                zp ? (int)zero->numel() : 0, cur_stream()),
+            "lenet_conv1_fwd");
+}
+
+void lenet_conv2_fwd(const at::Tensor& P1, int64_t B, const at::Tensor& Wt2, const at::Tensor& bias,
+                     const at::Tensor& P2, const at::Tensor& A2) {
+  check_cuda(P1, "P1", F32, B * 2880);
+  check_cuda(Wt2, "Wt2", F32, 500 * 64);
+  check_cuda(bias, "conv2.bias", F32, 50);
+  check_cuda(P2, "P2", F32, B * 800);
+  check_cuda(A2, "A2", U8, B * 800);
+  hip_check(pde_lenet_conv2_fwd(ptr<float>(P1), (int)B, ptr<float>(Wt2), ptr<float>(bias), ptr<float>(P2),
+                                ptr<uint8_t>(A2), cur_stream()),
+            "lenet_conv2_fwd");
+}
+
+void lenet_fc1_fwd(const at::Tensor& P2, int64_t B, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& H1) {
+  check_cuda(P2, "P2", F32, B * 800);
+  check_cuda(W, "fc1.weight", F32, 500 * 800);
+  check_cuda(bias, "fc1.bias", F32, 500);
+  check_cuda(H1, "H1", F32, B * 500);
+  hip_check(pde_lenet_fc1_fwd(ptr<float>(P2), (int)B, ptr<float>(W), ptr<float>(bias), ptr<float>(H1), cur_stream()),
+            "lenet_fc1_fwd");
+}
+
+void lenet_head(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& labels,
+                double inv_b, const OptT& logp, const OptT& dZ2, const OptT& dZ1, const OptT& loss_sum,
+                const OptT& correct) {
+  check_cuda(H1, "H1", F32, B * 500);
+  check_cuda(W2, "fc2.weight", F32, 5000);
+  check_cuda(b2, "fc2.bias", F32, 10);
+  check_cuda(labels, "labels", I64, B);
+  float* dz1 = optr<float>(dZ1, "dZ1", F32, B * 500);
+  float* dz2 = optr<float>(dZ2, "dZ2", F32, B * 10);
+  TORCH_CHECK((dz1 == nullptr) == (dz2 == nullptr), "dZ1 and dZ2 go together");
+  hip_check(pde_lenet_head(ptr<float>(H1), (int)B, ptr<float>(W2), ptr<float>(b2), ptr<long long>(labels), (float)inv_b,
+                           optr<float>(logp, "logp", F32, B * 10), dz2, dz1, optr<double>(loss_sum, "loss_sum", F64, 1),
+                           optr<unsigned long long>(correct, "correct", I64, 1), cur_stream()),
+            "lenet_head");
+}
+
+void lenet_head_bwd(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const at::Tensor& logp, const at::Tensor& g,
+                    const at::Tensor& dZ2, const at::Tensor& dZ1) {
+  check_cuda(H1, "H1", F32, B * 500);
+  check_cuda(W2, "fc2.weight", F32, 5000);
+  check_cuda(logp, "logp", F32, B * 10);
+  check_cuda(g, "grad_logp", F32, B * 10);
+  check_cuda(dZ2, "dZ2", F32, B * 10);
+  check_cuda(dZ1, "dZ1", F32, B * 500);
+  hip_check(pde_lenet_head_bwd(ptr<float>(H1), (int)B, ptr<float>(W2), ptr<float>(logp), ptr<float>(g), ptr<float>(dZ2),
+                               ptr<float>(dZ1), cur_stream()),
+            "lenet_head_bwd");
+}
+
+void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& dZ1, const at::Tensor& dZ2,
+                  const at::Tensor& W1, int64_t B, const at::Tensor& dP2m, const at::Tensor& gW1, const at::Tensor& gb1,
+                  const at::Tensor& gW2, const at::Tensor& gb2) {
+  check_cuda(P2, "P2", F32, B * 800);
+  check_cuda(H1, "H1", F32, B * 500);
+  check_cuda(dZ1, "dZ1", F32, B * 500);
+  check_cuda(dZ2, "dZ2", F32, B * 10);
+  check_cuda(W1, "fc1.weight", F32, 400000);
+  check_cuda(dP2m, "dP2m", F32, B * 800);
+  check_cuda(gW1, "gW1", F32, 400000);
+  check_cuda(gb1, "gb1", F32, 500);
+  check_cuda(gW2, "gW2", F32, 5000);
+  check_cuda(gb2, "gb2", F32, 10);
+  hip_check(pde_lenet_fc_bwd(ptr<float>(P2), ptr<float>(H1), ptr<float>(dZ1), ptr<float>(dZ2), ptr<float>(W1), (int)B,
+                             ptr<float>(dP2m), ptr<float>(gW1), ptr<float>(gb1), ptr<float>(gW2), ptr<float>(gb2),
+                             cur_stream()),
+            "lenet_fc_bwd");
+}
+
+void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tensor& P1, const at::Tensor& A1,
+                    const at::Tensor& dP2m, const at::Tensor& A2, const at::Tensor& W2c, int64_t B,
+                    const at::Tensor& gW1c, const at::Tensor& gb1c, const at::Tensor& gW2c, const at::Tensor& gb2c) {
+  check_cuda(X, "X", F32);
+  check_cuda(rows, "rows", I32, B);
+  check_cuda(P1, "P1", F32, B * 2880);
+  check_cuda(A1, "A1", U8, B * 2880);
+  check_cuda(dP2m, "dP2m", F32, B * 800);
+  check_cuda(A2, "A2", U8, B * 800);
+  check_cuda(W2c, "conv2.weight", F32, 25000);
+  check_cuda(gW1c, "gW1c", F32, 500);
+  check_cuda(gb1c, "gb1c", F32, 20);
+  check_cuda(gW2c, "gW2c", F32, 25000);
+  check_cuda(gb2c, "gb2c", F32, 50);
+  hip_check(pde_lenet_conv_bwd(ptr<float>(X), ptr<int>(rows), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(dP2m),
+                               ptr<uint8_t>(A2), ptr<float>(W2c), (int)B, ptr<float>(gW1c), ptr<float>(gb1c),
+                               ptr<float>(gW2c), ptr<float>(gb2c), cur_stream()),
+            "lenet_conv_bwd");
+}
+
+// ------------------------------------------------------------------------------------------------
+void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v, double lr,
+               double b1, double b2, double eps, double wd, bool decoupled, double grad_scale, const at::Tensor& step,
+               const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst) {
+  const int64_t n = p.numel();
+  check_cuda(p, "params", F32);
+  check_cuda(g, "grads", F32, n);
+  check_cuda(m, "exp_avg", F32, n);
+  check_cuda(v, "exp_avg_sq", F32, n);
+  check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
+  check_cuda(arrive, "arrive", I32, 1);
+  TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
+  float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
+  if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
+  hip_check(pde_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), n, (float)lr, (float)b1,
+                          (float)b2, (float)eps, (float)wd, decoupled ? 1 : 0, (float)grad_scale, ptr<long long>(step),
+                          ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, cur_stream()),
+            "adam_flat");
+}
+
+void sgd_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, double lr, double momentum,
+              double dampening, double wd, bool nesterov, double grad_scale, const at::Tensor& step,
+              const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst) {
+  const int64_t n = p.numel();
+  check_cuda(p, "params", F32);
+  check_cuda(g, "grads", F32, n);
+  check_cuda(buf, "momentum_buffer", F32, momentum != 0.0 ? n : 0);
+  check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
+  check_cuda(arrive, "arrive", I32, 1);
+  TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
+  float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
+  if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
+  hip_check(pde_sgd_flat(ptr<float>(p), ptr<float>(g), ptr<float>(buf), n, (float)lr, (float)momentum,
+                         (float)dampening, (float)wd, nesterov ? 1 : 0, (float)grad_scale, ptr<long long>(step),
+                         ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, cur_stream()),
+            "sgd_flat");
+}
+
+void lenet_pack_w2(const at::Tensor& w2, const at::Tensor& dst) {
+  check_cuda(w2, "conv2.weight", F32, 25000);
+  check_cuda(dst, "Wt2", F32, 500 * 64);
+  hip_check(pde_lenet_pack_w2(ptr<float>(w2), ptr<float>(dst), cur_stream()), "lenet_pack_w2");
+}
+
+void scale_(const at::Tensor& x, double s) {
+  check_cuda(x, "x", F32);
+  hip_check(pde_scale(ptr<float>(x), x.numel(), (float)s, cur_stream()), "scale_");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "CDNA4 (gfx950) HIP kernels of pytorch_distributed_example_amd";
+  m.attr("arch") = "gfx950";
+  namespace py = pybind11;
+  m.def("lenet_conv1_fwd", &lenet_conv1_fwd, py::arg("X"), py::arg("idx"), py::arg("step"), py::arg("nbatches"),
+        py::arg("stride"), py::arg("labels_all"), py::arg("B"), py::arg("w"), py::arg("bias"), py::arg("P1"), py::arg("A1"),
+        py::arg("cur_row"), py::arg("cur_lbl"), py::arg("zero"));
+  m.def("lenet_conv2_fwd", &lenet_conv2_fwd);
+  m.def("lenet_fc1_fwd", &lenet_fc1_fwd);
+  m.def("lenet_head", &lenet_head);
+  m.def("lenet_head_bwd", &lenet_head_bwd);
+  m.def("lenet_fc_bwd", &lenet_fc_bwd);
+  m.def("lenet_conv_bwd", &lenet_conv_bwd);
+  m.def("adam_flat", &adam_flat);
+  m.def("sgd_flat", &sgd_flat);
+  m.def("lenet_pack_w2", &lenet_pack_w2);
+  m.def("scale_", &scale_);
+}

@@ -1,0 +1,258 @@
+"""Fused, graph-capturable data-parallel training step for the reference toy CNN.
+
+Per step (reference semantics: /root/reference/mnist/main.py:84-99 forward, cross_entropy,
+zero_grad, backward, average_gradients, Adam step, meters) this issues:
+
+  compute stream : F1 conv1 (+gather, +grad zeroing) -> F2 conv2 -> F3 fc1 -> F4 head/loss/dlogits
+                   -> B1 fc backward --(event)--> B2 conv backward --(event)--> [wait comm] -> fused Adam
+  comm stream    :                    all_reduce(bucket 0: fc grads, 1.62 MB) | all_reduce(bucket 1: conv grads)
+
+* Gradients live in one flat buffer laid out in bucket order (``parallel.flat``); bucket 0 (fc1/fc2,
+  94 % of the bytes) is complete after B1, so its all-reduce overlaps the conv backward (B2).
+* The 1/world_size average of ``average_gradients`` (main.py:122-127) is folded into Adam's
+  ``grad_scale``; all-reduces are plain SUMs on the flat bucket views.
+* Loss/accuracy meters accumulate on the device and are read once per epoch (no per-step
+  ``.item()`` syncs, survey S1).
+* The dataset is device resident; the epoch permutation is uploaded once per epoch and batch b of
+  the epoch is gathered inside F1 from a device batch counter that the fused Adam advances, so a
+  captured hipGraph replays consecutive steps with no host work at all.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .._ext import kernels
+from ..ops.lenet_fused import pack_conv2_weight
+from ..parallel.flat import FlatLayout
+
+FC_BUCKET = ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"]
+CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"]
+
+
+class LeNetTrainStep:
+    def __init__(self, net: torch.nn.Module, batch_size: int = 128, lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, optimizer: str = "adam", momentum: float = 0.0,
+                 comm=None, overlap: bool = True):
+        self.net = net
+        p0 = next(net.parameters())
+        if not p0.is_cuda:
+            raise ValueError("LeNetTrainStep needs the model on a GPU")
+        self.device = p0.device
+        self.B = int(batch_size)
+        self.lr, self.betas, self.eps, self.wd = float(lr), tuple(betas), float(eps), float(weight_decay)
+        self.optimizer = optimizer
+        self.momentum = float(momentum)
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.overlap = overlap
+        self.K = kernels()
+        dev = self.device
+        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, CONV_BUCKET])
+        self.params, self.grads = self.layout.bind(net)
+        V = self.layout.view
+        self.p = {n: V(self.params, n) for n in self.layout.slots}
+        self.g = {n: V(self.grads, n) for n in self.layout.slots}
+        self.bucket_grads = [self.layout.bucket_view(self.grads, i) for i in range(2)]
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params) if optimizer == "adam" else self.m
+        self.counters = torch.zeros(2, device=dev, dtype=torch.int64)   # [optimizer step, batch in epoch]
+        self.arrive = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.Wt2 = pack_conv2_weight(self.p["conv2.weight"])
+        self.pack_off = self.layout.slots["conv2.weight"].offset
+        f32 = dict(device=dev, dtype=torch.float32)
+        B = self.B
+        self.P1 = torch.empty(B * 2880, **f32)
+        self.A1 = torch.empty(B * 2880, device=dev, dtype=torch.uint8)
+        self.P2 = torch.empty(B * 800, **f32)
+        self.A2 = torch.empty(B * 800, device=dev, dtype=torch.uint8)
+        self.H1 = torch.empty(B * 500, **f32)
+        self.dZ1 = torch.empty(B * 500, **f32)
+        self.dZ2 = torch.empty(B * 10, **f32)
+        self.dP2m = torch.empty(B * 800, **f32)
+        self.cur_row = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.cur_lbl = torch.zeros(B, device=dev, dtype=torch.int64)
+        self.loss_sum = torch.zeros(1, device=dev, dtype=torch.float64)
+        self.correct = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.samples = 0
+        self.eval_loss = torch.zeros(1, device=dev, dtype=torch.float64)
+        self.eval_correct = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.world > 1 else None
+        self._ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.X = self.Y = self.idx = None
+        self.nbatches = 0
+        self.graphs = {}
+
+    # ------------------------------------------------------------------ data binding
+    def bind_dataset(self, images: torch.Tensor, labels: torch.Tensor):
+        if images.device != self.device or labels.device != self.device:
+            raise ValueError("dataset must be resident on the training device")
+        self.X = images.reshape(images.shape[0], 784).contiguous()
+        self.Y = labels.to(torch.int64).contiguous()
+
+    def set_epoch_indices(self, idx: torch.Tensor):
+        """Upload this epoch's (rank-local) sample order; batches are [i*B, (i+1)*B) plus a ragged tail."""
+        idx = idx.to(self.device, torch.int32).contiguous()
+        n = idx.numel()
+        if self.idx is not None and self.idx.numel() == n:
+            self.idx.copy_(idx)          # keep the address captured by existing graphs
+        else:
+            self.idx = idx
+            self.graphs.clear()
+        self.nfull = n // self.B
+        self.tail = n - self.nfull * self.B
+        self.nbatches = self.nfull + (1 if self.tail else 0)
+        self.counters[1].zero_()
+
+    # ------------------------------------------------------------------ the step
+    def _launch(self, B: int):
+        K, p, g = self.K, self.p, self.g
+        K.lenet_conv1_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
+                          p["conv1.weight"], p["conv1.bias"], self.P1, self.A1, self.cur_row, self.cur_lbl,
+                          self.bucket_grads[1])
+        K.lenet_conv2_fwd(self.P1, B, self.Wt2, p["conv2.bias"], self.P2, self.A2)
+        K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1)
+        K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], self.cur_lbl, 1.0 / B, None, self.dZ2, self.dZ1,
+                     self.loss_sum, self.correct)
+        K.lenet_fc_bwd(self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
+                       g["fc1.bias"], g["fc2.weight"], g["fc2.bias"])
+        cur = torch.cuda.current_stream(self.device)
+        if self.world > 1 and self.overlap:
+            self._ev[0].record(cur)
+            self.comm_stream.wait_event(self._ev[0])
+            with torch.cuda.stream(self.comm_stream):
+                self.comm.all_reduce_(self.bucket_grads[0])
+        K.lenet_conv_bwd(self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
+                         g["conv1.weight"], g["conv1.bias"], g["conv2.weight"], g["conv2.bias"])
+        if self.world > 1:
+            self._ev[1].record(cur)
+            self.comm_stream.wait_event(self._ev[1])
+            with torch.cuda.stream(self.comm_stream):
+                if not self.overlap:
+                    self.comm.all_reduce_(self.grads)
+                else:
+                    self.comm.all_reduce_(self.bucket_grads[1])
+            cur.wait_stream(self.comm_stream)
+        scale = 1.0 / self.world
+        if self.optimizer == "adam":
+            K.adam_flat(self.params, self.grads, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps,
+                        self.wd, False, scale, self.counters, self.arrive, 2, self.pack_off, self.Wt2)
+        else:
+            K.sgd_flat(self.params, self.grads, self.m, self.lr, self.momentum, 0.0, self.wd, False, scale,
+                       self.counters, self.arrive, 2, self.pack_off, self.Wt2)
+
+    def _batch_size_at(self, b: int) -> int:
+        return self.B if b < self.nfull else self.tail
+
+    def step(self, B: Optional[int] = None):
+        """Run one training step eagerly (B defaults to the full batch size)."""
+        self._launch(B or self.B)
+
+    def capture(self, B: Optional[int] = None, warmup: int = 0):
+        """Capture one step of batch size B into a hipGraph (replayed by ``replay``)."""
+        B = B or self.B
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._launch(B)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._launch(B)
+        self.graphs[B] = g
+        return g
+
+    def replay(self, B: Optional[int] = None):
+        B = B or self.B
+        g = self.graphs.get(B)
+        if g is None:
+            g = self.capture(B)
+            # capturing does not execute: run the captured step now so call semantics stay "one step"
+        g.replay()
+
+    # ------------------------------------------------------------------ epochs / meters
+    def run_epoch(self, use_graph: bool = True):
+        """All batches of the bound epoch (full batches via graph replay, then the ragged tail)."""
+        for b in range(self.nbatches):
+            Bb = self._batch_size_at(b)
+            if use_graph:
+                self.replay(Bb)
+            else:
+                self.step(Bb)
+        self.samples += self.nfull * self.B + self.tail
+
+    def read_meters(self, reset: bool = True):
+        loss = float(self.loss_sum.item())
+        correct = int(self.correct.item())
+        n = self.samples
+        if reset:
+            self.loss_sum.zero_()
+            self.correct.zero_()
+            self.samples = 0
+        return loss, correct, n
+
+    @torch.no_grad()
+    def evaluate(self, images: torch.Tensor, labels: torch.Tensor, batch_size: Optional[int] = None):
+        """Forward-only pass over a (device) test set with the fused kernels; returns (loss_sum, correct, n)."""
+        K, p = self.K, self.p
+        bs = batch_size or self.B
+        X = images.reshape(images.shape[0], 784).contiguous()
+        Y = labels.to(torch.int64).contiguous()
+        n = X.shape[0]
+        self.eval_loss.zero_()
+        self.eval_correct.zero_()
+        P1 = torch.empty(bs * 2880, device=self.device)
+        A1 = torch.empty(bs * 2880, device=self.device, dtype=torch.uint8)
+        P2 = torch.empty(bs * 800, device=self.device)
+        A2 = torch.empty(bs * 800, device=self.device, dtype=torch.uint8)
+        H1 = torch.empty(bs * 500, device=self.device)
+        for s in range(0, n, bs):
+            B = min(bs, n - s)
+            K.lenet_conv1_fwd(X[s:s + B], None, None, 0, 0, None, B, p["conv1.weight"], p["conv1.bias"], P1, A1,
+                              None, None, None)
+            K.lenet_conv2_fwd(P1, B, self.Wt2, p["conv2.bias"], P2, A2)
+            K.lenet_fc1_fwd(P2, B, p["fc1.weight"], p["fc1.bias"], H1)
+            K.lenet_head(H1, B, p["fc2.weight"], p["fc2.bias"], Y[s:s + B], 1.0 / B, None, None, None,
+                         self.eval_loss, self.eval_correct)
+        return float(self.eval_loss.item()), int(self.eval_correct.item()), n
+
+    # ------------------------------------------------------------------ optimizer state (torch format)
+    def optimizer_state_dict(self):
+        """``torch.optim.Adam.state_dict()``-compatible dict (params indexed in registration order)."""
+        names = [n for n, _ in self.net.named_parameters()]
+        step = float(self.counters[0].item())
+        state = {}
+        for i, n in enumerate(names):
+            st = {"step": torch.tensor(step)}
+            if self.optimizer == "adam":
+                st["exp_avg"] = self.layout.view(self.m, n).detach().clone()
+                st["exp_avg_sq"] = self.layout.view(self.v, n).detach().clone()
+            elif self.momentum:
+                st["momentum_buffer"] = self.layout.view(self.m, n).detach().clone()
+            state[i] = st
+        group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.wd, "amsgrad": False,
+                 "params": list(range(len(names)))} if self.optimizer == "adam" else {
+            "lr": self.lr, "momentum": self.momentum, "weight_decay": self.wd, "dampening": 0.0,
+            "nesterov": False, "params": list(range(len(names)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd):
+        names = [n for n, _ in self.net.named_parameters()]
+        for i, n in enumerate(names):
+            st = sd["state"].get(i)
+            if not st:
+                continue
+            if "exp_avg" in st:
+                self.layout.view(self.m, n).copy_(st["exp_avg"])
+                self.layout.view(self.v, n).copy_(st["exp_avg_sq"])
+            if "momentum_buffer" in st and st["momentum_buffer"] is not None:
+                self.layout.view(self.m, n).copy_(st["momentum_buffer"])
+            self.counters[0].fill_(int(float(st["step"])))
+        self.sync_params()
+
+    def sync_params(self):
+        """Re-derive kernel-side weight copies after parameters were changed externally."""
+        pack_conv2_weight(self.p["conv2.weight"], self.Wt2)

@@ -1,0 +1,3 @@
+"""Model zoo: the reference toy CNN (``Net``) plus the driver-added configs."""
+from .lenet import Net, build_net, PARAM_SPECS, NUM_PARAMS  # noqa: F401
+from .mlp import MLP  # noqa: F401

@@ -1,0 +1,96 @@
+"""Flat parameter / gradient storage laid out in communication-bucket order.
+
+All parameters of a module are re-homed into ONE contiguous fp32 buffer (``p.data`` becomes a view),
+and all gradients into a second one (``p.grad`` is a view).  Buckets are contiguous ranges of
+both buffers, so a bucket all-reduce is a single collective on a zero-copy view, and the fused
+optimizer updates every parameter in one launch.  Each tensor starts on a 64-element (256 B)
+boundary, so vectorised kernels and RCCL see aligned buffers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+ALIGN = 64
+
+
+@dataclass
+class Slot:
+    name: str
+    offset: int
+    numel: int
+    shape: Tuple[int, ...]
+
+
+class FlatLayout:
+    def __init__(self, named_shapes: Sequence[Tuple[str, Tuple[int, ...]]], buckets: Sequence[Sequence[str]],
+                 align: int = ALIGN):
+        shapes = dict(named_shapes)
+        seen = [n for b in buckets for n in b]
+        if sorted(seen) != sorted(shapes):
+            raise ValueError("buckets must partition the parameter set exactly")
+        self.slots: Dict[str, Slot] = {}
+        self.bucket_ranges: List[Tuple[int, int]] = []
+        self.bucket_names: List[List[str]] = [list(b) for b in buckets]
+        off = 0
+        for b in buckets:
+            start = off
+            for n in b:
+                shp = tuple(shapes[n])
+                numel = 1
+                for d in shp:
+                    numel *= d
+                self.slots[n] = Slot(n, off, numel, shp)
+                off += (numel + align - 1) // align * align
+            self.bucket_ranges.append((start, off))
+        self.total = off
+
+    @classmethod
+    def for_module(cls, module: torch.nn.Module, buckets=None, bucket_cap_bytes: int | None = None):
+        named = [(n, tuple(p.shape)) for n, p in module.named_parameters() if p.requires_grad]
+        if buckets is None:
+            buckets = reverse_order_buckets(named, bucket_cap_bytes or (25 << 20))
+        return cls(named, buckets)
+
+    def bind(self, module: torch.nn.Module, device=None, dtype=torch.float32):
+        """Move ``module``'s parameters into flat storage; returns (flat_params, flat_grads)."""
+        params = dict(module.named_parameters())
+        dev = device or next(iter(params.values())).device
+        flat_p = torch.zeros(self.total, device=dev, dtype=dtype)
+        flat_g = torch.zeros(self.total, device=dev, dtype=dtype)
+        for n, s in self.slots.items():
+            p = params[n]
+            v = flat_p[s.offset: s.offset + s.numel].view(s.shape)
+            v.copy_(p.detach())
+            p.data = v
+            p.grad = flat_g[s.offset: s.offset + s.numel].view(s.shape)
+        return flat_p, flat_g
+
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        s = self.slots[name]
+        return flat[s.offset: s.offset + s.numel].view(s.shape)
+
+    def bucket_view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
+        a, b = self.bucket_ranges[i]
+        return flat[a:b]
+
+
+def reverse_order_buckets(named_shapes, cap_bytes: int, elem_bytes: int = 4):
+    """DDP-style buckets: parameters in REVERSE registration order (gradients become ready roughly
+    in that order during backward), greedily packed up to ``cap_bytes`` per bucket."""
+    buckets, cur, cur_bytes = [], [], 0
+    for n, shp in reversed(list(named_shapes)):
+        numel = 1
+        for d in shp:
+            numel *= d
+        nb = numel * elem_bytes
+        if cur and cur_bytes + nb > cap_bytes:
+            buckets.append(cur)
+            cur, cur_bytes = [], 0
+        cur.append(n)
+        cur_bytes += nb
+    if cur:
+        buckets.append(cur)
+    return buckets

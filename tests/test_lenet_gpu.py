@@ -1,0 +1,137 @@
+"""GPU numerics of the fused LeNet HIP kernels vs plain PyTorch references (fp64 CPU)."""
+import pytest
+import torch
+
+from pytorch_distributed_example_amd.models import build_net
+from pytorch_distributed_example_amd import ops
+from pytorch_distributed_example_amd.engine import LeNetTrainStep
+from reference_impl import torch_twin, ref_step_grads
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _batch(B, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 1, 28, 28, generator=g)
+    y = torch.randint(0, 10, (B,), generator=g)
+    return x, y
+
+
+def _close(a, b, rtol, atol, what):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (ref scale {scale:.3e})"
+
+
+@pytest.mark.parametrize("B", [1, 16, 48, 76, 96, 128, 200])
+def _mostly_close(a, b, mean_tol, max_tol, what):
+    """Adam normalises each gradient element (g/sqrt(v)), so elements whose gradient is ~0 can move
+    by up to 2*lr on rounding noise alone; compare the bulk tightly and bound the worst case."""
+    d = (a.detach().double().cpu() - b.detach().double().cpu()).abs()
+    assert d.mean().item() <= mean_tol, f"{what}: mean abs diff {d.mean().item():.3e}"
+    assert d.max().item() <= max_tol, f"{what}: max abs diff {d.max().item():.3e}"
+
+
+def test_forward_matches_torch(B):
+    net = build_net(seed=1, device=DEV)
+    ref = torch_twin(net)
+    x, y = _batch(B, seed=B)
+    with torch.no_grad():
+        out = net(x.to(DEV))
+        r = ref(x.double())
+    _close(out, r, 1e-5, 1e-5, f"logp B={B}")
+
+
+@pytest.mark.parametrize("B", [1, 32, 76, 128])
+def test_backward_matches_torch(B):
+    net = build_net(seed=2, device=DEV)
+    ref = torch_twin(net)
+    x, y = _batch(B, seed=100 + B)
+    out = net(x.to(DEV))
+    loss = torch.nn.functional.nll_loss(torch.log_softmax(out, 1), y.to(DEV))  # CE(logp) as in the reference
+    loss.backward()
+    _, rloss, rg = ref_step_grads(ref, x.double(), y)
+    _close(loss, rloss, 1e-5, 1e-6, "loss")
+    for n, p in net.named_parameters():
+        _close(p.grad, rg[n], 2e-4, 1e-6, f"grad {n} B={B}")
+
+
+@pytest.mark.parametrize("B", [128, 76])
+def test_engine_step_grads_and_loss(B):
+    net = build_net(seed=3, device=DEV)
+    ref = torch_twin(net)
+    n = 4 * B + 10
+    x, y = _batch(n, seed=7)
+    eng = LeNetTrainStep(net, batch_size=B)
+    eng.bind_dataset(x.to(DEV), y.to(DEV))
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    eng.set_epoch_indices(perm)
+    eng.step(B)  # batch 0
+    torch.cuda.synchronize()
+    sel = perm[:B].long()
+    _, rloss, rg = ref_step_grads(ref, x[sel].double(), y[sel])
+    loss_sum, correct, _ = eng.read_meters()
+    _close(torch.tensor(loss_sum / B), rloss, 1e-5, 1e-6, "engine loss")
+    for name in rg:
+        _close(eng.g[name], rg[name], 2e-4, 1e-6, f"engine grad {name}")
+
+
+def test_adam_kernel_matches_torch_adam():
+    from pytorch_distributed_example_amd._ext import kernels
+    K = kernels()
+    torch.manual_seed(0)
+    n = 4096
+    p = torch.randn(n, device=DEV)
+    pref = p.detach().clone().cpu().requires_grad_(True)
+    opt = torch.optim.Adam([pref], lr=1e-3)
+    m = torch.zeros_like(p); v = torch.zeros_like(p)
+    step = torch.zeros(1, device=DEV, dtype=torch.int64); arrive = torch.zeros(1, device=DEV, dtype=torch.int32)
+    for it in range(5):
+        g = torch.randn(n) * (10 ** (it - 2))
+        pref.grad = g.clone()
+        opt.step()
+        K.adam_flat(p, g.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1.0, step, arrive, 1, -1, None)
+    torch.cuda.synchronize()
+    assert int(step.item()) == 5
+    _close(p, pref.detach(), 0, 2e-6, "adam params")
+
+
+def test_engine_multi_step_tracks_torch_adam():
+    B = 64
+    net = build_net(seed=4, device=DEV)
+    ref = torch_twin(net, dtype=torch.float32, device=DEV)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    n = 6 * B
+    x, y = _batch(n, seed=9)
+    xd, yd = x.to(DEV), y.to(DEV)
+    eng = LeNetTrainStep(net, batch_size=B)
+    eng.bind_dataset(xd, yd)
+    eng.set_epoch_indices(torch.arange(n, dtype=torch.int32))
+    for s in range(6):
+        eng.step(B)
+        sl = slice(s * B, (s + 1) * B)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(xd[sl]), yd[sl]).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    for (nm, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        _mostly_close(p, q, 2e-6, 6 * 2e-3, f"param after 6 steps {nm}")
+
+
+def test_graph_replay_equals_eager():
+    B = 128
+    x, y = _batch(5 * B, seed=11)
+    outs = []
+    for use_graph in (False, True):
+        net = build_net(seed=5, device=DEV)
+        eng = LeNetTrainStep(net, batch_size=B)
+        eng.bind_dataset(x.to(DEV), y.to(DEV))
+        eng.set_epoch_indices(torch.arange(5 * B, dtype=torch.int32))
+        eng.run_epoch(use_graph=use_graph)
+        torch.cuda.synchronize()
+        outs.append((eng.params.clone(), eng.read_meters()))
+    assert int(outs[0][1][1]) == int(outs[1][1][1])
+    _mostly_close(outs[1][0], outs[0][0], 2e-6, 5 * 2e-3, "graph vs eager params")
