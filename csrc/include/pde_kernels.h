@@ -9,31 +9,37 @@ extern "C" {
 #endif
 
 // ---- LeNet (toy CNN) fused kernels: csrc/kernels/lenet.hip ----
-hipError_t pde_lenet_conv1_fwd(const float* X, const int* idx, const long long* step, int nbatches, int stride,
-                               const long long* labels_all, int B, const float* w, const float* bias, float* P1,
-                               uint8_t* A1, int* cur_row, long long* cur_lbl, float* zero_ptr, int zero_n,
-                               hipStream_t st);
-hipError_t pde_lenet_conv2_fwd(const float* P1, int B, const float* Wt2, const float* bias, float* P2, uint8_t* A2,
-                               hipStream_t st);
-hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float* bias, float* H1, hipStream_t st);
+hipError_t pde_lenet_conv_fwd(const float* X, const int* idx, int n_idx, const long long* step, int nbatches,
+                              int stride, const long long* labels_all, int B, const float* w1, const float* b1,
+                              const float* Wt2, const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2,
+                              int* cur_row, long long* cur_lbl, float* zero_ptr, int zero_n, int dbg, hipStream_t st);
+hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float* bias, float* H1, long long* ctr,
+                             int nctr, hipStream_t st);
 hipError_t pde_lenet_head(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
-                          float inv_b, float* logp_out, float* dZ2, float* dZ1, double* loss_sum,
-                          unsigned long long* correct, hipStream_t st);
+                          float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
+                          double* loss_sum, unsigned long long* correct, hipStream_t st);
 hipError_t pde_lenet_head_bwd(const float* H1, int B, const float* W2, const float* logp, const float* g, float* dZ2,
                               float* dZ1, hipStream_t st);
 hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, const float* dZ2, const float* W1,
-                            int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, hipStream_t st);
+                            int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, const float* row_loss,
+                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg,
+                            hipStream_t st);
 hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, const uint8_t* A1,
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,
-                              float* gb1c, float* gW2c, float* gb2c, hipStream_t st);
+                              float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride, int dbg,
+                              hipStream_t st);
 
 // ---- optimizers: csrc/kernels/optim.hip ----
-hipError_t pde_adam_flat(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2,
+// fold_*: gradient replicas folded before the update: for e in [fold_off, fold_off + fold_len),
+// g[e] = sum_{r < fold_nrep} g[e + r * fold_stride] (written back); replica storage r >= 1 is skipped.
+hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, float lr, float b1, float b2,
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
-                         int bump, long long pack_off, float* pack_dst, hipStream_t st);
-hipError_t pde_sgd_flat(float* p, const float* g, float* buf, long long n, float lr, float momentum, float dampening,
+                         int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
+                         int fold_nrep, int fold_stride, hipStream_t st);
+hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, float momentum, float dampening,
                         float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
-                        long long pack_off, float* pack_dst, hipStream_t st);
+                        long long pack_off, float* pack_dst, long long fold_off, int fold_len, int fold_nrep,
+                        int fold_stride, hipStream_t st);
 hipError_t pde_lenet_pack_w2(const float* w2, float* dst, hipStream_t st);
 hipError_t pde_scale(float* x, long long n, float s, hipStream_t st);
 

@@ -2,17 +2,22 @@
 // /root/reference/mnist/main.py:130-147) trained with Adam + cross-entropy
 // (/root/reference/mnist/main.py:78-101).
 //
-// One training step = 6 launches (+ the fused Adam of adam.hip):
-//   F1 k_conv1_fwd : sampler-index gather + conv1(1->20,5x5) + bias + ReLU + maxpool2x2 (+argmax codes)
-//                    + zeroes the atomically-accumulated conv grads (side job)
-//   F2 k_conv2_fwd : conv2(20->50,5x5) as implicit GEMM on v_mfma_f32_32x32x2_f32 + bias + ReLU + pool
-//   F3 k_fc1_fwd   : fc1 (800->500) on v_mfma_f32_16x16x4_f32, split-K over 4 waves + bias + ReLU
-//   F4 k_head      : fc2 (500->10) + log_softmax + cross_entropy(log_softmax) + dlogits + fc2-dgrad +
-//                    ReLU mask -> dZ1, device-side loss/accuracy meters (no .item() per step)
-//   B1 k_fc_bwd    : dW1/db1 (MFMA), dW2/db2 (VALU), dP2 = dZ1*W1 (MFMA) masked by ReLU
-//   B2 k_conv_bwd  : conv2 wgrad (MFMA, atomics over image groups) + conv2 dgrad (MFMA) with col2im in
-//                    LDS + maxpool1/ReLU backward + conv1 wgrad (sparse, 1 of 4 pool positions)
-// Layout conventions (fp32 throughout, the reference model is fp32):
+// One training step = 5 launches here (+ the fused Adam of optim.hip):
+//   F1 k_conv_fwd : sampler-index gather + conv1(1->20) + bias + ReLU + maxpool (VALU, weights in LDS)
+//                   + conv2(20->50) implicit GEMM on v_mfma_f32_32x32x2_f32 + bias + ReLU + maxpool;
+//                   conv1's output never leaves LDS on the way to conv2 (it is also stored for backward)
+//   F2 k_fc1_fwd  : fc1 (800->500) on v_mfma_f32_16x16x4_f32, split-K over 4 waves + bias + ReLU
+//   F3 k_head     : fc2 (500->10) + log_softmax + cross_entropy(log_softmax) + dlogits + fc2-dgrad +
+//                   ReLU mask -> dZ1; per-row loss/hit for the device-side meters
+//   B1 k_fc_bwd   : dP2 = dZ1 W1 (MFMA, masked by ReLU), dW1|db1 and dW2|db2 (MFMA, bias grads as a
+//                   ones column of the B operand), meters folded by one thread (no atomics)
+//   B2 k_conv_bwd : conv2 wgrad|bgrad (MFMA, ones column, atomics over 8-image groups) + conv2 dgrad
+//                   (MFMA) with col2im as an LDS gather + maxpool1/ReLU backward + conv1 wgrad|bgrad (MFMA)
+// Latency rule used throughout (MI355X_MICROARCH.md, cycle constants): a dependent global round
+// trip costs ~1 us on data another XCD just wrote, so every kernel issues ALL of its global loads
+// into registers first (compile-time-sized, clamped indices, never a branch around a load), waits
+// once, and then works from LDS/registers.
+// Layouts (fp32 throughout, the reference model is fp32):
 //   X    [N][784] dataset (device resident), idx int32 sampler indices, labels int64
 //   P1   [B][20][12][12] pooled conv1 out, A1 uint8 argmax code (dy*2+dx) per pooled element
 //   P2   [B][800] pooled conv2 out flattened as view(-1, 800) (c*16 + h*4 + w), A2 codes
@@ -30,203 +35,276 @@ constexpr int kHid = 500;
 constexpr int kCls = 10;
 
 // -------------------------------------------------------------------------------------------------
-// Batch bookkeeping shared by the kernels: the batch's sample rows either come from an explicit
-// index list, or from an epoch permutation indexed by a device-side step counter (graph replay).
+// Batch bookkeeping: the batch's sample rows either come from an explicit index list, or from an
+// epoch permutation indexed by a device-side batch counter (hipGraph replay needs no host work).
 struct BatchSrc {
   const int* idx;              // epoch permutation (or per-batch list) or nullptr (identity)
-  const long long* step;       // device step counter or nullptr
+  const long long* step;       // device batch counter or nullptr
   int nbatches;                // batches per epoch when step != nullptr
-  int batch;                   // B (stride between batches in idx)
+  int batch;                   // stride between batches in idx
+  int n_idx;                   // length of idx (reads are clamped: a full-size launch on a ragged tail is safe)
 };
 
 __device__ __forceinline__ int sample_row(const BatchSrc& s, int b) {
   if (!s.idx) return b;
   long long off = 0;
   if (s.step) off = (long long)((*s.step) % s.nbatches) * s.batch;
-  return s.idx[off + b];
+  return s.idx[min(off + b, (long long)s.n_idx - 1)];
 }
 
 // =================================================================================================
-// F1: conv1 + bias + relu + maxpool.  grid (B, 4 channel groups of 5), block 192 (3 waves).
-// Thread t < 144 owns pooled position (ph, pw) = (t/12, t%12) for the block's 5 channels: a 6x6
-// input patch in registers, weights wave-uniform (scalar loads), 500 FMAs.
-// =================================================================================================
-__global__ __launch_bounds__(192) void k_conv1_fwd(const float* __restrict__ X, BatchSrc src,
-                                                   const long long* __restrict__ labels_all,
-                                                   const float* __restrict__ w, const float* __restrict__ bias,
-                                                   float* __restrict__ P1, uint8_t* __restrict__ A1,
-                                                   int* __restrict__ cur_row, long long* __restrict__ cur_lbl,
-                                                   float* __restrict__ zero_ptr, int zero_n) {
-  const int b = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
-  if (zero_ptr) {
-    const int nb = gridDim.x * gridDim.y, bid = g * gridDim.x + b;
-    for (int i = bid * 192 + t; i < zero_n; i += nb * 192) zero_ptr[i] = 0.f;
-  }
-  __shared__ __attribute__((aligned(16))) float xs[kImg];
-  const int row = sample_row(src, b);
-  if (g == 0 && t == 0) {
-    if (cur_row) cur_row[b] = row;
-    if (cur_lbl && labels_all) cur_lbl[b] = labels_all[row];
-  }
-  const float4* xsrc = reinterpret_cast<const float4*>(X + (size_t)row * kImg);
-  for (int i = t; i < kImg / 4; i += 192) reinterpret_cast<float4*>(xs)[i] = xsrc[i];
-  __syncthreads();
-  if (t >= 144) return;
-  const int ph = t / 12, pw = t - ph * 12;
-  float patch[36];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) patch[i * 6 + j] = xs[(2 * ph + i) * 28 + 2 * pw + j];
-#pragma unroll
-  for (int c = 0; c < 5; ++c) {
-    const int cc = g * 5 + c;
-    const float bv = bias[cc];
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const float wv = w[cc * 25 + kh * 5 + kw];
-        a0 = fmaf(wv, patch[kh * 6 + kw], a0);
-        a1 = fmaf(wv, patch[kh * 6 + kw + 1], a1);
-        a2 = fmaf(wv, patch[(kh + 1) * 6 + kw], a2);
-        a3 = fmaf(wv, patch[(kh + 1) * 6 + kw + 1], a3);
-      }
-    // relu then maxpool (first maximum in scan order wins, as ATen's max_pool2d)
-    float r0 = fmaxf(a0 + bv, 0.f), r1 = fmaxf(a1 + bv, 0.f), r2 = fmaxf(a2 + bv, 0.f), r3 = fmaxf(a3 + bv, 0.f);
-    float best = r0; int code = 0;
-    if (r1 > best) { best = r1; code = 1; }
-    if (r2 > best) { best = r2; code = 2; }
-    if (r3 > best) { best = r3; code = 3; }
-    const size_t o = ((size_t)(b * 20 + cc) * 12 + ph) * 12 + pw;
-    P1[o] = best;
-    A1[o] = (uint8_t)code;
-  }
-}
-
-// =================================================================================================
-// F2: conv2 implicit GEMM.  grid (B, 2 row-halves), block 256.
-// Per block: C[co 64][px 32] = sum_{k'<500} Wt2[k'][co] * im2col[k'][px], px = output rows 4h..4h+3.
-// wave w: co-tile (w&1), K-half (w>>1), 125 x v_mfma_f32_32x32x2_f32 on one accumulator (the
-// instruction's dependent latency equals its issue interval, so one chain runs at full rate).
-// A (weights) streams from L2 straight to VGPRs (coalesced 2 x 128 B per step); B from LDS.
+// F1: conv1 + conv2 forward.  grid (B, 2 co-tiles), block 256.
+// Block (b, ct) stages the ct-th 32 columns of Wt2 (64 KB) and its image; the weight loads are
+// issued right after the image / conv1 weights so their latency hides under conv1's compute.
+// conv1 (all 20 channels; recomputed by both co-tile blocks, it is 0.29 MFLOP vs conv2's 1.6) runs
+// on v_mfma_f32_32x32x2_f32 with the max-pool done on the accumulator registers.
+// conv2: wave w = (px-half w&1, K-half w>>1), 125 x v_mfma_f32_32x32x2_f32 on one accumulator
+// (dependent latency == issue interval), A = weights from LDS, B = im2col of conv1's LDS output.
+// Side jobs: block ct==0 stores P1/A1 (for backward) and the batch's row/label; the grid zeroes
+// the atomically-accumulated conv gradient bucket.
 // =================================================================================================
 template <int KK>
-__device__ __forceinline__ f32x16 conv2_mainloop(const float* __restrict__ wa, const float* xb) {
+__device__ __forceinline__ f32x16 conv2_mainloop(const float* wa, const float* xb) {
   f32x16 acc = {0.f};
 #pragma unroll
   for (int s = 0; s < 125; ++s) {
     const int S = KK * 125 + s;             // MFMA step; k' = 2S + (lane>>5)
     const int grp = S / 10, kh = grp / 5, kw = grp % 5, ci0 = (S % 10) * 2;
-    const float a = wa[(2 * S) * 64];
-    const float bv = xb[ci0 * 96 + kh * 12 + kw];
-    acc = mfma32x32x2(a, bv, acc);
+    acc = mfma32x32x2(wa[(2 * S) * 32], xb[ci0 * 144 + kh * 12 + kw], acc);
   }
   return acc;
 }
 
-__global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ P1, const float* __restrict__ Wt2,
-                                                   const float* __restrict__ bias, float* __restrict__ P2,
-                                                   uint8_t* __restrict__ A2) {
-  __shared__ __attribute__((aligned(16))) float xs[20 * 96];
-  __shared__ float red[2][64][33];
-  const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
-  const float* src = P1 + (size_t)b * kP1 + 48 * h;
-  for (int i = t; i < 20 * 96; i += 256) {
-    const int ci = i / 96, r = i - ci * 96;
-    xs[i] = src[ci * 144 + r];
+constexpr int kFwdWs = 500 * 32;           // staged weight slice (floats)
+constexpr int kFwdLds = kFwdWs + kP1 + kImg + 528;
+
+__global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, BatchSrc src,
+                                                  const long long* __restrict__ labels_all,
+                                                  const float* __restrict__ w1, const float* __restrict__ b1,
+                                                  const float* __restrict__ Wt2, const float* __restrict__ b2,
+                                                  float* __restrict__ P1, uint8_t* __restrict__ A1,
+                                                  float* __restrict__ P2, uint8_t* __restrict__ A2,
+                                                  int* __restrict__ cur_row, long long* __restrict__ cur_lbl,
+                                                  float* __restrict__ zero_ptr, int zero_n, int dbg) {
+  // dbg (ablation only): 1 skip conv1 compute, 2 skip conv2 MFMA, 4 skip weight-slice staging
+  __shared__ __attribute__((aligned(16))) float smem[kFwdLds];
+  float* ws = smem;                        // [500 k'][32 co]
+  float* xs = smem + kFwdWs;               // conv1 output [20][144]
+  float* xin = xs + kP1;                   // input image [784]
+  float* w1s = xin + kImg;                 // conv1 weight [500] + bias [20] (+pad)
+  const int b = blockIdx.x, ct = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
+  if (zero_ptr) {
+    const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
+    for (int i = bid * 256 + t; i < zero_n; i += nb * 256) zero_ptr[i] = 0.f;
+  }
+  const int row = sample_row(src, b);
+  // ---- phase 0: issue every global load (image + conv1 weights first, then the weight slice) ----
+  const float4 xv = reinterpret_cast<const float4*>(X + (size_t)row * kImg)[min(t, kImg / 4 - 1)];
+  const float4 wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
+  const float bv1 = b1[min(t, 19)];
+  float4 tmp[16];
+  {
+    const float4* wsrc = reinterpret_cast<const float4*>(Wt2) + ct * 8;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = (dbg & 4) ? t : min(t + 256 * i, 3999);   // 4000 float4: row e>>3, column chunk e&7
+      tmp[i] = wsrc[(e >> 3) * 16 + (e & 7)];
+    }
+  }
+  if (t < kImg / 4) reinterpret_cast<float4*>(xin)[t] = xv;
+  if (t < 125) reinterpret_cast<float4*>(w1s)[t] = wv;
+  if (t < 20) w1s[500 + t] = bv1;
+  if (ct == 0 && t == 0) {
+    if (cur_row) cur_row[b] = row;
+    if (cur_lbl && labels_all) cur_lbl[b] = labels_all[row];
   }
   __syncthreads();
-  const int ct = w & 1, kk = w >> 1, khalf = l >> 5, px = l & 31;
-  const float* xb = xs + khalf * 96 + (px >> 3) * 12 + (px & 7);
-  const float* wa = Wt2 + khalf * 64 + ct * 32 + (l & 31);
-  f32x16 acc = kk == 0 ? conv2_mainloop<0>(wa, xb) : conv2_mainloop<1>(wa, xb);
+  // ---- phase 1: conv1 on v_mfma_f32_32x32x2_f32 + bias + relu + maxpool ----
+  // C[m][ch] = sum_tap im2col[m][tap] * W1[ch][tap] with m = 4 * pooled_pos + sub (sub = dy*2+dx):
+  // rows (r&3) of the accumulator are the 4 sub-positions of one pooled position, so the 2x2 max
+  // pool (first maximum in scan order wins, as ATen) happens in registers.  576 = 18 tiles of 32.
+  if (!(dbg & 1)) {
+    const int ch = l & 31, hi = l >> 5;
+    const float chm = ch < 20 ? 1.f : 0.f;
+    float wb[13];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[kk][ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf][px] = acc[r];
-  __syncthreads();
-  for (int o = t; o < 400; o += 256) {
-    const int co = o >> 3, ph = (o >> 2) & 1, pw = o & 3;
-    const float bv = bias[co];
-    float best = -1.f; int code = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = (2 * ph + (q >> 1)) * 8 + 2 * pw + (q & 1);
-      const float v = fmaxf(red[0][co][p] + red[1][co][p] + bv, 0.f);
-      if (v > best) { best = v; code = q; }
+    for (int s2 = 0; s2 < 13; ++s2) {
+      const int tap = 2 * s2 + hi;
+      wb[s2] = (tap < 25) ? w1s[min(ch, 19) * 25 + min(tap, 24)] * chm : 0.f;
     }
-    const size_t oi = (size_t)b * kFeat + co * 16 + (2 * h + ph) * 4 + pw;
-    P2[oi] = best;
-    A2[oi] = (uint8_t)code;
+    const float bch = w1s[500 + min(ch, 19)];
+    for (int tile = w; tile < 18; tile += 4) {
+      const int m = tile * 32 + ch, pp = m >> 2, sub = m & 3;
+      const float* xa = xin + (2 * (pp / 12) + (sub >> 1)) * 28 + 2 * (pp % 12) + (sub & 1);
+      f32x16 acc = {0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 13; ++s2) {
+        const int t0 = 2 * s2, t1 = min(2 * s2 + 1, 24);
+        const int off = hi ? (t1 / 5) * 28 + t1 % 5 : (t0 / 5) * 28 + t0 % 5;
+        acc = mfma32x32x2(xa[off], wb[s2], acc);
+      }
+      if (ch < 20) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int pq = tile * 8 + 2 * g + hi;          // pooled position of registers 4g..4g+3
+          float best = fmaxf(acc[4 * g] + bch, 0.f);
+          int code = 0;
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float v = fmaxf(acc[4 * g + q] + bch, 0.f);
+            if (v > best) { best = v; code = q; }
+          }
+          xs[ch * 144 + pq] = best;
+          if (ct == 0) {
+            const size_t o = (size_t)b * kP1 + ch * 144 + pq;
+            P1[o] = best;
+            A1[o] = (uint8_t)code;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (t + 256 * i < 4000) reinterpret_cast<float4*>(ws)[t + 256 * i] = tmp[i];
+  __syncthreads();
+  // ---- phase 2: conv2 implicit GEMM ----
+  const int ph2 = w & 1, kk = w >> 1, khalf = l >> 5, pl = l & 31;
+  const float* xb = xs + khalf * 144 + (ph2 * 4 + (pl >> 3)) * 12 + (pl & 7);
+  const float* wa = ws + khalf * 32 + pl;
+  f32x16 acc = {0.f};
+  if (!(dbg & 2)) acc = kk == 0 ? conv2_mainloop<0>(wa, xb) : conv2_mainloop<1>(wa, xb);
+  else acc[0] = wa[0] + xb[0];
+  __syncthreads();                         // ws is reused as the reduction buffer below
+  float* red = smem;                       // [2][32][65]
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    red[(kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 65 + ph2 * 32 + pl] = acc[r];
+  __syncthreads();
+  const int nco = ct == 0 ? 32 : 18;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int o = t + 256 * r;
+    if (o < nco * 16) {
+      const int cl = o >> 4, ph = (o >> 2) & 3, pw = o & 3, co = ct * 32 + cl;
+      const float bv = b2[co];
+      float best = -1.f; int code = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = (2 * ph + (q >> 1)) * 8 + 2 * pw + (q & 1);
+        const float v = fmaxf(red[cl * 65 + p] + red[(32 + cl) * 65 + p] + bv, 0.f);
+        if (v > best) { best = v; code = q; }
+      }
+      const size_t oi = (size_t)b * kFeat + co * 16 + ph * 4 + pw;
+      P2[oi] = best;
+      A2[oi] = (uint8_t)code;
+    }
   }
 }
 
 // =================================================================================================
-// F3: H1 = relu(P2 @ W1^T + b1).  grid (32 n-tiles, ceil(B/16) m-tiles), block 256 (4 waves split K).
+// F2: H1 = relu(P2 @ W1^T + b1).  grid (32 n-tiles, ceil(B/16) m-tiles), block 256 (4 waves split K).
 // Lane-contiguous K: each lane loads 4 consecutive k of its A row and of its B column (W1 row) as
-// one float4; MFMA j uses element j.  Two accumulators hide the 40-cycle dependent latency.
+// one float4; MFMA j uses element j.  The 13 K-chunks of a wave are fully unrolled so all 26
+// 16-B loads are in flight before the first MFMA.  Block (0,0) also advances the engine's device
+// counters (optimizer step, batch position): F1 of this step has already consumed them and the
+// fused Adam that follows reads the new optimizer step.
 // =================================================================================================
 __global__ __launch_bounds__(256) void k_fc1_fwd(const float* __restrict__ P2, int B, const float* __restrict__ W,
-                                                 const float* __restrict__ bias, float* __restrict__ H1) {
+                                                 const float* __restrict__ bias, float* __restrict__ H1,
+                                                 long long* __restrict__ ctr, int nctr) {
   __shared__ float red[4][16][17];
   const int nt = blockIdx.x, mt = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
+  if (ctr && nt == 0 && mt == 0 && t == 0)
+    for (int c = 0; c < nctr; ++c) ctr[c] += 1;
   const int row = mt * 16 + (l & 15), n = nt * 16 + (l & 15), kg = l >> 4;
   const float am = row < B ? 1.f : 0.f, bm = n < kHid ? 1.f : 0.f;
   const float4* ap = reinterpret_cast<const float4*>(P2 + (size_t)min(row, B - 1) * kFeat + kg * 4);
   const float4* bp = reinterpret_cast<const float4*>(W + (size_t)min(n, kHid - 1) * kFeat + kg * 4);
+  float4 a[13], bb[13];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int c = min(w + 4 * i, kFeat / 16 - 1);
+    a[i] = ap[c * 4];
+    bb[i] = bp[c * 4];
+  }
+  const float bvv = bias[min(n, kHid - 1)];
   f32x4 acc0 = {0.f}, acc1 = {0.f};
-  for (int c = w; c < kFeat / 16; c += 4) {
-    const float4 a = ap[c * 4], bb = bp[c * 4];
-    acc0 = mfma16x16x4(a.x * am, bb.x * bm, acc0);
-    acc1 = mfma16x16x4(a.y * am, bb.y * bm, acc1);
-    acc0 = mfma16x16x4(a.z * am, bb.z * bm, acc0);
-    acc1 = mfma16x16x4(a.w * am, bb.w * bm, acc1);
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const float km = (w + 4 * i < kFeat / 16) ? am : 0.f;
+    acc0 = mfma16x16x4(a[i].x * km, bb[i].x * bm, acc0);
+    acc1 = mfma16x16x4(a[i].y * km, bb[i].y * bm, acc1);
+    acc0 = mfma16x16x4(a[i].z * km, bb[i].z * bm, acc0);
+    acc1 = mfma16x16x4(a[i].w * km, bb[i].w * bm, acc1);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[w][(l >> 4) * 4 + r][l & 15] = acc0[r] + acc1[r];
   __syncthreads();
-  const int i = t >> 4, j = t & 15, gm = mt * 16 + i, gn = nt * 16 + j;
-  if (gm < B && gn < kHid) {
-    const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j] + bias[gn];
-    H1[(size_t)gm * kHid + gn] = fmaxf(v, 0.f);
+  if (w == 0) {
+    // C layout: lane (l&15) owns column n, rows (l>>4)*4 + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = (l >> 4) * 4 + r, j = l & 15, gm = mt * 16 + i;
+      if (gm < B && n < kHid) {
+        const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j] + bvv;
+        H1[(size_t)gm * kHid + n] = fmaxf(v, 0.f);
+      }
+    }
   }
 }
 
 // =================================================================================================
-// F4: fc2 + log_softmax + cross_entropy + backward to dZ1.  grid ceil(B/4), block 256: wave = row.
+// F3: fc2 + log_softmax + cross_entropy + backward to dZ1.  grid ceil(B/4), block 256: wave = row.
 // The reference computes F.cross_entropy(F.log_softmax(z)) (main.py:89,147): the loss applies a
 // second log_softmax to the log-probs.  We evaluate exactly that chain, and its gradient
 //   dlogp = (softmax(logp) - onehot)/B ; dz = dlogp - exp(logp) * sum(dlogp)
 // then dH1 = dz @ W2, dZ1 = dH1 * (H1 > 0).
-// Modes: dZ1 == nullptr -> forward/eval only (loss + accuracy meters, optional logp output).
+// Lane l owns hidden units n = l + 64 j (j < 8): every load/store instruction is 256 contiguous B.
+// Meters: per-row loss / hit written to row_loss/row_hit (summed later by one thread of B1, no
+// same-address atomics in the hot path); if those are null and loss_sum is given (eval), one
+// atomic per block after an LDS reduction.
+// Modes: dZ1 == nullptr -> forward/eval only.
 // =================================================================================================
 __global__ __launch_bounds__(256) void k_head(const float* __restrict__ H1, int B, const float* __restrict__ W2,
                                               const float* __restrict__ b2, const long long* __restrict__ labels,
                                               float inv_b, float* __restrict__ logp_out, float* __restrict__ dZ2,
-                                              float* __restrict__ dZ1, double* __restrict__ loss_sum,
+                                              float* __restrict__ dZ1, float* __restrict__ row_loss,
+                                              int* __restrict__ row_hit, double* __restrict__ loss_sum,
                                               unsigned long long* __restrict__ correct) {
-  const int t = threadIdx.x, l = t & 63, row = blockIdx.x * 4 + (t >> 6);
-  if (row >= B) return;
-  const int n0 = l * 8;
-  float h[8];
-  {
-    const float4* hp = reinterpret_cast<const float4*>(H1 + (size_t)row * kHid + min(n0, kHid - 4));
-    float4 u = hp[0], v = n0 + 4 < kHid ? hp[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool ok = n0 < kHid;
-    h[0] = ok ? u.x : 0.f; h[1] = ok ? u.y : 0.f; h[2] = ok ? u.z : 0.f; h[3] = ok ? u.w : 0.f;
-    h[4] = v.x; h[5] = v.y; h[6] = v.z; h[7] = v.w;
+  __shared__ float sl[4];
+  __shared__ int sh[4];
+  const int t = threadIdx.x, l = t & 63, wv = t >> 6, row = blockIdx.x * 4 + wv;
+  const bool live = row < B;
+  const int rc = min(row, B - 1);
+  float h[8], w2[kCls][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = min(l + 64 * j, kHid - 1);
+    h[j] = H1[(size_t)rc * kHid + n];
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) w2[c][j] = W2[c * kHid + n];
   }
+  const int y = (int)labels[rc];
+  float bias[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) bias[c] = b2[c];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (l + 64 * j < kHid) ? h[j] : 0.f;
   float z[kCls];
 #pragma unroll
   for (int c = 0; c < kCls; ++c) {
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + j;
-      s = fmaf(h[j], n < kHid ? W2[c * kHid + n] : 0.f, s);
-    }
-    z[c] = wave_sum(s) + b2[c];
+    for (int j = 0; j < 8; ++j) s = fmaf(h[j], w2[c][j], s);
+    z[c] = s;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) z[c] += __shfl_xor(z[c], o, 64);
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) z[c] += bias[c];
   // model output: log_softmax(z)
   float m = z[0];
 #pragma unroll
@@ -249,14 +327,22 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ H1, int 
 #pragma unroll
   for (int c = 0; c < kCls; ++c) se2 += expf(lp[c] - m2);
   const float lse2 = logf(se2);
-  const int y = (int)labels[row];
   float lpy = 0.f;
 #pragma unroll
   for (int c = 0; c < kCls; ++c) lpy = (c == y) ? lp[c] - m2 - lse2 : lpy;
-  if (l == 0) {
-    if (loss_sum) atomicAdd(loss_sum, (double)(-lpy));
-    if (correct && pred == y) atomicAdd(correct, 1ULL);
+  const float loss = -lpy;
+  const int hit = pred == y ? 1 : 0;
+  if (row_loss) {
+    if (live && l == 0) { row_loss[row] = loss; row_hit[row] = hit; }
+  } else if (loss_sum) {
+    if (l == 0) { sl[wv] = live ? loss : 0.f; sh[wv] = live ? hit : 0; }
+    __syncthreads();
+    if (t == 0) {
+      atomicAdd(loss_sum, (double)(sl[0] + sl[1] + sl[2] + sl[3]));
+      atomicAdd(correct, (unsigned long long)(sh[0] + sh[1] + sh[2] + sh[3]));
+    }
   }
+  if (!live) return;
   if (logp_out && l < kCls) {
     float v = 0.f;
 #pragma unroll
@@ -279,23 +365,17 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ H1, int 
     for (int c = 0; c < kCls; ++c) v = (c == l) ? dz[c] : v;
     dZ2[(size_t)row * kCls + l] = v;
   }
-  float o[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int n = min(n0 + j, kHid - 1);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < kCls; ++c) s = fmaf(dz[c], W2[c * kHid + n], s);
-    o[j] = h[j] > 0.f ? s : 0.f;
-  }
-  if (n0 < kHid) {
-    float4* dp = reinterpret_cast<float4*>(dZ1 + (size_t)row * kHid + n0);
-    dp[0] = make_float4(o[0], o[1], o[2], o[3]);
-    if (n0 + 4 < kHid) dp[1] = make_float4(o[4], o[5], o[6], o[7]);
+    for (int c = 0; c < kCls; ++c) s = fmaf(dz[c], w2[c][j], s);
+    const int n = l + 64 * j;
+    if (n < kHid) dZ1[(size_t)row * kHid + n] = h[j] > 0.f ? s : 0.f;
   }
 }
 
-// F4b (autograd path): backward of log_softmax + fc2 + ReLU from an arbitrary upstream gradient
+// F3b (autograd path): backward of log_softmax + fc2 + ReLU from an arbitrary upstream gradient
 // g = dL/dlogp (any loss placed after the model):  dz = g - exp(logp) * sum(g); dZ2 = dz;
 // dZ1 = (dz @ W2) * (H1 > 0).  grid ceil(B/4), block 256, wave = row.
 __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ H1, int B, const float* __restrict__ W2,
@@ -303,275 +383,442 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ H1, 
                                                   float* __restrict__ dZ2, float* __restrict__ dZ1) {
   const int t = threadIdx.x, l = t & 63, row = blockIdx.x * 4 + (t >> 6);
   if (row >= B) return;
+  float gg[kCls], lpv[kCls], w2[kCls][8], h[8];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) { gg[c] = g[(size_t)row * kCls + c]; lpv[c] = logp[(size_t)row * kCls + c]; }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = min(l + 64 * j, kHid - 1);
+    h[j] = H1[(size_t)row * kHid + n];
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) w2[c][j] = W2[c * kHid + n];
+  }
   float dz[kCls], sg = 0.f;
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) sg += g[(size_t)row * kCls + c];
+  for (int c = 0; c < kCls; ++c) sg += gg[c];
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) dz[c] = g[(size_t)row * kCls + c] - expf(logp[(size_t)row * kCls + c]) * sg;
+  for (int c = 0; c < kCls; ++c) dz[c] = gg[c] - expf(lpv[c]) * sg;
   if (l < kCls) {
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < kCls; ++c) v = (c == l) ? dz[c] : v;
     dZ2[(size_t)row * kCls + l] = v;
   }
-  const int n0 = l * 8;
-  if (n0 >= kHid) return;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int n = n0 + j;
-    if (n < kHid) {
-      float s = 0.f;
+    float s = 0.f;
 #pragma unroll
-      for (int c = 0; c < kCls; ++c) s = fmaf(dz[c], W2[c * kHid + n], s);
-      dZ1[(size_t)row * kHid + n] = H1[(size_t)row * kHid + n] > 0.f ? s : 0.f;
-    }
+    for (int c = 0; c < kCls; ++c) s = fmaf(dz[c], w2[c][j], s);
+    const int n = l + 64 * j;
+    if (n < kHid) dZ1[(size_t)row * kHid + n] = h[j] > 0.f ? s : 0.f;
   }
 }
 
+// Block-wide sum of one float per thread (256 threads); every thread gets the result.
+__device__ __forceinline__ float block_sum256(float v, float* scratch) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+  __syncthreads();
+  return r;
+}
+
 // =================================================================================================
-// B1: fc backward, three block roles in one launch.
-//   role C [0, nC)        : dP2m = (dZ1 @ W1) * (P2 > 0)      16x16 tiles, split-K 4 waves
-//   role A [nC, nC+nA)    : dW1 = dZ1^T @ P2                  16x16 tile per wave, K = B
-//   role B [.., +8)       : dW2 = dZ2^T @ H1, db1 = sum dZ1, db2 = sum dZ2   (VALU)
+// B1: fc backward, three block roles in one launch (all loads of a wave issued before its MFMAs).
+//   role C [0, nC)       : dP2m = (dZ1 @ W1) * (P2 > 0)      16x16 tiles, split-K over 4 waves
+//   role A [nC, nC+416)  : [dW1 | db1] = dZ1^T @ [P2 | 1]      16x16 tile per wave, K = B; n-tile 50
+//                          is the bias tile (B operand = ones column), so db1 costs one MFMA chain
+//   role B [.., +8)      : [dW2 | db2] = dZ2^T @ [H1 | 1]      (column 500 of H1 taken as ones)
+//                          block 0 also folds F3's per-row loss/hit into the meters (single writer)
 // =================================================================================================
+constexpr int kBChunk = 128;   // batch rows per unrolled load batch (role A / B)
+
 __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, const float* __restrict__ H1,
                                                 const float* __restrict__ dZ1, const float* __restrict__ dZ2,
                                                 const float* __restrict__ W1, int B, float* __restrict__ dP2m,
                                                 float* __restrict__ gW1, float* __restrict__ gb1,
-                                                float* __restrict__ gW2, float* __restrict__ gb2) {
+                                                float* __restrict__ gW2, float* __restrict__ gb2,
+                                                const float* __restrict__ row_loss, const int* __restrict__ row_hit,
+                                                double* __restrict__ loss_sum, unsigned long long* __restrict__ correct,
+                                                int dbg) {
+  // dbg (ablation only): 1 skip role C, 2 skip role A, 4 skip role B
   __shared__ float red[4][16][17];
-  __shared__ float redB[4][11][64];
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  __shared__ float scratch[4];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, kg = l >> 4;
   const int mtiles = (B + 15) / 16;
   const int nC = mtiles * 50, nA = 32 * 13;
   int bid = blockIdx.x;
   if (bid < nC) {
-    // ---- role C: dP2 tile (mt, nt) over K = 500 (hidden) ----
+    if (dbg & 1) return;
+    // ---- role C: dP2 tile (mt, nt) over K = 500 (hidden); wave w takes K-chunks w, w+4, ... ----
     const int mt = bid / 50, nt = bid % 50;
-    const int row = mt * 16 + (l & 15), n = nt * 16 + (l & 15), kg = l >> 4;
+    const int row = mt * 16 + (l & 15), n = nt * 16 + (l & 15);
     const float am = row < B ? 1.f : 0.f;
-    const float* ap = dZ1 + (size_t)min(row, B - 1) * kHid + kg * 4;
+    const float* arow = dZ1 + (size_t)min(row, B - 1) * kHid;
+    float4 a[8];
+    float bv[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k0 = (w + 4 * i) * 16 + kg * 4, kc = min(k0, kHid - 4);
+      a[i] = *reinterpret_cast<const float4*>(arow + kc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[i][j] = W1[(size_t)(kc + j) * kFeat + n];
+    }
+    const float pm = P2[(size_t)min(mt * 16 + (t >> 4), B - 1) * kFeat + nt * 16 + (t & 15)];
     f32x4 acc0 = {0.f}, acc1 = {0.f};
-    for (int c = w; c < 32; c += 4) {        // chunk c: k in [16c, 16c+16), k < 500
-      const int k0 = c * 16 + kg * 4;
-      float4 a = k0 < kHid ? *reinterpret_cast<const float4*>(ap + c * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float* bcol = W1 + (size_t)min(k0, kHid - 4) * kFeat + n;
-      const float km = k0 < kHid ? 1.f : 0.f;
-      acc0 = mfma16x16x4(a.x * am, bcol[0] * km, acc0);
-      acc1 = mfma16x16x4(a.y * am, bcol[kFeat] * km, acc1);
-      acc0 = mfma16x16x4(a.z * am, bcol[2 * kFeat] * km, acc0);
-      acc1 = mfma16x16x4(a.w * am, bcol[3 * kFeat] * km, acc1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float km = ((w + 4 * i) * 16 + kg * 4 < kHid) ? am : 0.f;
+      acc0 = mfma16x16x4(a[i].x * km, bv[i][0], acc0);
+      acc1 = mfma16x16x4(a[i].y * km, bv[i][1], acc1);
+      acc0 = mfma16x16x4(a[i].z * km, bv[i][2], acc0);
+      acc1 = mfma16x16x4(a[i].w * km, bv[i][3], acc1);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][(l >> 4) * 4 + r][l & 15] = acc0[r] + acc1[r];
     __syncthreads();
     const int i = t >> 4, j = t & 15, gm = mt * 16 + i, gn = nt * 16 + j;
     if (gm < B) {
-      const size_t o = (size_t)gm * kFeat + gn;
       const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j];
-      dP2m[o] = P2[o] > 0.f ? v : 0.f;
+      dP2m[(size_t)gm * kFeat + gn] = pm > 0.f ? v : 0.f;
     }
     return;
   }
   bid -= nC;
   if (bid < nA) {
-    // ---- role A: dW1 tile (mt over 500, nt over 800), K = batch ----
+    if (dbg & 2) return;
+    // ---- role A: [dW1|db1] tile (mt over 500, nt over 800 + bias tile 50), K = batch ----
     const int mt = bid / 13, nt = (bid % 13) * 4 + w;
-    if (nt >= 50) return;
-    const int m = mt * 16 + (l & 15), n = nt * 16 + (l & 15), kg = l >> 4;
-    const int mc = min(m, kHid - 1);
+    if (nt > 50) return;
+    const int m = mt * 16 + (l & 15), n = nt * 16 + (l & 15);
+    const int mc = min(m, kHid - 1), nc = min(n, kFeat - 1);
     const float mm = m < kHid ? 1.f : 0.f;
+    const bool bias_tile = nt == 50;                  // wave-uniform
+    const float ones = (n == kFeat) ? 1.f : 0.f;
     f32x4 acc0 = {0.f}, acc1 = {0.f};
-    int b0 = 0;
-    for (; b0 + 8 <= B; b0 += 8) {
-      const int r0 = b0 + kg, r1 = b0 + 4 + kg;
-      acc0 = mfma16x16x4(dZ1[(size_t)r0 * kHid + mc] * mm, P2[(size_t)r0 * kFeat + n], acc0);
-      acc1 = mfma16x16x4(dZ1[(size_t)r1 * kHid + mc] * mm, P2[(size_t)r1 * kFeat + n], acc1);
-    }
-    for (; b0 < B; b0 += 4) {
-      const int r = b0 + kg;
-      const float km = r < B ? mm : 0.f;
-      const int rc = min(r, B - 1);
-      acc0 = mfma16x16x4(dZ1[(size_t)rc * kHid + mc] * km, P2[(size_t)rc * kFeat + n], acc0);
+    for (int b0 = 0; b0 < B; b0 += kBChunk) {
+      float av[kBChunk / 4], bvv[kBChunk / 4];
+#pragma unroll
+      for (int i = 0; i < kBChunk / 4; ++i) {
+        const int r = b0 + 4 * i + kg, rc = min(r, B - 1);
+        av[i] = dZ1[(size_t)rc * kHid + mc] * (r < B ? mm : 0.f);
+      }
+      if (!bias_tile) {
+#pragma unroll
+        for (int i = 0; i < kBChunk / 4; ++i) {
+          const int rc = min(b0 + 4 * i + kg, B - 1);
+          bvv[i] = P2[(size_t)rc * kFeat + nc];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kBChunk / 4; ++i) bvv[i] = ones;
+      }
+#pragma unroll
+      for (int i = 0; i < kBChunk / 4; i += 2) {
+        acc0 = mfma16x16x4(av[i], bvv[i], acc0);
+        acc1 = mfma16x16x4(av[i + 1], bvv[i + 1], acc1);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gm = mt * 16 + (l >> 4) * 4 + r;
-      if (gm < kHid) gW1[(size_t)gm * kFeat + n] = acc0[r] + acc1[r];
+      const float v = acc0[r] + acc1[r];
+      if (gm < kHid) {
+        if (!bias_tile) gW1[(size_t)gm * kFeat + n] = v;
+        else if (n == kFeat) gb1[gm] = v;
+      }
     }
     return;
   }
   bid -= nA;
-  // ---- role B: columns n = bid*64 + lane ----
-  const int n = bid * 64 + l, nc = min(n, kHid - 1);
-  float acc[11];
+  if (dbg & 4) return;
+  // ---- role B: [dW2|db2] tile nt (columns 16nt..16nt+15 over 500 + ones column 500), K = batch ----
+  {
+    const int nt = bid * 4 + w;                        // 0..31
+    const int n = nt * 16 + (l & 15), nc = min(n, kHid - 1);
+    const int c = l & 15, cc = min(c, kCls - 1);
+    const float cm = c < kCls ? 1.f : 0.f;
+    const float hm = n < kHid ? 1.f : 0.f, ones = n == kHid ? 1.f : 0.f;
+    f32x4 acc0 = {0.f}, acc1 = {0.f};
+    for (int b0 = 0; b0 < B; b0 += kBChunk) {
+      float av[kBChunk / 4], bvv[kBChunk / 4];
 #pragma unroll
-  for (int c = 0; c < 11; ++c) acc[c] = 0.f;
-  for (int b = w; b < B; b += 4) {
-    const float hv = H1[(size_t)b * kHid + nc];
+      for (int i = 0; i < kBChunk / 4; ++i) {
+        const int r = b0 + 4 * i + kg, rc = min(r, B - 1);
+        av[i] = dZ2[(size_t)rc * kCls + cc] * (r < B ? cm : 0.f);
+        bvv[i] = H1[(size_t)rc * kHid + nc] * hm + ones;
+      }
 #pragma unroll
-    for (int c = 0; c < kCls; ++c) acc[c] = fmaf(dZ2[b * kCls + c], hv, acc[c]);
-    acc[10] += dZ1[(size_t)b * kHid + nc];
+      for (int i = 0; i < kBChunk / 4; i += 2) {
+        acc0 = mfma16x16x4(av[i], bvv[i], acc0);
+        acc1 = mfma16x16x4(av[i + 1], bvv[i + 1], acc1);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ci = (l >> 4) * 4 + r;
+      const float v = acc0[r] + acc1[r];
+      if (ci < kCls) {
+        if (n < kHid) gW2[ci * kHid + n] = v;
+        else if (n == kHid) gb2[ci] = v;
+      }
+    }
   }
-#pragma unroll
-  for (int c = 0; c < 11; ++c) redB[w][c][l] = acc[c];
-  __syncthreads();
-  if (w == 0 && n < kHid) {
-#pragma unroll
-    for (int c = 0; c < kCls; ++c)
-      gW2[c * kHid + n] = redB[0][c][l] + redB[1][c][l] + redB[2][c][l] + redB[3][c][l];
-    gb1[n] = redB[0][10][l] + redB[1][10][l] + redB[2][10][l] + redB[3][10][l];
-  }
-  if (bid == 0 && t < kCls) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dZ2[b * kCls + t];
-    gb2[t] = s;
-  }
-}
-
-// Expand the pooled/masked gradient dP2m[b] (+ argmax codes) into dY2 [co][px] in LDS (stride 65).
-__device__ __forceinline__ void expand_dy2(float* dys, const float* __restrict__ dP2m, const uint8_t* __restrict__ A2,
-                                           int b, int t, int nthreads) {
-  const float* g = dP2m + (size_t)b * kFeat;
-  const uint8_t* a = A2 + (size_t)b * kFeat;
-  for (int i = t; i < 50 * 64; i += nthreads) {
-    const int co = i >> 6, px = i & 63, oh = px >> 3, ow = px & 7;
-    const int q = co * 16 + (oh >> 1) * 4 + (ow >> 1);
-    const int code = (oh & 1) * 2 + (ow & 1);
-    dys[co * 65 + px] = (a[q] == code) ? g[q] : 0.f;
+  if (bid == 0 && row_loss && loss_sum) {
+    float ls = 0.f, hs = 0.f;
+    for (int r = t; r < B; r += 256) { ls += row_loss[r]; hs += (float)row_hit[r]; }
+    const float tl = block_sum256(ls, scratch);
+    const float th = block_sum256(hs, scratch);
+    if (t == 0) {
+      loss_sum[0] += (double)tl;
+      correct[0] += (unsigned long long)(th + 0.5f);
+    }
   }
 }
 
 // =================================================================================================
-// B2: conv backward, two block roles in one launch.
-//   role W [0, nW)        : conv2 wgrad.  block = (group of 4 images, 4 of the 32 tiles of the
-//                           [co 64][k 512] output); wave = one 32x32 tile, K = 64 px per image on
-//                           v_mfma_f32_32x32x2_f32; partial sums atomically added to gW2c.
-//   role D [nW, nW + 4B)  : block = (image, group of 5 input channels).  conv2 dgrad as the GEMM
-//                           T[k][px] = sum_co W[co][k] dY2[co][px] (k restricted to the group's 125
-//                           taps), col2im scatter-add into LDS, then maxpool1 + ReLU backward and
-//                           conv1 wgrad/bgrad on the 1-of-4 nonzero positions; plus conv2 bias grad.
+// B2: conv backward, two block roles in one launch, 512 threads (8 waves) per block.
+//   role W [0, nW)       : conv2 wgrad + bias grad.  block = (group of 8 images, 32 k-columns);
+//                          wave = (co-tile of 16, k-tile of 16) on v_mfma_f32_16x16x4_f32, K = 8 x 64 px.
+//                          The A operand dY2[co][px] is produced on the fly from the pooled gradient and
+//                          the argmax codes (no expanded tile), B is the im2col of the P1 slice of the
+//                          block's <= 3 input channels; column k = 500 of B is all ones so that column
+//                          of the product is the conv2 bias gradient.  Partials are atomically added:
+//                          16 adders per address (an earlier 2-image version with 64 adders spent 18 us
+//                          in atomics alone, tools/kbench_lenet.py).
+//   role D [nW, nW + 4B) : block = (image, group of 5 input channels).
+//                          (1) conv2 dgrad T[k][px] = sum_co W[co][k] dY2[co][px] (the group's 125 taps)
+//                              on v_mfma_f32_32x32x2_f32, stored to LDS with plain stores;
+//                          (2) col2im as a gather (each dP1 element sums its <= 25 taps: no LDS atomics,
+//                              which cost 19 us in the scatter-add version), maxpool1 + ReLU mask;
+//                          (3) conv1 wgrad|bgrad = dY1[c][576 px] @ [im2col(X) | 1] on
+//                              v_mfma_f32_16x16x4_f32 over 4 K-quarters, one atomic per output.
 // =================================================================================================
-constexpr int kWImgs = 4;
+constexpr int kWImgs = 8;                      // images per role-W block
+constexpr int kWImgStride = kFeat + 200 + 432; // g800 | codes (800 B) | P1 slice (3 ch x 144)
+constexpr int kDysS = 3264;                    // role D carve: dys [50][65] (later dY1 [5][576])
+constexpr int kTS = 128 * 65;                  // T [128 k][65]
+constexpr int kBwdLds = kDysS + kTS + 720 + kImg + kFeat + 200 + 720 + 180;
 
-__global__ __launch_bounds__(256) void k_conv_bwd(const float* __restrict__ X, const int* __restrict__ rows,
+__global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, const int* __restrict__ rows,
                                                   const float* __restrict__ P1, const uint8_t* __restrict__ A1,
                                                   const float* __restrict__ dP2m, const uint8_t* __restrict__ A2,
                                                   const float* __restrict__ W2c, int B,
                                                   float* __restrict__ gW1c, float* __restrict__ gb1c,
-                                                  float* __restrict__ gW2c, float* __restrict__ gb2c) {
-  __shared__ __attribute__((aligned(16))) float smem[64 * 65 + kP1 + 16];
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int nIG = (B + kWImgs - 1) / kWImgs, nW = nIG * 8;
+                                                  float* __restrict__ gW2c, float* __restrict__ gb2c,
+                                                  int c1_nrep, int c1_rep_stride, int dbg) {
+  // conv1 grads go to replica (b % c1_nrep) at a stride of c1_rep_stride floats (the consumer folds
+  // the replicas): 128 images adding into 520 addresses was the single largest cost (17 us).
+  // dbg (ablation only; 0 in production): 1 skip role W, 2 skip role D, 4 no global atomics,
+  // 16 skip conv1 wgrad, 32 skip MFMA loops.  Skipped results stay live.
+  __shared__ __attribute__((aligned(16))) float smem[kBwdLds];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lg = l >> 4;
+  const int nIG = (B + kWImgs - 1) / kWImgs, nW = nIG * 16;
+  const float4* P1v = reinterpret_cast<const float4*>(P1);
+  const float4* Gv = reinterpret_cast<const float4*>(dP2m);
+  const uint4* Av = reinterpret_cast<const uint4*>(A2);
   int bid = blockIdx.x;
   if (bid < nW) {
-    float* dys = smem;                 // [64][65]
-    float* p1s = smem + 64 * 65;       // [20][144]
-    const int ig = bid >> 3, tg = bid & 7;
-    const int tile = tg * 4 + w, mt = tile >> 4, nt = tile & 15;
-    for (int i = 50 * 65 + t; i < 64 * 65; i += 256) dys[i] = 0.f;
-    const int kidx = nt * 32 + (l & 31);
-    const float kmask = kidx < 500 ? 1.f : 0.f;
-    const int kc = min(kidx, 499);
-    const int ci = kc / 25, rem = kc - ci * 25, kh = rem / 5, kw = rem - kh * 5;
-    const float* bsrc = p1s + ci * 144 + kh * 12 + kw + (l >> 5);
-    const float* asrc = dys + (mt * 32 + (l & 31)) * 65 + (l >> 5);
-    f32x16 acc = {0.f};
-    for (int ii = 0; ii < kWImgs; ++ii) {
-      const int b = ig * kWImgs + ii;
-      if (b >= B) break;
-      __syncthreads();
-      expand_dy2(dys, dP2m, A2, b, t, 256);
-      const float4* s4 = reinterpret_cast<const float4*>(P1 + (size_t)b * kP1);
-      for (int i = t; i < kP1 / 4; i += 256) reinterpret_cast<float4*>(p1s)[i] = s4[i];
-      __syncthreads();
+    if (dbg & 1) return;
+    const int ig = bid >> 4, kp = bid & 15;
+    const int ci_base = (32 * kp) / 25;
+    // ---- loads for the 8 images: pooled grad (200 float4), codes (50 uint4), P1 slice (108 float4) ----
+    // 358 16-B pieces per image, 2864 per block: 6 per thread, all issued before the first LDS store.
+    float4 v4[6];
 #pragma unroll
-      for (int s = 0; s < 32; ++s) {
-        const float av = asrc[2 * s];
-        const float bv = bsrc[(s >> 2) * 12 + 2 * (s & 3)] * kmask;
-        acc = mfma32x32x2(av, bv, acc);
+    for (int j = 0; j < 6; ++j) {
+      const int e = t + 512 * j;                  // piece id in [0, 8*358)
+      const int ii = min(e / 358, kWImgs - 1), pc = e - (e / 358) * 358;
+      const int b = min(ig * kWImgs + ii, B - 1);
+      const int q = max(pc - 250, 0), ch = min(ci_base + q / 36, 19);
+      // one unconditional 16-B load from a selected source (no branch around a load)
+      const float4* src = pc < 200 ? Gv + (size_t)b * 200 + pc
+                        : pc < 250 ? reinterpret_cast<const float4*>(Av + (size_t)b * 50 + (pc - 200))
+                                   : P1v + (size_t)b * 720 + ch * 36 + (q % 36);
+      v4[j] = *src;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int e = t + 512 * j;
+      if (e < kWImgs * 358) {
+        const int ii = e / 358, pc = e - ii * 358;
+        reinterpret_cast<float4*>(smem + ii * kWImgStride)[pc] = v4[j];
+      }
+    }
+    if (t < 160) smem[kWImgs * kWImgStride + t] = t < 80 ? 1.f : 0.f;   // B operand of the k >= 500 columns
+    __syncthreads();
+    const int ct = w & 3, kt = 2 * kp + (w >> 2);
+    const int co = ct * 16 + (l & 15), coc = min(co, 49);
+    const float com = co < 50 ? 1.f : 0.f;
+    const int kk = kt * 16 + (l & 15);
+    const int kc = min(kk, 499), ci = kc / 25, rem = kc - ci * 25, kh = rem / 5, kw = rem - kh * 5;
+    // Lane-contiguous pixels: in chunk c (output rows 2c, 2c+1) lane group lg owns row 2c+(lg>>1),
+    // columns 4(lg&1)+j, j<4 (MFMA j uses pixel j of the lane's run).  One 8-B read gives the two
+    // pooled gradients, one 2-B read their argmax codes, and the P1 reads are immediate offsets.
+    const int boff = (ci - ci_base) * 144 + (kh + (lg >> 1)) * 12 + kw + 4 * (lg & 1);
+    const float* cst = smem + kWImgs * kWImgStride + (kk == 500 ? 0 : 80);   // ones | zeros
+    f32x4 acc0 = {0.f}, acc1 = {0.f};
+    if (!(dbg & 32)) {
+      for (int ii = 0; ii < kWImgs; ++ii) {
+        const float* gi = smem + ii * kWImgStride;
+        const uint8_t* ci8 = reinterpret_cast<const uint8_t*>(gi + kFeat) + coc * 16 + 2 * (lg & 1);
+        const float* gq = gi + coc * 16 + 2 * (lg & 1);
+        const float* p1s = kk < 500 ? gi + kFeat + 200 + boff : cst;
+        const float bm = (ig * kWImgs + ii < B) ? com : 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float2 gg = *reinterpret_cast<const float2*>(gq + 4 * c);
+          const unsigned short cc = *reinterpret_cast<const unsigned short*>(ci8 + 4 * c);
+          const int c0 = cc & 0xff, c1 = cc >> 8, sb = (lg >> 1) * 2;
+          const float g0 = gg.x * bm, g1 = gg.y * bm;
+          acc0 = mfma16x16x4(c0 == sb ? g0 : 0.f, p1s[24 * c + 0], acc0);
+          acc1 = mfma16x16x4(c0 == sb + 1 ? g0 : 0.f, p1s[24 * c + 1], acc1);
+          acc0 = mfma16x16x4(c1 == sb ? g1 : 0.f, p1s[24 * c + 2], acc0);
+          acc1 = mfma16x16x4(c1 == sb + 1 ? g1 : 0.f, p1s[24 * c + 3], acc1);
+        }
       }
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      if (co < 50 && kidx < 500) atomicAdd(&gW2c[co * 500 + kidx], acc[r]);
+    for (int r = 0; r < 4; ++r) {
+      const int cor = ct * 16 + lg * 4 + r;
+      const float v = acc0[r] + acc1[r];
+      if (cor < 50 && (!(dbg & 4) || v == 1234.5f)) {
+        if (kk < 500) atomicAdd(&gW2c[cor * 500 + kk], v);
+        else if (kk == 500) atomicAdd(&gb2c[cor], v);
+      }
     }
     return;
   }
   bid -= nW;
+  if (dbg & 2) return;
   // ---- role D ----
   const int b = bid >> 2, cg = bid & 3;
   if (b >= B) return;
-  float* dys = smem;                   // [50][65] (region rounded to 3264 floats: 16-B aligned carve)
-  float* dp1 = smem + 3264;            // [5][144]
+  float* dys = smem;                   // [50][65]; later dY1 [5][576]
+  float* T = smem + kDysS;             // [128][65]
+  float* dp1 = T + kTS;                // [5][144]
   float* xs = dp1 + 720;               // [784]
-  uint8_t* cds = reinterpret_cast<uint8_t*>(xs + kImg);  // [720] codes
-  for (int i = t; i < 720; i += 256) dp1[i] = 0.f;
-  expand_dy2(dys, dP2m, A2, b, t, 256);
-  {
-    const float4* s4 = reinterpret_cast<const float4*>(X + (size_t)rows[b] * kImg);
-    for (int i = t; i < kImg / 4; i += 256) reinterpret_cast<float4*>(xs)[i] = s4[i];
-  }
-  if (cg == 0 && t < 50) {
-    const float* g = dP2m + (size_t)b * kFeat + t * 16;
-    float s = 0.f;
+  float* g800 = xs + kImg;             // [800]
+  uint8_t* a800 = reinterpret_cast<uint8_t*>(g800 + kFeat);   // [800]
+  float* p1m = g800 + kFeat + 200;     // [720] P1 values of the group's channels
+  uint8_t* cds = reinterpret_cast<uint8_t*>(p1m + 720);       // [720] A1 codes
+  // ---- loads: dgrad A operand (W2c), dP2m, A2, X row, P1 / A1 of the channel group ----
+  const int dmt = w >> 1, dpt = w & 1;                        // dgrad tile: k-tile, px-tile
+  const int kl = dmt * 32 + (l & 31);
+  const float km = kl < 125 ? 1.f : 0.f;
+  const float* wa = W2c + (l >> 5) * 500 + cg * 125 + min(kl, 124);
+  float av[25];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) s += g[p];
-    atomicAdd(&gb2c[t], s);
+  for (int s = 0; s < 25; ++s) av[s] = wa[2 * s * 500];
+  const float4 gv = Gv[(size_t)b * 200 + min(t, 199)];
+  const uint4 a2v = Av[(size_t)b * 50 + min(t, 49)];
+  const float4 xv = reinterpret_cast<const float4*>(X + (size_t)rows[b] * kImg)[min(t, kImg / 4 - 1)];
+  const float4 pv = P1v[(size_t)b * 720 + cg * 180 + min(t, 179)];
+  const uint4 cv = reinterpret_cast<const uint4*>(A1 + (size_t)b * kP1 + cg * 720)[min(t, 44)];
+  if (t < 200) reinterpret_cast<float4*>(g800)[t] = gv;
+  if (t < 50) reinterpret_cast<uint4*>(a800)[t] = a2v;
+  if (t < kImg / 4) reinterpret_cast<float4*>(xs)[t] = xv;
+  if (t < 180) reinterpret_cast<float4*>(p1m)[t] = pv;
+  if (t < 45) reinterpret_cast<uint4*>(cds)[t] = cv;
+  __syncthreads();
+  // (0) dY2[co][px] from the pooled gradient + codes
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const int i = t + 512 * r;
+    if (i < 50 * 64) {
+      const int c = i >> 6, px = i & 63, oh = px >> 3, ow = px & 7;
+      const int q = c * 16 + (oh >> 1) * 4 + (ow >> 1);
+      dys[c * 65 + px] = (a800[q] == (oh & 1) * 2 + (ow & 1)) ? g800[q] : 0.f;
+    }
   }
   __syncthreads();
+  // (1) dgrad tile (dmt, dpt): 25 x 32x32x2 over co = 50
   {
-    // wave w: k-tile mt = w (k_local in [32w, 32w+32), valid < 125), both px tiles.
-    const int kl = w * 32 + (l & 31);
-    const float km = kl < 125 ? 1.f : 0.f;
-    const float* wa = W2c + (l >> 5) * 500 + cg * 125 + min(kl, 124);
-    const float* b0p = dys + (l >> 5) * 65 + (l & 31);
-    f32x16 acc0 = {0.f}, acc1 = {0.f};
+    const float* bp = dys + (l >> 5) * 65 + dpt * 32 + (l & 31);
+    f32x16 acc = {0.f};
 #pragma unroll
     for (int s = 0; s < 25; ++s) {
-      const float a = wa[2 * s * 500] * km;
-      acc0 = mfma32x32x2(a, b0p[2 * s * 65], acc0);
-      acc1 = mfma32x32x2(a, b0p[2 * s * 65 + 32], acc1);
+      if (dbg & 32) { acc[0] += av[s]; continue; }
+      acc = mfma32x32x2(av[s] * km, bp[2 * s * 65], acc);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k = w * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-      if (k < 125) {
-        const int cl = k / 25, rem = k - cl * 25, kh = rem / 5, kw = rem - kh * 5;
-        const int px0 = l & 31, oh0 = px0 >> 3, ow = px0 & 7;
-        atomicAdd(&dp1[cl * 144 + (oh0 + kh) * 12 + ow + kw], acc0[r]);
-        atomicAdd(&dp1[cl * 144 + (oh0 + 4 + kh) * 12 + ow + kw], acc1[r]);
+    for (int r = 0; r < 16; ++r)
+      T[(dmt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 65 + dpt * 32 + (l & 31)] = acc[r];
+  }
+  __syncthreads();
+  // (2) col2im gather + maxpool1/relu mask: dP1[cl][ih][iw] = sum_{kh,kw} T[cl*25+kh*5+kw][(ih-kh)*8+iw-kw]
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int o = t + 512 * r;
+    if (o < 720) {
+      const int cl = o / 144, p = o - cl * 144, ih = p / 12, iw = p - ih * 12;
+      float sacc = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh) {
+        const int oh = ih - kh;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const int ow = iw - kw;
+          const bool ok = oh >= 0 && oh < 8 && ow >= 0 && ow < 8;
+          const int idx = ok ? (cl * 25 + kh * 5 + kw) * 65 + oh * 8 + ow : 0;
+          const float tv = T[idx];
+          sacc += ok ? tv : 0.f;
+        }
       }
+      dp1[o] = p1m[o] > 0.f ? sacc : 0.f;
     }
   }
   __syncthreads();
-  // maxpool1 + relu backward mask, codes to LDS
-  for (int i = t; i < 720; i += 256) {
-    const size_t gi = (size_t)b * kP1 + cg * 720 + i;
-    if (!(P1[gi] > 0.f)) dp1[i] = 0.f;
-    cds[i] = A1[gi];
+  // (3) dense dY1 [5][576] (into the dead dys region) from dP1 + maxpool1 codes
+  float* dy1 = dys;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int o = t + 512 * r;
+    if (o < 720) {
+      const int cl = o / 144, p = o - cl * 144, ph = p / 12, pw = p - ph * 12;
+      const float g = dp1[o];
+      const int code = cds[o];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dy1[cl * 576 + (2 * ph + (q >> 1)) * 24 + 2 * pw + (q & 1)] = (code == q) ? g : 0.f;
+    }
   }
   __syncthreads();
-  // conv1 wgrad: 125 outputs (cl, kh, kw) x 2 halves of the 144 pooled positions
-  if (t < 250) {
-    const int o = t >> 1, half = t & 1;
-    const int cl = o / 25, rem = o - cl * 25, kh = rem / 5, kw = rem - kh * 5;
-    float s = 0.f, sb = 0.f;
-    for (int p = half * 72; p < half * 72 + 72; ++p) {
-      const float g = dp1[cl * 144 + p];
-      const int code = cds[cl * 144 + p];
-      const int ph = p / 12, pw = p - ph * 12;
-      const int y = 2 * ph + (code >> 1) + kh, x = 2 * pw + (code & 1) + kw;
-      s = fmaf(g, xs[y * 28 + x], s);
-      sb += g;
+  if (dbg & 16) return;
+  // (4) conv1 wgrad|bgrad: C[c][tap] = sum_pos dY1[c][pos] * [X(pos+tap) | 1]; wave = (tap-tile, K-quarter)
+  float* red = T;                                             // T is dead: [4][16][33] partials
+  {
+    const int nt = w & 1, kq = w >> 1;
+    const int c = l & 15, cc = min(c, 4);
+    const float cmask = c < 5 ? 1.f : 0.f;
+    const int tap = nt * 16 + (l & 15);
+    const float tmask = tap < 25 ? 1.f : 0.f, tone = tap == 25 ? 1.f : 0.f;
+    const int tc = min(tap, 24), th = tc / 5, tw = tc - th * 5;
+    const float* ap = dy1 + cc * 576 + kq * 144 + lg;
+    const float* xp = xs + (6 * kq + th) * 28 + tw + lg;
+    f32x4 acc0 = {0.f}, acc1 = {0.f};
+#pragma unroll
+    for (int s = 0; s < 36; ++s) {
+      const int ohs = (4 * s) / 24, ows = (4 * s) % 24;       // pos = 144kq + 4s + lg
+      const float a = ap[4 * s] * cmask;
+      const float bv = xp[ohs * 28 + ows] * tmask + tone;
+      if (s & 1) acc1 = mfma16x16x4(a, bv, acc1);
+      else acc0 = mfma16x16x4(a, bv, acc0);
     }
-    s += __shfl_xor(s, 1, 64);
-    sb += __shfl_xor(sb, 1, 64);
-    if (half == 0) {
-      const int c = cg * 5 + cl;
-      atomicAdd(&gW1c[c * 25 + rem], s);
-      if (rem == 0) atomicAdd(&gb1c[c], sb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(kq * 16 + lg * 4 + r) * 33 + nt * 16 + (l & 15)] = acc0[r] + acc1[r];
+  }
+  __syncthreads();
+  if (t < 130) {
+    const int c = t / 26, tap = t - c * 26;
+    const float v = red[c * 33 + tap] + red[(16 + c) * 33 + tap] + red[(32 + c) * 33 + tap] +
+                    red[(48 + c) * 33 + tap];
+    if (!(dbg & 4) || v == 1234.5f) {
+      const int ch = cg * 5 + c;
+      const size_t rep = (size_t)(b % c1_nrep) * c1_rep_stride;
+      if (tap < 25) atomicAdd(&gW1c[rep + ch * 25 + tap], v);
+      else atomicAdd(&gb1c[rep + ch], v);
     }
   }
 }
@@ -583,32 +830,27 @@ __global__ __launch_bounds__(256) void k_conv_bwd(const float* __restrict__ X, c
 // =================================================================================================
 extern "C" {
 
-hipError_t pde_lenet_conv1_fwd(const float* X, const int* idx, const long long* step, int nbatches, int stride,
-                               const long long* labels_all, int B, const float* w, const float* bias, float* P1,
-                               uint8_t* A1, int* cur_row, long long* cur_lbl, float* zero_ptr, int zero_n,
-                               hipStream_t st) {
-  BatchSrc src{idx, step, nbatches, stride > 0 ? stride : B};
-  hipLaunchKernelGGL(k_conv1_fwd, dim3(B, 4), dim3(192), 0, st, X, src, labels_all, w, bias, P1, A1, cur_row,
-                     cur_lbl, zero_ptr, zero_n);
+hipError_t pde_lenet_conv_fwd(const float* X, const int* idx, int n_idx, const long long* step, int nbatches,
+                              int stride, const long long* labels_all, int B, const float* w1, const float* b1,
+                              const float* Wt2, const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2,
+                              int* cur_row, long long* cur_lbl, float* zero_ptr, int zero_n, int dbg, hipStream_t st) {
+  BatchSrc src{idx, step, nbatches, stride > 0 ? stride : B, n_idx};
+  hipLaunchKernelGGL(k_conv_fwd, dim3(B, 2), dim3(256), 0, st, X, src, labels_all, w1, b1, Wt2, b2, P1, A1, P2, A2,
+                     cur_row, cur_lbl, zero_ptr, zero_n, dbg);
   return hipGetLastError();
 }
 
-hipError_t pde_lenet_conv2_fwd(const float* P1, int B, const float* Wt2, const float* bias, float* P2, uint8_t* A2,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(k_conv2_fwd, dim3(B, 2), dim3(256), 0, st, P1, Wt2, bias, P2, A2);
-  return hipGetLastError();
-}
-
-hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float* bias, float* H1, hipStream_t st) {
-  hipLaunchKernelGGL(k_fc1_fwd, dim3(32, (B + 15) / 16), dim3(256), 0, st, P2, B, W, bias, H1);
+hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float* bias, float* H1, long long* ctr,
+                             int nctr, hipStream_t st) {
+  hipLaunchKernelGGL(k_fc1_fwd, dim3(32, (B + 15) / 16), dim3(256), 0, st, P2, B, W, bias, H1, ctr, nctr);
   return hipGetLastError();
 }
 
 hipError_t pde_lenet_head(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
-                          float inv_b, float* logp_out, float* dZ2, float* dZ1, double* loss_sum,
-                          unsigned long long* correct, hipStream_t st) {
+                          float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
+                          double* loss_sum, unsigned long long* correct, hipStream_t st) {
   hipLaunchKernelGGL(k_head, dim3((B + 3) / 4), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2, dZ1,
-                     loss_sum, correct);
+                     row_loss, row_hit, loss_sum, correct);
   return hipGetLastError();
 }
 
@@ -619,18 +861,22 @@ hipError_t pde_lenet_head_bwd(const float* H1, int B, const float* W2, const flo
 }
 
 hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, const float* dZ2, const float* W1,
-                            int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, hipStream_t st) {
+                            int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, const float* row_loss,
+                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg,
+                            hipStream_t st) {
   const int nblk = ((B + 15) / 16) * 50 + 32 * 13 + 8;
-  hipLaunchKernelGGL(k_fc_bwd, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2);
+  hipLaunchKernelGGL(k_fc_bwd, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2,
+                     row_loss, row_hit, loss_sum, correct, dbg);
   return hipGetLastError();
 }
 
 hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, const uint8_t* A1,
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,
-                              float* gb1c, float* gW2c, float* gb2c, hipStream_t st) {
-  const int nblk = ((B + kWImgs - 1) / kWImgs) * 8 + 4 * B;
-  hipLaunchKernelGGL(k_conv_bwd, dim3(nblk), dim3(256), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
-                     gW2c, gb2c);
+                              float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride, int dbg,
+                              hipStream_t st) {
+  const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B;
+  hipLaunchKernelGGL(k_conv_bwd, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
+                     gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, dbg);
   return hipGetLastError();
 }
 

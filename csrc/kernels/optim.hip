@@ -6,7 +6,8 @@
 // The step counter lives on the device: every block reads t = *step + 1 and the last block to
 // arrive publishes *step = t (arrival counter reset in the same block), so the whole optimizer
 // step is capturable in a hipGraph and replayable without host involvement.  `bump` = number of
-// consecutive int64 counters advanced by the last block (0: none; [0] is the optimizer step).
+// consecutive int64 counters advanced by the last block (0: none; [0] is the optimizer step);
+// bump < 0: the caller's earlier kernel already advanced the counter, t = *step, no fan-in at all.
 // grad_scale folds the DDP 1/world_size average (or any loss scale) into the update.
 // Optional epilogue: repack the LeNet conv2 weight [50][20][5][5] into the [k'][64] layout the
 // conv2 forward kernel streams (k' = (kh*5+kw)*20+ci), so no separate repack launch exists.
@@ -20,10 +21,36 @@ struct Pack {
   float* dst;      // [500][64]
 };
 
+struct Fold {
+  long long off;   // first element of the canonical gradient (replica 0); -1 = none
+  int len;         // elements per replica unit (multiple of 4)
+  int nrep;        // replicas (1 = nothing to fold)
+  int stride;      // floats between replicas (multiple of 4)
+};
+
+// Returns false for float4 groups that are replica storage (r >= 1): they are not parameters.
+// For canonical groups, sums the replicas into g4 (written back so p.grad holds the true gradient).
+__device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long i, float4& gg) {
+  if (fd.off < 0 || fd.nrep <= 1) return true;
+  const long long e = 4 * i - fd.off;
+  if (e < 0 || e >= (long long)fd.stride * fd.nrep) return true;
+  const long long r = e / fd.stride, o = e - r * fd.stride;
+  if (r > 0) return false;
+  if (o < fd.len) {
+    for (int k = 1; k < fd.nrep; ++k) {
+      const float4 x = g4[i + (long long)k * (fd.stride / 4)];
+      gg.x += x.x; gg.y += x.y; gg.z += x.z; gg.w += x.w;
+    }
+    g4[i] = gg;
+  }
+  return true;
+}
+
 __device__ __forceinline__ void pack_store(const Pack& pk, long long i, float v) {
-  const long long e = i - pk.off;
-  if (pk.off >= 0 && e >= 0 && e < 25000) {
-    const int co = (int)(e / 500), k = (int)(e % 500), ci = k / 25, r = k % 25;
+  const long long e64 = i - pk.off;
+  if (pk.off >= 0 && e64 >= 0 && e64 < 25000) {
+    const int e = (int)e64;                 // 32-bit index math (64-bit division is ~100 instructions)
+    const int co = e / 500, k = e - co * 500, ci = k / 25, r = k - ci * 25;
     pk.dst[(r * 20 + ci) * 64 + co] = v;
   }
 }
@@ -41,23 +68,24 @@ __device__ __forceinline__ bool last_block(unsigned* arrive, long long t) {
   return is_last != 0;
 }
 
-__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, long long n4,
                                               float lr, float b1, float b2, float eps, float wd, int decoupled,
                                               float grad_scale, long long* __restrict__ step,
-                                              unsigned* __restrict__ arrive, int bump, Pack pk) {
-  const long long t = *step + 1;
+                                              unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd) {
+  const long long t = bump < 0 ? *step : *step + 1;   // bump < 0: counter pre-advanced by an earlier kernel
   const float bc1 = 1.f - powf(b1, (float)t);
   const float bc2 = 1.f - powf(b2, (float)t);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   const float omb1 = 1.f - b1, omb2 = 1.f - b2;
   float4* p4 = reinterpret_cast<float4*>(p);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* g4 = reinterpret_cast<float4*>(g);
   float4* m4 = reinterpret_cast<float4*>(m);
   float4* v4 = reinterpret_cast<float4*>(v);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
+    if (!fold_grad(fd, g4, i, gg)) continue;
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -83,16 +111,17 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
 
 // torch.optim.SGD semantics (torch/optim/sgd.py): d_p = g + wd*p; buf = momentum*buf + (1-dampening)*d_p
 // (buf = d_p on the first step); d_p = nesterov ? d_p + momentum*buf : buf; p -= lr*d_p.
-__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
                                              long long n4, float lr, float momentum, float dampening, float wd,
                                              int nesterov, float grad_scale, long long* __restrict__ step,
-                                             unsigned* __restrict__ arrive, int bump, Pack pk) {
-  const long long t = *step + 1;
+                                             unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd) {
+  const long long t = bump < 0 ? *step : *step + 1;
   float4* p4 = reinterpret_cast<float4*>(p);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* g4 = reinterpret_cast<float4*>(g);
   float4* b4 = reinterpret_cast<float4*>(buf);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 pp = p4[i], gg = g4[i];
+    if (!fold_grad(fd, g4, i, gg)) continue;
     float4 bb = momentum != 0.f ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float* pa = &pp.x; float* ga = &gg.x; float* ba = &bb.x;
 #pragma unroll
@@ -140,23 +169,27 @@ inline int grid_for(long long n4) {
 
 extern "C" {
 
-hipError_t pde_adam_flat(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2,
+hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, float lr, float b1, float b2,
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
-                         int bump, long long pack_off, float* pack_dst, hipStream_t st) {
+                         int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
+                         int fold_nrep, int fold_stride, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
   hipLaunchKernelGGL(k_adam, dim3(grid_for(n4)), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps, wd, decoupled,
-                     grad_scale, step, arrive, bump, Pack{pack_off, pack_dst});
+                     grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
+                     Fold{fold_off, fold_len, fold_nrep, fold_stride});
   return hipGetLastError();
 }
 
-hipError_t pde_sgd_flat(float* p, const float* g, float* buf, long long n, float lr, float momentum, float dampening,
+hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, float momentum, float dampening,
                         float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
-                        long long pack_off, float* pack_dst, hipStream_t st) {
+                        long long pack_off, float* pack_dst, long long fold_off, int fold_len, int fold_nrep,
+                        int fold_stride, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
   hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4)), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
-                     nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst});
+                     nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
+                     Fold{fold_off, fold_len, fold_nrep, fold_stride});
   return hipGetLastError();
 }
 

@@ -46,54 +46,51 @@ constexpr auto U8 = at::kByte;
 constexpr auto F64 = at::kDouble;
 
 // ------------------------------------------------------------------------------------------------
-void lenet_conv1_fwd(const at::Tensor& X, const OptT& idx, const OptT& step, int64_t nbatches, int64_t stride,
-                     const OptT& labels_all,
-                     int64_t B, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& P1,
-                     const at::Tensor& A1, const OptT& cur_row, const OptT& cur_lbl, const OptT& zero) {
+void lenet_conv_fwd(const at::Tensor& X, const OptT& idx, const OptT& step, int64_t nbatches, int64_t stride,
+                    const OptT& labels_all, int64_t B, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& Wt2,
+                    const at::Tensor& b2, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& P2,
+                    const at::Tensor& A2, const OptT& cur_row, const OptT& cur_lbl, const OptT& zero, int64_t dbg) {
   TORCH_CHECK(B >= 1, "batch must be >= 1");
   check_cuda(X, "X", F32);
   TORCH_CHECK(X.numel() % 784 == 0, "X must be [N,1,28,28]");
   if (!idx.has_value()) TORCH_CHECK(X.numel() >= B * 784, "X smaller than batch");
-  check_cuda(w, "conv1.weight", F32, 500);
-  check_cuda(bias, "conv1.bias", F32, 20);
+  check_cuda(w1, "conv1.weight", F32, 500);
+  check_cuda(b1, "conv1.bias", F32, 20);
+  check_cuda(Wt2, "Wt2", F32, 500 * 64);
+  check_cuda(b2, "conv2.bias", F32, 50);
   check_cuda(P1, "P1", F32, B * 2880);
   check_cuda(A1, "A1", U8, B * 2880);
-  const int* ip = optr<int>(idx, "idx", I32, B);
-  const long long* sp = optr<long long>(step, "step", I64, 1);
-  const int64_t st = stride > 0 ? stride : B;
-  if (sp) TORCH_CHECK(ip && nbatches >= 1 && idx->numel() >= (nbatches - 1) * st + B, "step-indexed batches need idx");
-  float* zp = optr<float>(zero, "zero", F32);
-  hip_check(pde_lenet_conv1_fwd(ptr<float>(X), ip, sp, (int)nbatches, (int)st, optr<long long>(labels_all, "labels", I64), (int)B,
-                                ptr<float>(w), ptr<float>(bias), ptr<float>(P1), ptr<uint8_t>(A1),
-                                optr<int>(cur_row, "cur_row", I32, B), optr<long long>(cur_lbl, "cur_lbl", I64, B), zp,
-                                zp ? (int)zero->numel() : 0, cur_stream()),
-            "lenet_conv1_fwd");
-}
-
-void lenet_conv2_fwd(const at::Tensor& P1, int64_t B, const at::Tensor& Wt2, const at::Tensor& bias,
-                     const at::Tensor& P2, const at::Tensor& A2) {
-  check_cuda(P1, "P1", F32, B * 2880);
-  check_cuda(Wt2, "Wt2", F32, 500 * 64);
-  check_cuda(bias, "conv2.bias", F32, 50);
   check_cuda(P2, "P2", F32, B * 800);
   check_cuda(A2, "A2", U8, B * 800);
-  hip_check(pde_lenet_conv2_fwd(ptr<float>(P1), (int)B, ptr<float>(Wt2), ptr<float>(bias), ptr<float>(P2),
-                                ptr<uint8_t>(A2), cur_stream()),
-            "lenet_conv2_fwd");
+  const int* ip = optr<int>(idx, "idx", I32, step.has_value() ? 1 : B);
+  const long long* sp = optr<long long>(step, "step", I64, 1);
+  const int64_t st = stride > 0 ? stride : B;
+  if (sp) TORCH_CHECK(ip && nbatches >= 1, "step-indexed batches need idx");
+  float* zp = optr<float>(zero, "zero", F32);
+  hip_check(pde_lenet_conv_fwd(ptr<float>(X), ip, ip ? (int)idx->numel() : 0, sp, (int)nbatches, (int)st,
+                               optr<long long>(labels_all, "labels", I64), (int)B, ptr<float>(w1), ptr<float>(b1),
+                               ptr<float>(Wt2), ptr<float>(b2), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(P2),
+                               ptr<uint8_t>(A2), optr<int>(cur_row, "cur_row", I32, B),
+                               optr<long long>(cur_lbl, "cur_lbl", I64, B), zp, zp ? (int)zero->numel() : 0,
+                               (int)dbg, cur_stream()),
+            "lenet_conv_fwd");
 }
 
-void lenet_fc1_fwd(const at::Tensor& P2, int64_t B, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& H1) {
+void lenet_fc1_fwd(const at::Tensor& P2, int64_t B, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& H1,
+                   const OptT& ctr) {
   check_cuda(P2, "P2", F32, B * 800);
   check_cuda(W, "fc1.weight", F32, 500 * 800);
   check_cuda(bias, "fc1.bias", F32, 500);
   check_cuda(H1, "H1", F32, B * 500);
-  hip_check(pde_lenet_fc1_fwd(ptr<float>(P2), (int)B, ptr<float>(W), ptr<float>(bias), ptr<float>(H1), cur_stream()),
+  long long* cp = optr<long long>(ctr, "counters", I64, 1);
+  hip_check(pde_lenet_fc1_fwd(ptr<float>(P2), (int)B, ptr<float>(W), ptr<float>(bias), ptr<float>(H1), cp,
+                              cp ? (int)ctr->numel() : 0, cur_stream()),
             "lenet_fc1_fwd");
 }
 
 void lenet_head(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& labels,
-                double inv_b, const OptT& logp, const OptT& dZ2, const OptT& dZ1, const OptT& loss_sum,
-                const OptT& correct) {
+                double inv_b, const OptT& logp, const OptT& dZ2, const OptT& dZ1, const OptT& row_loss,
+                const OptT& row_hit, const OptT& loss_sum, const OptT& correct) {
   check_cuda(H1, "H1", F32, B * 500);
   check_cuda(W2, "fc2.weight", F32, 5000);
   check_cuda(b2, "fc2.bias", F32, 10);
@@ -101,8 +98,12 @@ void lenet_head(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const at:
   float* dz1 = optr<float>(dZ1, "dZ1", F32, B * 500);
   float* dz2 = optr<float>(dZ2, "dZ2", F32, B * 10);
   TORCH_CHECK((dz1 == nullptr) == (dz2 == nullptr), "dZ1 and dZ2 go together");
+  float* rl = optr<float>(row_loss, "row_loss", F32, B);
+  int* rh = optr<int>(row_hit, "row_hit", I32, B);
+  TORCH_CHECK((rl == nullptr) == (rh == nullptr), "row_loss and row_hit go together");
   hip_check(pde_lenet_head(ptr<float>(H1), (int)B, ptr<float>(W2), ptr<float>(b2), ptr<long long>(labels), (float)inv_b,
-                           optr<float>(logp, "logp", F32, B * 10), dz2, dz1, optr<double>(loss_sum, "loss_sum", F64, 1),
+                           optr<float>(logp, "logp", F32, B * 10), dz2, dz1, rl, rh,
+                           optr<double>(loss_sum, "loss_sum", F64, 1),
                            optr<unsigned long long>(correct, "correct", I64, 1), cur_stream()),
             "lenet_head");
 }
@@ -122,7 +123,8 @@ void lenet_head_bwd(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const
 
 void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& dZ1, const at::Tensor& dZ2,
                   const at::Tensor& W1, int64_t B, const at::Tensor& dP2m, const at::Tensor& gW1, const at::Tensor& gb1,
-                  const at::Tensor& gW2, const at::Tensor& gb2) {
+                  const at::Tensor& gW2, const at::Tensor& gb2, const OptT& row_loss, const OptT& row_hit,
+                  const OptT& loss_sum, const OptT& correct, int64_t dbg) {
   check_cuda(P2, "P2", F32, B * 800);
   check_cuda(H1, "H1", F32, B * 500);
   check_cuda(dZ1, "dZ1", F32, B * 500);
@@ -135,13 +137,16 @@ void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& 
   check_cuda(gb2, "gb2", F32, 10);
   hip_check(pde_lenet_fc_bwd(ptr<float>(P2), ptr<float>(H1), ptr<float>(dZ1), ptr<float>(dZ2), ptr<float>(W1), (int)B,
                              ptr<float>(dP2m), ptr<float>(gW1), ptr<float>(gb1), ptr<float>(gW2), ptr<float>(gb2),
-                             cur_stream()),
+                             optr<float>(row_loss, "row_loss", F32, B), optr<int>(row_hit, "row_hit", I32, B),
+                             optr<double>(loss_sum, "loss_sum", F64, 1),
+                             optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, cur_stream()),
             "lenet_fc_bwd");
 }
 
 void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tensor& P1, const at::Tensor& A1,
                     const at::Tensor& dP2m, const at::Tensor& A2, const at::Tensor& W2c, int64_t B,
-                    const at::Tensor& gW1c, const at::Tensor& gb1c, const at::Tensor& gW2c, const at::Tensor& gb2c) {
+                    const at::Tensor& gW1c, const at::Tensor& gb1c, const at::Tensor& gW2c, const at::Tensor& gb2c,
+                    int64_t c1_nrep, int64_t c1_rep_stride, int64_t dbg) {
   check_cuda(X, "X", F32);
   check_cuda(rows, "rows", I32, B);
   check_cuda(P1, "P1", F32, B * 2880);
@@ -149,51 +154,68 @@ void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tenso
   check_cuda(dP2m, "dP2m", F32, B * 800);
   check_cuda(A2, "A2", U8, B * 800);
   check_cuda(W2c, "conv2.weight", F32, 25000);
-  check_cuda(gW1c, "gW1c", F32, 500);
+  TORCH_CHECK(c1_nrep >= 1 && (c1_nrep == 1 || c1_rep_stride >= 520), "bad conv1 replica layout");
+  check_cuda(gW1c, "gW1c", F32, 500 + (c1_nrep - 1) * c1_rep_stride);
   check_cuda(gb1c, "gb1c", F32, 20);
+  if (c1_nrep > 1)
+    TORCH_CHECK(gb1c.data_ptr<float>() + (c1_nrep - 1) * c1_rep_stride + 20 <=
+                    gW1c.data_ptr<float>() + gW1c.numel(), "conv1 replicas must fit in the gW1c storage view");
   check_cuda(gW2c, "gW2c", F32, 25000);
   check_cuda(gb2c, "gb2c", F32, 50);
   hip_check(pde_lenet_conv_bwd(ptr<float>(X), ptr<int>(rows), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(dP2m),
                                ptr<uint8_t>(A2), ptr<float>(W2c), (int)B, ptr<float>(gW1c), ptr<float>(gb1c),
-                               ptr<float>(gW2c), ptr<float>(gb2c), cur_stream()),
+                               ptr<float>(gW2c), ptr<float>(gb2c), (int)c1_nrep, (int)c1_rep_stride, (int)dbg,
+                               cur_stream()),
             "lenet_conv_bwd");
 }
 
 // ------------------------------------------------------------------------------------------------
 void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v, double lr,
                double b1, double b2, double eps, double wd, bool decoupled, double grad_scale, const at::Tensor& step,
-               const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst) {
+               const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst, int64_t fold_off,
+               int64_t fold_len, int64_t fold_nrep, int64_t fold_stride) {
   const int64_t n = p.numel();
   check_cuda(p, "params", F32);
   check_cuda(g, "grads", F32, n);
   check_cuda(m, "exp_avg", F32, n);
+  if (fold_off >= 0 && fold_nrep > 1)
+    TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
+                    fold_off + fold_stride * fold_nrep <= n, "bad gradient fold layout");
   check_cuda(v, "exp_avg_sq", F32, n);
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
+  TORCH_CHECK(bump >= -1, "bump must be >= -1");
   check_cuda(arrive, "arrive", I32, 1);
   TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
   float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
   if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
   hip_check(pde_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), n, (float)lr, (float)b1,
                           (float)b2, (float)eps, (float)wd, decoupled ? 1 : 0, (float)grad_scale, ptr<long long>(step),
-                          ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, cur_stream()),
+                          ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, fold_off, (int)fold_len,
+                          (int)fold_nrep, (int)fold_stride, cur_stream()),
             "adam_flat");
 }
 
 void sgd_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, double lr, double momentum,
               double dampening, double wd, bool nesterov, double grad_scale, const at::Tensor& step,
-              const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst) {
+              const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst, int64_t fold_off,
+              int64_t fold_len, int64_t fold_nrep, int64_t fold_stride) {
   const int64_t n = p.numel();
   check_cuda(p, "params", F32);
   check_cuda(g, "grads", F32, n);
   check_cuda(buf, "momentum_buffer", F32, momentum != 0.0 ? n : 0);
+  if (fold_off >= 0 && fold_nrep > 1)
+    TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
+                    fold_off + fold_stride * fold_nrep <= n, "bad gradient fold layout");
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
+  TORCH_CHECK(bump >= -1, "bump must be >= -1");
   check_cuda(arrive, "arrive", I32, 1);
   TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
   float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
   if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
   hip_check(pde_sgd_flat(ptr<float>(p), ptr<float>(g), ptr<float>(buf), n, (float)lr, (float)momentum,
                          (float)dampening, (float)wd, nesterov ? 1 : 0, (float)grad_scale, ptr<long long>(step),
-                         ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, cur_stream()),
+                         ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, fold_off, (int)fold_len,
+                         (int)fold_nrep, (int)fold_stride, cur_stream()),
             "sgd_flat");
 }
 
@@ -214,17 +236,27 @@ PYBIND11_MODULE(_kernels, m) {
   m.doc() = "CDNA4 (gfx950) HIP kernels of pytorch_distributed_example_amd";
   m.attr("arch") = "gfx950";
   namespace py = pybind11;
-  m.def("lenet_conv1_fwd", &lenet_conv1_fwd, py::arg("X"), py::arg("idx"), py::arg("step"), py::arg("nbatches"),
-        py::arg("stride"), py::arg("labels_all"), py::arg("B"), py::arg("w"), py::arg("bias"), py::arg("P1"), py::arg("A1"),
-        py::arg("cur_row"), py::arg("cur_lbl"), py::arg("zero"));
-  m.def("lenet_conv2_fwd", &lenet_conv2_fwd);
+  m.def("lenet_conv_fwd", &lenet_conv_fwd, py::arg("X"), py::arg("idx"), py::arg("step"), py::arg("nbatches"),
+        py::arg("stride"), py::arg("labels_all"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wt2"),
+        py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("cur_row"),
+        py::arg("cur_lbl"), py::arg("zero"), py::arg("dbg") = 0);
   m.def("lenet_fc1_fwd", &lenet_fc1_fwd);
   m.def("lenet_head", &lenet_head);
   m.def("lenet_head_bwd", &lenet_head_bwd);
-  m.def("lenet_fc_bwd", &lenet_fc_bwd);
-  m.def("lenet_conv_bwd", &lenet_conv_bwd);
-  m.def("adam_flat", &adam_flat);
-  m.def("sgd_flat", &sgd_flat);
+  m.def("lenet_fc_bwd", &lenet_fc_bwd, py::arg("P2"), py::arg("H1"), py::arg("dZ1"), py::arg("dZ2"), py::arg("W1"),
+        py::arg("B"), py::arg("dP2m"), py::arg("gW1"), py::arg("gb1"), py::arg("gW2"), py::arg("gb2"),
+        py::arg("row_loss"), py::arg("row_hit"), py::arg("loss_sum"), py::arg("correct"), py::arg("dbg") = 0);
+  m.def("lenet_conv_bwd", &lenet_conv_bwd, py::arg("X"), py::arg("rows"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
+        py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("gW2c"), py::arg("gb2c"),
+        py::arg("c1_nrep") = 1, py::arg("c1_rep_stride") = 0, py::arg("dbg") = 0);
+  m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"), py::arg("b1"),
+        py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("decoupled"), py::arg("grad_scale"), py::arg("step"),
+        py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),
+        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0);
+  m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
+        py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("grad_scale"), py::arg("step"),
+        py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),
+        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0);
   m.def("lenet_pack_w2", &lenet_pack_w2);
   m.def("scale_", &scale_);
 }

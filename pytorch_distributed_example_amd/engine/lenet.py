@@ -3,7 +3,7 @@
 Per step (reference semantics: /root/reference/mnist/main.py:84-99 forward, cross_entropy,
 zero_grad, backward, average_gradients, Adam step, meters) this issues:
 
-  compute stream : F1 conv1 (+gather, +grad zeroing) -> F2 conv2 -> F3 fc1 -> F4 head/loss/dlogits
+  compute stream : F1 conv1+conv2 (+gather, +grad zeroing) -> F2 fc1 -> F3 head/loss/dlogits
                    -> B1 fc backward --(event)--> B2 conv backward --(event)--> [wait comm] -> fused Adam
   comm stream    :                    all_reduce(bucket 0: fc grads, 1.62 MB) | all_reduce(bucket 1: conv grads)
 
@@ -14,7 +14,7 @@ zero_grad, backward, average_gradients, Adam step, meters) this issues:
 * Loss/accuracy meters accumulate on the device and are read once per epoch (no per-step
   ``.item()`` syncs, survey S1).
 * The dataset is device resident; the epoch permutation is uploaded once per epoch and batch b of
-  the epoch is gathered inside F1 from a device batch counter that the fused Adam advances, so a
+  the epoch is gathered inside F1 from a device batch counter that F2 advances, so a
   captured hipGraph replays consecutive steps with no host work at all.
 """
 from __future__ import annotations
@@ -29,7 +29,9 @@ from ..ops.lenet_fused import pack_conv2_weight
 from ..parallel.flat import FlatLayout
 
 FC_BUCKET = ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"]
-CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"]
+CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv1.grad_replicas", "conv2.weight", "conv2.bias"]
+C1_NREP = 16          # conv1 gradient replicas (atomic contention: 128 images -> 8 adders per address)
+C1_STRIDE = 576       # conv1.weight (500 -> 512 slot) + conv1.bias (20 -> 64 slot)
 
 
 class LeNetTrainStep:
@@ -50,11 +52,18 @@ class LeNetTrainStep:
         self.overlap = overlap
         self.K = kernels()
         dev = self.device
-        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, CONV_BUCKET])
+        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, CONV_BUCKET],
+                                 extra_shapes={"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,)})
         self.params, self.grads = self.layout.bind(net)
         V = self.layout.view
-        self.p = {n: V(self.params, n) for n in self.layout.slots}
-        self.g = {n: V(self.grads, n) for n in self.layout.slots}
+        self.p = {n: V(self.params, n) for n in self.layout.param_names}
+        self.g = {n: V(self.grads, n) for n in self.layout.param_names}
+        c1 = self.layout.slots["conv1.weight"].offset
+        assert self.layout.slots["conv1.bias"].offset == c1 + 512
+        assert self.layout.slots["conv1.grad_replicas"].offset == c1 + C1_STRIDE
+        self.c1_off = c1
+        self.g_c1w_rep = self.grads[c1: c1 + C1_NREP * C1_STRIDE]
+        self.g_c1b_rep = self.grads[c1 + 512: c1 + C1_NREP * C1_STRIDE]
         self.bucket_grads = [self.layout.bucket_view(self.grads, i) for i in range(2)]
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params) if optimizer == "adam" else self.m
@@ -74,6 +83,8 @@ class LeNetTrainStep:
         self.dP2m = torch.empty(B * 800, **f32)
         self.cur_row = torch.zeros(B, device=dev, dtype=torch.int32)
         self.cur_lbl = torch.zeros(B, device=dev, dtype=torch.int64)
+        self.row_loss = torch.zeros(B, **f32)
+        self.row_hit = torch.zeros(B, device=dev, dtype=torch.int32)
         self.loss_sum = torch.zeros(1, device=dev, dtype=torch.float64)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int64)
         self.samples = 0
@@ -109,15 +120,15 @@ class LeNetTrainStep:
     # ------------------------------------------------------------------ the step
     def _launch(self, B: int):
         K, p, g = self.K, self.p, self.g
-        K.lenet_conv1_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
-                          p["conv1.weight"], p["conv1.bias"], self.P1, self.A1, self.cur_row, self.cur_lbl,
-                          self.bucket_grads[1])
-        K.lenet_conv2_fwd(self.P1, B, self.Wt2, p["conv2.bias"], self.P2, self.A2)
-        K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1)
+        K.lenet_conv_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
+                         p["conv1.weight"], p["conv1.bias"], self.Wt2, p["conv2.bias"], self.P1, self.A1, self.P2,
+                         self.A2, self.cur_row, self.cur_lbl, self.bucket_grads[1])
+        K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1, self.counters)   # bumps counters
         K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], self.cur_lbl, 1.0 / B, None, self.dZ2, self.dZ1,
-                     self.loss_sum, self.correct)
+                     self.row_loss, self.row_hit, None, None)
         K.lenet_fc_bwd(self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
-                       g["fc1.bias"], g["fc2.weight"], g["fc2.bias"])
+                       g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], self.row_loss, self.row_hit, self.loss_sum,
+                       self.correct)
         cur = torch.cuda.current_stream(self.device)
         if self.world > 1 and self.overlap:
             self._ev[0].record(cur)
@@ -125,7 +136,7 @@ class LeNetTrainStep:
             with torch.cuda.stream(self.comm_stream):
                 self.comm.all_reduce_(self.bucket_grads[0])
         K.lenet_conv_bwd(self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
-                         g["conv1.weight"], g["conv1.bias"], g["conv2.weight"], g["conv2.bias"])
+                         self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE)
         if self.world > 1:
             self._ev[1].record(cur)
             self.comm_stream.wait_event(self._ev[1])
@@ -138,10 +149,12 @@ class LeNetTrainStep:
         scale = 1.0 / self.world
         if self.optimizer == "adam":
             K.adam_flat(self.params, self.grads, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps,
-                        self.wd, False, scale, self.counters, self.arrive, 2, self.pack_off, self.Wt2)
+                        self.wd, False, scale, self.counters, self.arrive, -1, self.pack_off, self.Wt2,
+                        self.c1_off, C1_STRIDE, C1_NREP, C1_STRIDE)
         else:
             K.sgd_flat(self.params, self.grads, self.m, self.lr, self.momentum, 0.0, self.wd, False, scale,
-                       self.counters, self.arrive, 2, self.pack_off, self.Wt2)
+                       self.counters, self.arrive, -1, self.pack_off, self.Wt2,
+                       self.c1_off, C1_STRIDE, C1_NREP, C1_STRIDE)
 
     def _batch_size_at(self, b: int) -> int:
         return self.B if b < self.nfull else self.tail
@@ -211,18 +224,17 @@ class LeNetTrainStep:
         H1 = torch.empty(bs * 500, device=self.device)
         for s in range(0, n, bs):
             B = min(bs, n - s)
-            K.lenet_conv1_fwd(X[s:s + B], None, None, 0, 0, None, B, p["conv1.weight"], p["conv1.bias"], P1, A1,
-                              None, None, None)
-            K.lenet_conv2_fwd(P1, B, self.Wt2, p["conv2.bias"], P2, A2)
-            K.lenet_fc1_fwd(P2, B, p["fc1.weight"], p["fc1.bias"], H1)
+            K.lenet_conv_fwd(X[s:s + B], None, None, 0, 0, None, B, p["conv1.weight"], p["conv1.bias"], self.Wt2,
+                             p["conv2.bias"], P1, A1, P2, A2, None, None, None)
+            K.lenet_fc1_fwd(P2, B, p["fc1.weight"], p["fc1.bias"], H1, None)
             K.lenet_head(H1, B, p["fc2.weight"], p["fc2.bias"], Y[s:s + B], 1.0 / B, None, None, None,
-                         self.eval_loss, self.eval_correct)
+                         None, None, self.eval_loss, self.eval_correct)
         return float(self.eval_loss.item()), int(self.eval_correct.item()), n
 
     # ------------------------------------------------------------------ optimizer state (torch format)
     def optimizer_state_dict(self):
         """``torch.optim.Adam.state_dict()``-compatible dict (params indexed in registration order)."""
-        names = [n for n, _ in self.net.named_parameters()]
+        names = list(self.layout.param_names)
         step = float(self.counters[0].item())
         state = {}
         for i, n in enumerate(names):

@@ -2,7 +2,7 @@
 
 ``Net.forward`` (/root/reference/mnist/main.py:139-147) is
   relu(conv1) -> maxpool2 -> relu(conv2) -> maxpool2 -> view(-1, 800) -> relu(fc1) -> fc2 -> log_softmax
-and is executed here by the fused kernels of ``csrc/kernels/lenet.hip`` (4 launches forward,
+and is executed here by the fused kernels of ``csrc/kernels/lenet.hip`` (3 launches forward,
 3 backward).  The function returns log-probabilities exactly like the reference model, so any loss
 can follow it; the training engine (``engine/lenet.py``) additionally fuses the loss and runs the
 whole step without autograd.
@@ -51,14 +51,13 @@ class LeNetFunction(torch.autograd.Function):
         if xf.dtype != torch.float32:
             raise TypeError("LeNet fused path is fp32 (the reference model's dtype)")
         pack_conv2_weight(w2c, ws.Wt2)
-        K.lenet_conv1_fwd(xf, None, None, 0, 0, None, B, w1c.detach().contiguous(), b1c.detach().contiguous(),
-                          ws.P1, ws.A1, None, None, None)
-        K.lenet_conv2_fwd(ws.P1, B, ws.Wt2, b2c.detach().contiguous(), ws.P2, ws.A2)
-        K.lenet_fc1_fwd(ws.P2, B, w1f.detach().contiguous(), b1f.detach().contiguous(), ws.H1)
+        K.lenet_conv_fwd(xf, None, None, 0, 0, None, B, w1c.detach().contiguous(), b1c.detach().contiguous(), ws.Wt2,
+                         b2c.detach().contiguous(), ws.P1, ws.A1, ws.P2, ws.A2, None, None, None)
+        K.lenet_fc1_fwd(ws.P2, B, w1f.detach().contiguous(), b1f.detach().contiguous(), ws.H1, None)
         logp = torch.empty(B, 10, device=dev, dtype=torch.float32)
         dummy = torch.zeros(B, device=dev, dtype=torch.long)
         K.lenet_head(ws.H1, B, w2f.detach().contiguous(), b2f.detach().contiguous(), dummy, 1.0 / B, logp,
-                     None, None, None, None)
+                     None, None, None, None, None, None)
         ctx.ws = ws
         ctx.save_for_backward(xf, w2c, w1f, w2f, logp)
         ctx.x_needs_grad = x.requires_grad
@@ -82,7 +81,8 @@ class LeNetFunction(torch.autograd.Function):
             views.append(grads[o:o + n].view(shp))
             o += n
         gw1c, gb1c, gw2c, gb2c, gw1f, gb1f, gw2f, gb2f = views
-        K.lenet_fc_bwd(ws.P2, ws.H1, ws.dZ1, ws.dZ2, w1f.detach().contiguous(), B, ws.dP2m, gw1f, gb1f, gw2f, gb2f)
+        K.lenet_fc_bwd(ws.P2, ws.H1, ws.dZ1, ws.dZ2, w1f.detach().contiguous(), B, ws.dP2m, gw1f, gb1f, gw2f, gb2f,
+                       None, None, None, None)
         K.lenet_conv_bwd(xf, ws.rows, ws.P1, ws.A1, ws.dP2m, ws.A2, w2c.detach().contiguous(), B, gw1c, gb1c, gw2c,
                          gb2c)
         return None, gw1c, gb1c, gw2c, gb2c, gw1f, gb1f, gw2f, gb2f

@@ -25,9 +25,14 @@ class Slot:
 
 
 class FlatLayout:
+    """``extra_shapes`` are non-parameter gradient slots (e.g. atomic-contention replicas) that take
+    part in the buckets (and therefore in the all-reduce) but are never bound to a parameter."""
+
     def __init__(self, named_shapes: Sequence[Tuple[str, Tuple[int, ...]]], buckets: Sequence[Sequence[str]],
-                 align: int = ALIGN):
+                 align: int = ALIGN, extra_shapes: Dict[str, Tuple[int, ...]] | None = None):
         shapes = dict(named_shapes)
+        self.param_names = list(shapes)
+        shapes.update(extra_shapes or {})
         seen = [n for b in buckets for n in b]
         if sorted(seen) != sorted(shapes):
             raise ValueError("buckets must partition the parameter set exactly")
@@ -61,6 +66,8 @@ class FlatLayout:
         flat_p = torch.zeros(self.total, device=dev, dtype=dtype)
         flat_g = torch.zeros(self.total, device=dev, dtype=dtype)
         for n, s in self.slots.items():
+            if n not in self.param_names:
+                continue
             p = params[n]
             v = flat_p[s.offset: s.offset + s.numel].view(s.shape)
             v.copy_(p.detach())

@@ -26,7 +26,6 @@ def _close(a, b, rtol, atol, what):
     assert err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (ref scale {scale:.3e})"
 
 
-@pytest.mark.parametrize("B", [1, 16, 48, 76, 96, 128, 200])
 def _mostly_close(a, b, mean_tol, max_tol, what):
     """Adam normalises each gradient element (g/sqrt(v)), so elements whose gradient is ~0 can move
     by up to 2*lr on rounding noise alone; compare the bulk tightly and bound the worst case."""
@@ -35,6 +34,7 @@ def _mostly_close(a, b, mean_tol, max_tol, what):
     assert d.max().item() <= max_tol, f"{what}: max abs diff {d.max().item():.3e}"
 
 
+@pytest.mark.parametrize("B", [1, 16, 48, 76, 96, 128, 200])
 def test_forward_matches_torch(B):
     net = build_net(seed=1, device=DEV)
     ref = torch_twin(net)
