@@ -43,6 +43,27 @@ hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, f
 hipError_t pde_lenet_pack_w2(const float* w2, float* dst, hipStream_t st);
 hipError_t pde_scale(float* x, long long n, float s, hipStream_t st);
 
+// ---- generic ops: csrc/kernels/generic.hip ----
+hipError_t pde_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int lda,
+                        int ldb, int ldc, int transA, int transB, long long sA, long long sB, long long sC, int batch,
+                        float alpha, float beta, int bias_mode, int relu, int atomic, hipStream_t st);
+hipError_t pde_xent_fwd(const float* x, const long long* y, int B, int C, float* row_loss, float* lse, hipStream_t st);
+hipError_t pde_xent_bwd(const float* x, const long long* y, const float* lse, const float* gscale, int per_row,
+                        float mul, int B, int C, float* dx, hipStream_t st);
+hipError_t pde_log_softmax_fwd(const float* x, int B, int C, float* out, hipStream_t st);
+hipError_t pde_log_softmax_bwd(const float* out, const float* g, int B, int C, float* dx, hipStream_t st);
+hipError_t pde_relu_fwd(const float* x, float* y, long long n, hipStream_t st);
+hipError_t pde_relu_bwd(const float* y, const float* g, float* dx, long long n, hipStream_t st);
+hipError_t pde_pool2_fwd(const float* x, int NC, int H, int W, float* y, uint8_t* code, hipStream_t st);
+hipError_t pde_pool2_bwd(const float* g, const uint8_t* code, int NC, int H, int W, float* dx, hipStream_t st);
+hipError_t pde_im2col(const float* x, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int OH, int OW,
+                      float* col, hipStream_t st);
+hipError_t pde_col2im(const float* col, int B, int C, int H, int W, int KH, int KW, int stride, int pad, int OH,
+                      int OW, float* dx, hipStream_t st);
+hipError_t pde_bias_grad_nchw(const float* dy, int B, int O, long long P, float* db, hipStream_t st);
+hipError_t pde_colsum(const float* x, int M, int N, float* out, hipStream_t st);
+hipError_t pde_gather_rows(const float* src, const long long* idx, int n, int row_floats, float* out, hipStream_t st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -230,6 +230,138 @@ void scale_(const at::Tensor& x, double s) {
   hip_check(pde_scale(ptr<float>(x), x.numel(), (float)s, cur_stream()), "scale_");
 }
 
+// ------------------------------------------------------------------------------------------------
+// generic ops
+void gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, const OptT& bias, int64_t M, int64_t N,
+          int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool transA, bool transB, int64_t sA, int64_t sB,
+          int64_t sC, int64_t batch, double alpha, double beta, int64_t bias_mode, bool relu, bool atomic) {
+  check_cuda(A, "A", F32);
+  check_cuda(B, "B", F32);
+  check_cuda(C, "C", F32);
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && batch > 0, "empty gemm");
+  const int64_t needA = (batch - 1) * sA + (transA ? (K - 1) * lda + M : (M - 1) * lda + K);
+  const int64_t needB = (batch - 1) * sB + (transB ? (N - 1) * ldb + K : (K - 1) * ldb + N);
+  const int64_t needC = (batch - 1) * sC + (M - 1) * ldc + N;
+  TORCH_CHECK(A.numel() >= needA && B.numel() >= needB && C.numel() >= needC, "gemm operand too small");
+  const float* bp = optr<float>(bias, "bias", F32, bias_mode == 1 ? N : (bias_mode == 2 ? M : 0));
+  TORCH_CHECK(bias_mode == 0 || bp, "bias_mode needs a bias");
+  hip_check(pde_gemm_f32(ptr<float>(A), ptr<float>(B), ptr<float>(C), bp, (int)M, (int)N, (int)K, (int)lda, (int)ldb,
+                         (int)ldc, transA, transB, sA, sB, sC, (int)batch, (float)alpha, (float)beta, (int)bias_mode,
+                         relu, atomic, cur_stream()),
+            "gemm");
+}
+
+void xent_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& row_loss, const at::Tensor& lse) {
+  check_cuda(x, "logits", F32);
+  TORCH_CHECK(x.dim() == 2, "logits must be [B, C]");
+  const int64_t B = x.size(0), C = x.size(1);
+  check_cuda(y, "target", I64, B);
+  check_cuda(row_loss, "row_loss", F32, B);
+  check_cuda(lse, "lse", F32, B);
+  hip_check(pde_xent_fwd(ptr<float>(x), ptr<long long>(y), (int)B, (int)C, ptr<float>(row_loss), ptr<float>(lse),
+                         cur_stream()),
+            "xent_fwd");
+}
+
+void xent_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& lse, const at::Tensor& gscale, bool per_row,
+              double mul, const at::Tensor& dx) {
+  check_cuda(x, "logits", F32);
+  const int64_t B = x.size(0), C = x.size(1);
+  check_cuda(y, "target", I64, B);
+  check_cuda(lse, "lse", F32, B);
+  check_cuda(gscale, "grad", F32, per_row ? B : 1);
+  check_cuda(dx, "dx", F32, B * C);
+  hip_check(pde_xent_bwd(ptr<float>(x), ptr<long long>(y), ptr<float>(lse), ptr<float>(gscale), per_row, (float)mul,
+                         (int)B, (int)C, ptr<float>(dx), cur_stream()),
+            "xent_bwd");
+}
+
+void log_softmax_fwd(const at::Tensor& x, const at::Tensor& out) {
+  check_cuda(x, "x", F32);
+  TORCH_CHECK(x.dim() == 2, "log_softmax kernel takes [B, C] (dim=1)");
+  check_cuda(out, "out", F32, x.numel());
+  hip_check(pde_log_softmax_fwd(ptr<float>(x), (int)x.size(0), (int)x.size(1), ptr<float>(out), cur_stream()),
+            "log_softmax_fwd");
+}
+
+void log_softmax_bwd(const at::Tensor& out, const at::Tensor& g, const at::Tensor& dx) {
+  check_cuda(out, "out", F32);
+  check_cuda(g, "grad", F32, out.numel());
+  check_cuda(dx, "dx", F32, out.numel());
+  hip_check(pde_log_softmax_bwd(ptr<float>(out), ptr<float>(g), (int)out.size(0), (int)out.size(1), ptr<float>(dx),
+                                cur_stream()),
+            "log_softmax_bwd");
+}
+
+void relu_fwd(const at::Tensor& x, const at::Tensor& y) {
+  check_cuda(x, "x", F32);
+  check_cuda(y, "y", F32, x.numel());
+  hip_check(pde_relu_fwd(ptr<float>(x), ptr<float>(y), x.numel(), cur_stream()), "relu_fwd");
+}
+
+void relu_bwd(const at::Tensor& y, const at::Tensor& g, const at::Tensor& dx) {
+  check_cuda(y, "y", F32);
+  check_cuda(g, "grad", F32, y.numel());
+  check_cuda(dx, "dx", F32, y.numel());
+  hip_check(pde_relu_bwd(ptr<float>(y), ptr<float>(g), ptr<float>(dx), y.numel(), cur_stream()), "relu_bwd");
+}
+
+void pool2_fwd(const at::Tensor& x, int64_t NC, int64_t H, int64_t W, const at::Tensor& y, const at::Tensor& code) {
+  check_cuda(x, "x", F32, NC * H * W);
+  check_cuda(y, "y", F32, NC * (H / 2) * (W / 2));
+  check_cuda(code, "code", U8, NC * (H / 2) * (W / 2));
+  hip_check(pde_pool2_fwd(ptr<float>(x), (int)NC, (int)H, (int)W, ptr<float>(y), ptr<uint8_t>(code), cur_stream()),
+            "pool2_fwd");
+}
+
+void pool2_bwd(const at::Tensor& g, const at::Tensor& code, int64_t NC, int64_t H, int64_t W, const at::Tensor& dx) {
+  check_cuda(g, "grad", F32, NC * (H / 2) * (W / 2));
+  check_cuda(code, "code", U8, NC * (H / 2) * (W / 2));
+  check_cuda(dx, "dx", F32, NC * H * W);
+  hip_check(pde_pool2_bwd(ptr<float>(g), ptr<uint8_t>(code), (int)NC, (int)H, (int)W, ptr<float>(dx), cur_stream()),
+            "pool2_bwd");
+}
+
+void im2col(const at::Tensor& x, int64_t B, int64_t C, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t stride,
+            int64_t pad, int64_t OH, int64_t OW, const at::Tensor& col) {
+  check_cuda(x, "x", F32, B * C * H * W);
+  check_cuda(col, "col", F32, B * C * KH * KW * OH * OW);
+  hip_check(pde_im2col(ptr<float>(x), (int)B, (int)C, (int)H, (int)W, (int)KH, (int)KW, (int)stride, (int)pad, (int)OH,
+                       (int)OW, ptr<float>(col), cur_stream()),
+            "im2col");
+}
+
+void col2im(const at::Tensor& col, int64_t B, int64_t C, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t stride,
+            int64_t pad, int64_t OH, int64_t OW, const at::Tensor& dx) {
+  check_cuda(col, "col", F32, B * C * KH * KW * OH * OW);
+  check_cuda(dx, "dx", F32, B * C * H * W);
+  hip_check(pde_col2im(ptr<float>(col), (int)B, (int)C, (int)H, (int)W, (int)KH, (int)KW, (int)stride, (int)pad,
+                       (int)OH, (int)OW, ptr<float>(dx), cur_stream()),
+            "col2im");
+}
+
+void bias_grad_nchw(const at::Tensor& dy, int64_t B, int64_t O, int64_t P, const at::Tensor& db) {
+  check_cuda(dy, "dy", F32, B * O * P);
+  check_cuda(db, "db", F32, O);
+  hip_check(pde_bias_grad_nchw(ptr<float>(dy), (int)B, (int)O, P, ptr<float>(db), cur_stream()), "bias_grad_nchw");
+}
+
+void colsum(const at::Tensor& x, int64_t M, int64_t N, const at::Tensor& out) {
+  check_cuda(x, "x", F32, M * N);
+  check_cuda(out, "out", F32, N);
+  hip_check(pde_colsum(ptr<float>(x), (int)M, (int)N, ptr<float>(out), cur_stream()), "colsum");
+}
+
+void gather_rows(const at::Tensor& src, const at::Tensor& idx, const at::Tensor& out) {
+  check_cuda(src, "src", F32);
+  check_cuda(idx, "idx", I64);
+  check_cuda(out, "out", F32);
+  const int64_t n = idx.numel(), row = src.numel() / std::max<int64_t>(1, src.size(0));
+  TORCH_CHECK(out.numel() >= n * row && row % 4 == 0, "gather_rows: bad sizes");
+  hip_check(pde_gather_rows(ptr<float>(src), ptr<long long>(idx), (int)n, (int)row, ptr<float>(out), cur_stream()),
+            "gather_rows");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_kernels, m) {
@@ -259,4 +391,22 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0);
   m.def("lenet_pack_w2", &lenet_pack_w2);
   m.def("scale_", &scale_);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("transA") = false,
+        py::arg("transB") = false, py::arg("sA") = 0, py::arg("sB") = 0, py::arg("sC") = 0, py::arg("batch") = 1,
+        py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("bias_mode") = 0, py::arg("relu") = false,
+        py::arg("atomic") = false);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("log_softmax_fwd", &log_softmax_fwd);
+  m.def("log_softmax_bwd", &log_softmax_bwd);
+  m.def("relu_fwd", &relu_fwd);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("pool2_fwd", &pool2_fwd);
+  m.def("pool2_bwd", &pool2_bwd);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im);
+  m.def("bias_grad_nchw", &bias_grad_nchw);
+  m.def("colsum", &colsum);
+  m.def("gather_rows", &gather_rows);
 }

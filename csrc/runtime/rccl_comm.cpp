@@ -1,0 +1,182 @@
+// RCCL communicator: see rccl_comm.h.
+#include "rccl_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace pde {
+
+namespace {
+
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
+}
+
+// framework dtype codes (same numbering as hostcomm.h DType)
+ncclDataType_t to_nccl_dtype(int d) {
+  switch (d) {
+    case 0: return ncclFloat32;
+    case 1: return ncclFloat64;
+    case 2: return ncclInt32;
+    case 3: return ncclInt64;
+    case 4: return ncclUint8;
+    case 5: return ncclInt8;
+    case 6: return ncclBfloat16;
+    case 7: return ncclFloat16;
+    case 8: return ncclUint8;
+  }
+  throw std::invalid_argument("dtype not supported by RCCL");
+}
+
+size_t nccl_size(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    default: return 8;
+  }
+}
+
+ncclRedOp_t to_nccl_op(int op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclProd;
+    case 2: return ncclMin;
+    case 3: return ncclMax;
+    case 4: return ncclAvg;
+  }
+  throw std::invalid_argument("reduce op not supported by RCCL (bitwise ops are host-only)");
+}
+
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+void* P(uintptr_t p) { return reinterpret_cast<void*>(p); }
+
+}  // namespace
+
+std::string RcclComm::make_unique_id() {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+int RcclComm::version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+RcclComm::RcclComm(const std::string& unique_id, int rank, int world, int device)
+    : rank_(rank), world_(world), device_(device) {
+  if (unique_id.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("bad RCCL unique id");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id.data(), sizeof(id));
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  nccl_check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+RcclComm::RcclComm(ncclComm_t c, int device) : comm_(c), device_(device) {
+  nccl_check(ncclCommUserRank(c, &rank_), "ncclCommUserRank");
+  nccl_check(ncclCommCount(c, &world_), "ncclCommCount");
+}
+
+RcclComm::~RcclComm() {
+  try {
+    destroy();
+  } catch (...) {
+  }
+}
+
+void RcclComm::check_open() const {
+  if (!comm_) throw std::runtime_error("RCCL communicator is destroyed or aborted");
+}
+
+void RcclComm::all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclAllReduce(P(send), P(recv), (size_t)count, to_nccl_dtype(dtype), to_nccl_op(op), comm_, S(stream)),
+             "ncclAllReduce");
+}
+
+void RcclComm::broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclBroadcast(P(send), P(recv), (size_t)count, to_nccl_dtype(dtype), root, comm_, S(stream)),
+             "ncclBroadcast");
+}
+
+void RcclComm::reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, int root, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclReduce(P(send), P(recv), (size_t)count, to_nccl_dtype(dtype), to_nccl_op(op), root, comm_, S(stream)),
+             "ncclReduce");
+}
+
+void RcclComm::all_gather(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclAllGather(P(send), P(recv), (size_t)count, to_nccl_dtype(dtype), comm_, S(stream)), "ncclAllGather");
+}
+
+void RcclComm::reduce_scatter(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclReduceScatter(P(send), P(recv), (size_t)count, to_nccl_dtype(dtype), to_nccl_op(op), comm_,
+                               S(stream)),
+             "ncclReduceScatter");
+}
+
+void RcclComm::all_to_all(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream) {
+  check_open();
+  const ncclDataType_t t = to_nccl_dtype(dtype);
+  const size_t bytes = (size_t)count * nccl_size(t);
+  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  for (int p = 0; p < world_; ++p) {
+    nccl_check(ncclSend((const char*)P(send) + p * bytes, (size_t)count, t, p, comm_, S(stream)), "ncclSend");
+    nccl_check(ncclRecv((char*)P(recv) + p * bytes, (size_t)count, t, p, comm_, S(stream)), "ncclRecv");
+  }
+  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+void RcclComm::send(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclSend(P(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, S(stream)), "ncclSend");
+}
+
+void RcclComm::recv(uintptr_t buf, int64_t count, int dtype, int peer, uintptr_t stream) {
+  check_open();
+  nccl_check(ncclRecv(P(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, S(stream)), "ncclRecv");
+}
+
+void RcclComm::group_start() { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+void RcclComm::group_end() { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); }
+
+std::shared_ptr<RcclComm> RcclComm::split(int color, int key) {
+  check_open();
+  ncclComm_t out = nullptr;
+  nccl_check(ncclCommSplit(comm_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &out, nullptr), "ncclCommSplit");
+  if (!out) return nullptr;
+  return std::shared_ptr<RcclComm>(new RcclComm(out, device_));
+}
+
+void RcclComm::abort() {
+  if (comm_) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
+void RcclComm::destroy() {
+  if (comm_) {
+    ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+}
+
+std::string RcclComm::async_error() {
+  if (!comm_) return "destroyed";
+  ncclResult_t r = ncclSuccess;
+  ncclCommGetAsyncError(comm_, &r);
+  return r == ncclSuccess ? "" : ncclGetErrorString(r);
+}
+
+}  // namespace pde

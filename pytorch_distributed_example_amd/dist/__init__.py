@@ -1,3 +1,9 @@
-"""torch.distributed-compatible process-group API over the framework's C++ runtime (WIP)."""
-def is_initialized():
-    return False
+"""torch.distributed-compatible process-group API over the framework's C++ runtime
+(TCP rendezvous store, host TCP collectives, RCCL over xGMI).  See ``dist/api.py``."""
+from .api import (  # noqa: F401
+    Backend, DEFAULT_TIMEOUT, EngineComm, GroupMember, ProcessGroup, ReduceOp, Work, all_gather,
+    all_gather_into_tensor, all_reduce, all_to_all_single, barrier, broadcast, broadcast_parameters,
+    destroy_process_group, engine_comm, gather, get_backend, get_default_group, get_rank, get_world_size,
+    init_process_group, irecv, is_available, is_initialized, isend, new_group, recv, reduce, reduce_op,
+    reduce_scatter, reduce_scatter_tensor, scatter, send,
+)

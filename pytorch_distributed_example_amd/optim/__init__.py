@@ -1,0 +1,2 @@
+"""Fused optimizers (one HIP launch per step over a flat buffer), torch.optim-compatible state."""
+from .fused import SGD, Adam, AdamW  # noqa: F401

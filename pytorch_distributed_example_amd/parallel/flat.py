@@ -59,9 +59,11 @@ class FlatLayout:
             buckets = reverse_order_buckets(named, bucket_cap_bytes or (25 << 20))
         return cls(named, buckets)
 
-    def bind(self, module: torch.nn.Module, device=None, dtype=torch.float32):
-        """Move ``module``'s parameters into flat storage; returns (flat_params, flat_grads)."""
-        params = dict(module.named_parameters())
+    def bind(self, module, device=None, dtype=torch.float32):
+        """Move parameters (a module or a {name: param} dict) into flat storage; returns
+        (flat_params, flat_grads).  Each parameter is tagged ``p._pde_flat = (layout, flat_params,
+        flat_grads, name)`` so DDP and the fused optimizers can share one buffer."""
+        params = dict(module.named_parameters()) if isinstance(module, torch.nn.Module) else dict(module)
         dev = device or next(iter(params.values())).device
         flat_p = torch.zeros(self.total, device=dev, dtype=dtype)
         flat_g = torch.zeros(self.total, device=dev, dtype=dtype)
@@ -73,6 +75,7 @@ class FlatLayout:
             v.copy_(p.detach())
             p.data = v
             p.grad = flat_g[s.offset: s.offset + s.numel].view(s.shape)
+            p._pde_flat = (self, flat_p, flat_g, n)
         return flat_p, flat_g
 
     def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
@@ -101,3 +104,21 @@ def reverse_order_buckets(named_shapes, cap_bytes: int, elem_bytes: int = 4):
     if cur:
         buckets.append(cur)
     return buckets
+
+
+def shared_flat(params):
+    """If every parameter in ``params`` is bound to the same flat buffer (and it covers exactly
+    them), return (layout, flat_params, flat_grads); else None."""
+    tags = [getattr(p, "_pde_flat", None) for p in params]
+    if not tags or any(t is None for t in tags):
+        return None
+    layout, fp, fg = tags[0][0], tags[0][1], tags[0][2]
+    if any(t[0] is not layout for t in tags):
+        return None
+    if sorted(t[3] for t in tags) != sorted(layout.param_names):
+        return None
+    for p, t in zip(params, tags):
+        s = layout.slots[t[3]]
+        if p.data_ptr() != fp[s.offset:].data_ptr():
+            return None
+    return layout, fp, fg

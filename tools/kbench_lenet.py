@@ -73,17 +73,32 @@ def main():
         "adam": lambda: K.adam_flat(e.params, e.grads, e.m, e.v, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1.0, e.counters,
                                     e.arrive, -1, e.pack_off, e.Wt2, e.c1_off, 576, 16, 576),
     }
+    # graph mode: G launches of a variant captured in one hipGraph -> GPU-side cost per launch
+    # (kernel + boundary), free of the ~4 us host launch overhead of eager Python launches
+    G = int(os.environ.get("KB_G", "20"))
+    graphs = {}
+    for name, fn in variants.items():
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            fn()
+        torch.cuda.current_stream().wait_stream(st)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(G):
+                fn()
+        graphs[name] = gr
     res = {k: [] for k in variants}
     for r in range(R):
-        for name, fn in variants.items():
-            fn()
+        for name, gr in graphs.items():
+            gr.replay()
             s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            for _ in range(N):
-                fn()
+            for _ in range(max(1, N // G)):
+                gr.replay()
             t.record()
             torch.cuda.synchronize()
-            res[name].append(s.elapsed_time(t) * 1e3 / N)
+            res[name].append(s.elapsed_time(t) * 1e3 / (max(1, N // G) * G))
     out = {k: {"median_us": sorted(v)[len(v) // 2], "min_us": min(v)} for k, v in res.items()}
     for k, v in out.items():
         print(f"{k:32s} median {v['median_us']:8.2f} us   min {v['min_us']:8.2f} us")
