@@ -49,8 +49,11 @@ class DistributedDataParallel(nn.Module):
                  static_graph: bool = False, init_sync: bool = True):
         super().__init__()
         self.module = module
-        self.process_group = process_group if process_group is not None else dist.get_default_group()
-        self.world_size = dist.get_world_size(self.process_group)
+        if process_group is None and not dist.is_initialized():
+            self.process_group, self.world_size = None, 1      # single process: flat grads, no comm
+        else:
+            self.process_group = process_group if process_group is not None else dist.get_default_group()
+            self.world_size = dist.get_world_size(self.process_group)
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True
         self.find_unused_parameters = find_unused_parameters
@@ -61,7 +64,7 @@ class DistributedDataParallel(nn.Module):
         if len(dtypes) != 1:
             raise NotImplementedError("all parameters must share one device and dtype")
         self.device = named[0][1].device
-        if init_sync:
+        if init_sync and self.world_size > 1:
             dist.broadcast_parameters(module, src=self.process_group.ranks[0], group=self.process_group,
                                       buffers=True)
         shapes = [(n, tuple(p.shape)) for n, p in named]

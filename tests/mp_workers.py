@@ -1,0 +1,261 @@
+"""Worker bodies for the multi-process tests (one process per rank, started by ``launch.run_gang``).
+
+Run as ``python tests/mp_workers.py <case> [args]`` with RANK / WORLD_SIZE / MASTER_* in the
+environment, exactly like a real job.  A case raises (non-zero exit) on any mismatch; results that
+the parent test compares across ranks are printed as ``RESULT <json>`` lines.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import warnings
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_distributed_example_amd import dist  # noqa: E402
+
+R = int(os.environ.get("RANK", 0))
+W = int(os.environ.get("WORLD_SIZE", 1))
+
+
+def emit(obj):
+    print("RESULT " + json.dumps(obj), flush=True)
+
+
+def _init(backend="gloo", method="env://"):
+    if method == "tcp":
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{os.environ['MASTER_PORT']}", rank=R,
+                                world_size=W)
+    else:
+        dist.init_process_group(backend, init_method="env://")
+    assert dist.is_initialized() and dist.get_rank() == R and dist.get_world_size() == W
+
+
+def _dev(backend):
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+DTYPES = [torch.float32, torch.float64, torch.int32, torch.int64, torch.uint8, torch.int8, torch.bfloat16,
+          torch.float16]
+
+
+def case_collectives(backend="gloo", method="env"):
+    _init(backend, method)
+    dev = _dev(backend)
+    # all_reduce: every dtype x op, small (direct) and large (ring) payloads
+    for n in (7, 100_003):
+        for dt in DTYPES:
+            base = (torch.arange(n, dtype=torch.float64) % 5 + 1)
+            x = (base * (R + 1)).to(dt).to(dev)
+            y = x.clone()
+            dist.all_reduce(y, op=dist.ReduceOp.SUM)
+            ref = sum((base * (r + 1)).to(dt).double() for r in range(W))
+            tol = 0.0 if not dt.is_floating_point else (2e-2 if dt in (torch.bfloat16, torch.float16) else 1e-6)
+            if dt == torch.uint8 or dt == torch.int8:
+                ref = ref.to(torch.int64).to(dt).double()  # wrap-around like the wire type
+            assert torch.allclose(y.double().cpu(), ref, rtol=tol, atol=tol), (n, dt)
+            if dt.is_floating_point:
+                for op, f in ((dist.ReduceOp.MAX, torch.maximum), (dist.ReduceOp.MIN, torch.minimum)):
+                    z = x.clone()
+                    dist.all_reduce(z, op=op)
+                    r0 = (base * 1).to(dt).double()
+                    rw = (base * W).to(dt).double()
+                    exp = f(r0, rw)
+                    assert torch.allclose(z.double().cpu(), exp, rtol=tol, atol=tol), (n, dt, op)
+    # AVG / PRODUCT
+    x = torch.full((33,), float(R + 1), device=dev)
+    dist.all_reduce(x, op=dist.ReduceOp.AVG)
+    assert torch.allclose(x.cpu(), torch.full((33,), (W + 1) / 2.0))
+    x = torch.full((5,), float(R + 1), device=dev, dtype=torch.float64)
+    dist.all_reduce(x, op=dist.ReduceOp.PRODUCT)
+    assert torch.allclose(x.cpu(), torch.full((5,), float(torch.arange(1, W + 1).prod())).double())
+    # bitwise ops on ints
+    x = torch.tensor([1 << R], device=dev, dtype=torch.int64)
+    dist.all_reduce(x, op=dist.ReduceOp.BOR)
+    assert int(x) == (1 << W) - 1
+    # broadcast from each root
+    for src in range(W):
+        t = torch.arange(1000, device=dev, dtype=torch.float32) * (R + 1)
+        dist.broadcast(t, src=src)
+        assert torch.equal(t.cpu(), torch.arange(1000, dtype=torch.float32) * (src + 1))
+    # all_gather (list + into_tensor)
+    t = torch.full((4, 3), float(R), device=dev)
+    outs = [torch.empty_like(t) for _ in range(W)]
+    dist.all_gather(outs, t)
+    for r in range(W):
+        assert torch.equal(outs[r].cpu(), torch.full((4, 3), float(r)))
+    big = torch.empty(W * 4, 3, device=dev)
+    dist.all_gather_into_tensor(big, t)
+    assert torch.equal(big.cpu(), torch.cat([torch.full((4, 3), float(r)) for r in range(W)]))
+    # reduce_scatter_tensor: rank r gets sum over ranks of chunk r
+    inp = torch.cat([torch.full((6,), float(10 * c + R)) for c in range(W)]).to(dev)
+    out = torch.empty(6, device=dev)
+    dist.reduce_scatter_tensor(out, inp)
+    assert torch.allclose(out.cpu(), torch.full((6,), float(10 * R * W + sum(range(W)))))
+    out2 = torch.empty(6, device=dev)
+    dist.reduce_scatter(out2, list(inp.chunk(W)))
+    assert torch.allclose(out2.cpu(), out.cpu())
+    # reduce to each dst
+    for dst in range(W):
+        t = torch.full((9,), float(R + 1), device=dev)
+        dist.reduce(t, dst=dst)
+        if R == dst:
+            assert torch.allclose(t.cpu(), torch.full((9,), W * (W + 1) / 2.0))
+    # gather / scatter
+    t = torch.full((2,), float(R), device=dev)
+    gl = [torch.empty(2, device=dev) for _ in range(W)] if R == 0 else None
+    dist.gather(t, gl, dst=0)
+    if R == 0:
+        assert [float(g[0]) for g in gl] == [float(r) for r in range(W)]
+    sl = [torch.full((3,), float(100 + r), device=dev) for r in range(W)] if R == W - 1 else None
+    s = torch.empty(3, device=dev)
+    dist.scatter(s, sl, src=W - 1)
+    assert torch.equal(s.cpu(), torch.full((3,), float(100 + R)))
+    # all_to_all_single: rank r sends value 100*r + j to rank j
+    inp = torch.tensor([100.0 * R + j for j in range(W) for _ in range(2)], device=dev)
+    out = torch.empty_like(inp)
+    dist.all_to_all_single(out, inp)
+    assert out.cpu().tolist() == [100.0 * j + R for j in range(W) for _ in range(2)]
+    # send / recv ring, isend / irecv
+    nxt, prv = (R + 1) % W, (R - 1) % W
+    s = torch.full((17,), float(R), device=dev)
+    r_ = torch.empty(17, device=dev)
+    if R % 2 == 0:
+        dist.send(s, nxt)
+        dist.recv(r_, prv)
+    else:
+        dist.recv(r_, prv)
+        dist.send(s, nxt)
+    assert torch.equal(r_.cpu(), torch.full((17,), float(prv)))
+    w1 = dist.isend(s * 2, nxt)
+    w2 = dist.irecv(r_, prv)
+    w1.wait()
+    w2.wait()
+    assert torch.equal(r_.cpu(), torch.full((17,), float(2 * prv)))
+    # async all_reduce
+    t = torch.ones(50_000, device=dev)
+    work = dist.all_reduce(t, async_op=True)
+    work.wait()
+    assert torch.allclose(t.cpu(), torch.full((50_000,), float(W)))
+    dist.barrier()
+    emit({"rank": R, "ok": True})
+    dist.destroy_process_group()
+
+
+def case_groups(backend="gloo"):
+    _init(backend)
+    dev = _dev(backend)
+    # the reference's toy pattern: new_group over all ranks every step + deprecated reduce_op
+    with warnings.catch_warnings(record=True) as wlog:
+        warnings.simplefilter("always")
+        for step in range(3):
+            g = dist.new_group(ranks=list(range(W)))
+            t = torch.IntTensor([R + step]).to(dev)
+            dist.all_reduce(t, op=dist.reduce_op.SUM, group=g)
+            assert int(t) == sum(range(W)) + W * step
+    assert any(issubclass(w.category, FutureWarning) for w in wlog)
+    # a strict subgroup: even ranks
+    evens = list(range(0, W, 2))
+    g = dist.new_group(ranks=evens)
+    if R in evens:
+        t = torch.tensor([float(R)], device=dev)
+        dist.all_reduce(t, group=g)
+        assert float(t) == float(sum(evens))
+        assert dist.get_world_size(g) == len(evens) and dist.get_rank(g) == evens.index(R)
+    else:
+        assert dist.get_rank(g) == -1
+    emit({"rank": R, "ok": True})
+    dist.destroy_process_group()
+
+
+def case_ddp(backend="gloo", bucket_mb="0.05", steps="4"):
+    """DDP over W ranks on a shard of a fixed global batch == single-process full-batch training."""
+    from pytorch_distributed_example_amd.models import build_net
+    from pytorch_distributed_example_amd.optim import Adam
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_example_amd import ops
+
+    _init(backend)
+    dev = _dev(backend)
+    torch.manual_seed(1234)
+    gx = torch.randn(8 * W, 1, 28, 28)
+    gy = torch.randint(0, 10, (8 * W,))
+    net = build_net(seed=7 + R, device=dev)          # deliberately different init: DDP must broadcast
+    ddp = DistributedDataParallel(net, bucket_cap_mb=float(bucket_mb))
+    opt = Adam(ddp.parameters(), lr=1e-2)
+    for _ in range(int(steps)):
+        x = gx[R * 8:(R + 1) * 8].to(dev)
+        y = gy[R * 8:(R + 1) * 8].to(dev)
+        opt.zero_grad()
+        loss = ops.cross_entropy(ddp(x), y)
+        loss.backward()
+        opt.step()
+    # no_sync: local accumulation, grads differ across ranks
+    with ddp.no_sync():
+        ops.cross_entropy(ddp(gx[R * 8:(R + 1) * 8].to(dev)), gy[R * 8:(R + 1) * 8].to(dev)).backward()
+    emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()],
+          "n_buckets": len(ddp.buckets)})
+    dist.destroy_process_group()
+
+
+def case_manual_average(backend="gloo", steps="4"):
+    """The reference's path: per-parameter all_reduce SUM / W after backward."""
+    from pytorch_distributed_example_amd.models import build_net
+    from pytorch_distributed_example_amd.optim import Adam
+    from pytorch_distributed_example_amd.parallel import average_gradients
+    from pytorch_distributed_example_amd import ops
+
+    _init(backend)
+    dev = _dev(backend)
+    torch.manual_seed(1234)
+    gx = torch.randn(8 * W, 1, 28, 28)
+    gy = torch.randint(0, 10, (8 * W,))
+    net = build_net(seed=7, device=dev)
+    opt = Adam(net.parameters(), lr=1e-2)
+    for _ in range(int(steps)):
+        opt.zero_grad()
+        ops.cross_entropy(net(gx[R * 8:(R + 1) * 8].to(dev)), gy[R * 8:(R + 1) * 8].to(dev)).backward()
+        average_gradients(net)
+        opt.step()
+    emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()]})
+    dist.destroy_process_group()
+
+
+def case_fail(backend="gloo"):
+    _init(backend)
+    if R == 1:
+        raise SystemExit(3)
+    dist.barrier()            # would hang forever without the launcher's gang termination
+
+
+def case_engine_comm(steps="3"):
+    """Fused engine with the RCCL comm path (W ranks, nccl), prints final param checksums."""
+    from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
+    from pytorch_distributed_example_amd.engine import LeNetTrainStep
+    from pytorch_distributed_example_amd.models import build_net
+
+    _init("nccl")
+    dev = _dev("nccl")
+    net = build_net(seed=3 + R, device=dev)
+    dist.broadcast_parameters(net)
+    ds = synthetic_mnist(512 * W, seed=0, device=dev)
+    eng = LeNetTrainStep(net, batch_size=64, comm=dist.engine_comm())
+    eng.bind_dataset(ds.images, ds.labels)
+    s = DistributedSampler(ds, num_replicas=W, rank=R, shuffle=False)
+    eng.set_epoch_indices(s.indices_tensor())
+    for _ in range(int(steps)):
+        eng.step()
+    torch.cuda.synchronize()
+    emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()]})
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    name = sys.argv[1]
+    globals()["case_" + name](*sys.argv[2:])

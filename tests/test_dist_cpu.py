@@ -1,0 +1,79 @@
+"""Distributed plumbing on CPU (survey §4 items 4/7): native store, host collectives, dist API,
+process groups, launcher failure handling -- W in {2, 3, 4} processes on 127.0.0.1."""
+import threading
+import time
+
+import pytest
+
+from _mp import run_ranks
+from pytorch_distributed_example_amd._ext import runtime
+from pytorch_distributed_example_amd.launch import free_port
+
+
+def test_store_basic():
+    rt = runtime()
+    srv = rt.StoreServer("127.0.0.1", 0)
+    a = rt.StoreClient("127.0.0.1", srv.port, 5000)
+    b = rt.StoreClient("127.0.0.1", srv.port, 5000)
+    a.set("k", b"v1")
+    assert b.get("k") == b"v1"
+    assert a.add("ctr", 3) == 3 and b.add("ctr", 4) == 7
+    assert b.check(["k", "ctr"]) and not b.check(["nope"])
+    got = {}
+
+    def waiter():
+        got["v"] = b.get("late")
+
+    t = threading.Thread(target=waiter)
+    t.start()
+    time.sleep(0.2)
+    a.set("late", b"x")
+    t.join(5)
+    assert got.get("v") == b"x"
+    # compare_set: missing key + empty expected -> set; wrong expected -> unchanged
+    assert a.compare_set("cas", b"", b"first") == b"first"
+    assert a.compare_set("cas", b"zzz", b"second") == b"first"
+    assert a.compare_set("cas", b"first", b"second") == b"second"
+    n = a.num_keys()
+    assert a.delete_key("k")
+    assert a.num_keys() == n - 1
+    b.timeout_ms = 300
+    with pytest.raises(Exception):
+        b.get("never-set")
+    b.timeout_ms = 5000
+    a.set("after-timeout", b"ok")
+    assert b.get("after-timeout") == b"ok"      # client recovers after a timed-out request
+    srv.stop()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collectives_env(world):
+    rc, res, logs = run_ranks("collectives", world, "gloo", "env")
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res)
+
+
+def test_collectives_tcp_w4():
+    rc, res, logs = run_ranks("collectives", 4, "gloo", "tcp")
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_groups_and_toy_pattern(world):
+    rc, res, logs = run_ranks("groups", world)
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res)
+
+
+def test_launcher_terminates_gang_on_failure():
+    t0 = time.time()
+    rc, _, logs = run_ranks("fail", 3)
+    assert rc == 3, logs
+    assert time.time() - t0 < 60
+
+
+def test_rank_none_error():
+    from pytorch_distributed_example_amd import dist
+    with pytest.raises((ValueError, TypeError), match="rank must be an integer"):
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=None, world_size=2)

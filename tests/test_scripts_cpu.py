@@ -1,0 +1,96 @@
+"""Golden-output tests for the reference-compatible CLIs (survey §4 item 7, Appendix B): the
+toy all-reduce script and the MNIST trainer on the CPU/gloo path, launched both the reference way
+(one process per rank with -i/-r/-s) and through the framework launcher."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from pytorch_distributed_example_amd.launch import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, PYTHONWARNINGS="ignore::FutureWarning", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+TOY_LINE = re.compile(r"^rank: (\d+), step: (\d+), value: (\d+), reduced sum: ([0-9.]+)\.$")
+EPOCH_LINE = re.compile(r"^Epoch: (\d+)/(\d+), train loss: ([0-9.]+), train acc: ([0-9.]+)%, "
+                        r"test loss: ([0-9.]+), test acc: ([0-9.]+)%?\.$")
+
+
+def _check_toy(lines, world, steps):
+    rows = [TOY_LINE.match(l) for l in lines]
+    rows = [tuple(map(float, m.groups())) for m in rows if m]
+    assert len(rows) == world * steps
+    for step in range(1, steps + 1):
+        at = [r for r in rows if r[1] == step]
+        assert sorted(int(r[0]) for r in at) == list(range(world))
+        assert len({r[3] for r in at}) == 1                     # every rank printed the same sum
+        assert at[0][3] == sum(r[2] for r in at)
+
+
+def test_toy_reference_style_three_shells():
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "scripts/toy.py"), "-i", f"tcp://127.0.0.1:{port}",
+                               "-r", str(r), "-s", "3", "--steps", "4", "--sleep", "0"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True, env=ENV) for r in range(3)]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert outs[0].splitlines()[0].startswith("Namespace(backend='gloo', init_method=")
+    _check_toy([l for o in outs for l in o.splitlines()], 3, 4)
+
+
+def test_toy_via_launcher():
+    out = subprocess.run([sys.executable, "-m", "pytorch_distributed_example_amd.launch", "-n", "4",
+                          os.path.join(ROOT, "scripts/toy.py"), "--steps", "3", "--sleep", "0"], cwd=ROOT,
+                         capture_output=True, text=True, env=ENV, timeout=180)
+    assert out.returncode == 0, out.stderr
+    _check_toy(out.stdout.splitlines(), 4, 3)
+
+
+def _mnist(args, n=None, timeout=300):
+    base = [os.path.join(ROOT, "scripts/mnist.py"), "--no-cuda", "--train-size", "1024", "--test-size", "256",
+            "--epochs", "2"] + args
+    cmd = [sys.executable] + (["-m", "pytorch_distributed_example_amd.launch", "-n", str(n)] if n else []) + base
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, env=ENV, timeout=timeout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    return out.stdout.splitlines()
+
+
+def test_mnist_single_process_golden():
+    lines = _mnist(["-s", "1"])
+    assert lines[0].startswith("Namespace(backend='nccl', init_method='tcp://127.0.0.1:23456', rank=None, "
+                               "world_size=1, epochs=2, no_cuda=True, learning_rate=0.001, root='data', "
+                               "batch_size=128, eval=False")
+    assert lines[1:4] == ["device = cpu", "Getting data loader with root = data", "obtained data_loader"]
+    ep = [EPOCH_LINE.match(l) for l in lines[4:]]
+    assert all(ep) and len(ep) == 2
+    assert ep[0].group(5) == "0" and ep[0].group(6) == "0"      # no --eval: zeros until the last epoch
+    assert float(ep[1].group(3)) < float(ep[0].group(3))         # loss decreases
+
+
+@pytest.mark.parametrize("ddp", ["on", "off"])
+def test_mnist_gloo_two_ranks(ddp):
+    lines = _mnist(["--backend", "gloo", "--eval", "--ddp", ddp], n=2)
+    assert lines.count("called init_process_group") == 2
+    ep = [m for m in map(EPOCH_LINE.match, lines) if m]
+    assert len(ep) == 4
+    # test metrics identical across ranks (replicas in sync)
+    last = [m for m in ep if m.group(1) == "2"]
+    assert last[0].group(5) == last[1].group(5) and last[0].group(6) == last[1].group(6)
+
+
+def test_mnist_save_resume(tmp_path):
+    ck = str(tmp_path / "ck.pt")
+    _mnist(["-s", "1", "--save", ck, "--epochs", "1"])
+    assert os.path.exists(ck)
+    lines = _mnist(["-s", "1", "--resume", ck, "--epochs", "2"])
+    ep = [m for m in map(EPOCH_LINE.match, lines) if m]
+    assert [m.group(1) for m in ep] == ["2"]
+
+
+def test_read_stats(tmp_path):
+    prof = str(tmp_path / "p.prof")
+    _mnist(["-s", "1", "--epochs", "1", "--cprofile", prof])
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/read_stats.py"), prof, "10"],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "tottime" in out.stdout
