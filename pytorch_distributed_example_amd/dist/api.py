@@ -430,7 +430,7 @@ def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool
         return None
     _check(tensor)
     code, dt, n = _op_code(op), _DTYPES[tensor.dtype], tensor.numel()
-    if g._gpu_ok(tensor):
+    if g._gpu_ok(tensor) and code <= 4:      # RCCL has no bitwise reductions
         return _gpu_launch(g, [tensor], lambda s: g.rccl.all_reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt,
                                                                      code, s), async_op)
     if tensor.is_cuda:
@@ -509,7 +509,7 @@ def reduce_scatter_tensor(output: torch.Tensor, input: torch.Tensor, op=ReduceOp
     if input.numel() != output.numel() * g.size():
         raise ValueError("input must hold world_size x output elements")
     code, dt = _op_code(op), _DTYPES[input.dtype]
-    if g._gpu_ok(input):
+    if g._gpu_ok(input) and code <= 4:
         return _gpu_launch(g, [output, input], lambda s: g.rccl.reduce_scatter(input.data_ptr(), output.data_ptr(),
                                                                                output.numel(), dt, code, s), async_op)
     if input.is_cuda:
@@ -531,7 +531,7 @@ def reduce(tensor: torch.Tensor, dst: int = 0, op=ReduceOp.SUM, group=None, asyn
         return None
     _check(tensor)
     root, code, dt, n = g.group_rank(dst), _op_code(op), _DTYPES[tensor.dtype], tensor.numel()
-    if g._gpu_ok(tensor):
+    if g._gpu_ok(tensor) and code <= 4:
         return _gpu_launch(g, [tensor], lambda s: g.rccl.reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt, code,
                                                                  root, s), async_op)
     if tensor.is_cuda:
@@ -643,6 +643,56 @@ def irecv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int 
         return _Completed()
     return Work(native=g.host.recv(tensor.data_ptr(), tensor.numel() * tensor.element_size(), g.group_rank(src),
                                    True), keep=(tensor,))
+
+
+class P2POp:
+    """One point-to-point op for ``batch_isend_irecv`` (``op`` is ``isend`` or ``irecv``)."""
+
+    def __init__(self, op, tensor: torch.Tensor, peer: int, group=None, tag: int = 0):
+        if op not in (isend, irecv):
+            raise ValueError("P2POp op must be dist.isend or dist.irecv")
+        self.op, self.tensor, self.peer, self.group, self.tag = op, tensor, peer, group, tag
+
+
+def batch_isend_irecv(p2p_op_list: List[P2POp]) -> List[Work]:
+    """Issue a set of sends/receives together.  GPU: one ``ncclGroupStart/End`` on the comm stream, so
+    any send/recv pattern (rings, exchanges, all-to-all by hand) progresses without deadlock.  Host:
+    all sends are queued asynchronously before the receives are posted."""
+    if not p2p_op_list:
+        return []
+    g = _group(p2p_op_list[0].group)
+    if any(_group(o.group) is not g for o in p2p_op_list):
+        raise ValueError("batch_isend_irecv: all ops must use the same group")
+    for o in p2p_op_list:
+        _check(o.tensor)
+    if all(g._gpu_ok(o.tensor) for o in p2p_op_list):
+        def fn(stream):
+            g.rccl.group_start()
+            try:
+                for o in p2p_op_list:
+                    t = o.tensor
+                    f = g.rccl.send if o.op is isend else g.rccl.recv
+                    f(t.data_ptr(), t.numel(), _DTYPES[t.dtype], g.group_rank(o.peer), stream)
+            finally:
+                g.rccl.group_end()
+        w = _gpu_launch(g, [o.tensor for o in p2p_op_list], fn, True)
+        return [w]
+    sends = [o for o in p2p_op_list if o.op is isend]
+    recvs = [o for o in p2p_op_list if o.op is irecv]
+    works = []
+    for o in sends:
+        t = o.tensor.detach().cpu().contiguous() if o.tensor.is_cuda else o.tensor
+        works.append(Work(native=g.host.send(t.data_ptr(), t.numel() * t.element_size(), g.group_rank(o.peer),
+                                             True), keep=(t,)))
+    for o in recvs:
+        if o.tensor.is_cuda:
+            recv(o.tensor, o.peer, g)
+            works.append(_Completed())
+        else:
+            t = o.tensor
+            works.append(Work(native=g.host.recv(t.data_ptr(), t.numel() * t.element_size(), g.group_rank(o.peer),
+                                                 True), keep=(t,)))
+    return works
 
 
 def barrier(group=None, async_op: bool = False, device_ids=None):

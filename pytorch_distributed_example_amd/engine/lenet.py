@@ -37,7 +37,7 @@ C1_STRIDE = 576       # conv1.weight (500 -> 512 slot) + conv1.bias (20 -> 64 sl
 class LeNetTrainStep:
     def __init__(self, net: torch.nn.Module, batch_size: int = 128, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, optimizer: str = "adam", momentum: float = 0.0,
-                 comm=None, overlap: bool = True):
+                 comm=None, overlap: bool = True, force_comm: bool = False):
         self.net = net
         p0 = next(net.parameters())
         if not p0.is_cuda:
@@ -50,6 +50,8 @@ class LeNetTrainStep:
         self.comm = comm
         self.world = comm.world_size if comm is not None else 1
         self.overlap = overlap
+        # force_comm: run the comm-stream/event path even at world size 1 (1-GPU testing of the W>1 path)
+        self.comm_on = comm is not None and (self.world > 1 or force_comm)
         self.K = kernels()
         dev = self.device
         self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, CONV_BUCKET],
@@ -90,7 +92,7 @@ class LeNetTrainStep:
         self.samples = 0
         self.eval_loss = torch.zeros(1, device=dev, dtype=torch.float64)
         self.eval_correct = torch.zeros(1, device=dev, dtype=torch.int64)
-        self.comm_stream = torch.cuda.Stream(device=dev) if self.world > 1 else None
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.comm_on else None
         self._ev = [torch.cuda.Event(), torch.cuda.Event()]
         self.X = self.Y = self.idx = None
         self.nbatches = 0
@@ -130,14 +132,14 @@ class LeNetTrainStep:
                        g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], self.row_loss, self.row_hit, self.loss_sum,
                        self.correct)
         cur = torch.cuda.current_stream(self.device)
-        if self.world > 1 and self.overlap:
+        if self.comm_on and self.overlap:
             self._ev[0].record(cur)
             self.comm_stream.wait_event(self._ev[0])
             with torch.cuda.stream(self.comm_stream):
                 self.comm.all_reduce_(self.bucket_grads[0])
         K.lenet_conv_bwd(self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
                          self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE)
-        if self.world > 1:
+        if self.comm_on:
             self._ev[1].record(cur)
             self.comm_stream.wait_event(self._ev[1])
             with torch.cuda.stream(self.comm_stream):

@@ -74,7 +74,10 @@ class FlatLayout:
             v = flat_p[s.offset: s.offset + s.numel].view(s.shape)
             v.copy_(p.detach())
             p.data = v
-            p.grad = flat_g[s.offset: s.offset + s.numel].view(s.shape)
+            gv = flat_g[s.offset: s.offset + s.numel].view(s.shape)
+            if p.grad is not None:          # binding after a backward (lazy optimizer init): keep the grad
+                gv.copy_(p.grad.detach())
+            p.grad = gv
             p._pde_flat = (self, flat_p, flat_g, n)
         return flat_p, flat_g
 

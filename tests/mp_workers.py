@@ -123,21 +123,33 @@ def case_collectives(backend="gloo", method="env"):
     dist.all_to_all_single(out, inp)
     assert out.cpu().tolist() == [100.0 * j + R for j in range(W) for _ in range(2)]
     # send / recv ring, isend / irecv
-    nxt, prv = (R + 1) % W, (R - 1) % W
-    s = torch.full((17,), float(R), device=dev)
-    r_ = torch.empty(17, device=dev)
-    if R % 2 == 0:
-        dist.send(s, nxt)
-        dist.recv(r_, prv)
-    else:
-        dist.recv(r_, prv)
-        dist.send(s, nxt)
-    assert torch.equal(r_.cpu(), torch.full((17,), float(prv)))
-    w1 = dist.isend(s * 2, nxt)
-    w2 = dist.irecv(r_, prv)
-    w1.wait()
-    w2.wait()
-    assert torch.equal(r_.cpu(), torch.full((17,), float(2 * prv)))
+    if W > 1:                     # point-to-point to self is not a valid RCCL pattern
+        nxt, prv = (R + 1) % W, (R - 1) % W
+        s = torch.full((17,), float(R), device=dev)
+        r_ = torch.empty(17, device=dev)
+        if R % 2 == 0:
+            dist.send(s, nxt)
+            dist.recv(r_, prv)
+        else:
+            dist.recv(r_, prv)
+            dist.send(s, nxt)
+        assert torch.equal(r_.cpu(), torch.full((17,), float(prv)))
+        s2 = s * 2
+        if dev.type == "cpu":
+            w1 = dist.isend(s2, nxt)
+            w2 = dist.irecv(r_, prv)
+            w1.wait()
+            w2.wait()
+            assert torch.equal(r_.cpu(), torch.full((17,), float(2 * prv)))
+        s3, r3 = s * 3, torch.empty(17, device=dev)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s3, nxt), dist.P2POp(dist.irecv, r3, prv)]):
+            w.wait()
+        assert torch.equal(r3.cpu(), torch.full((17,), float(3 * prv)))
+    elif dev.type == "cuda":      # grouped send/recv to self is valid: exercises the ncclGroup path
+        s3, r3 = torch.full((17,), 3.0, device=dev), torch.empty(17, device=dev)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s3, 0), dist.P2POp(dist.irecv, r3, 0)]):
+            w.wait()
+        assert torch.equal(r3.cpu(), torch.full((17,), 3.0))
     # async all_reduce
     t = torch.ones(50_000, device=dev)
     work = dist.all_reduce(t, async_op=True)
@@ -234,7 +246,7 @@ def case_fail(backend="gloo"):
     dist.barrier()            # would hang forever without the launcher's gang termination
 
 
-def case_engine_comm(steps="3"):
+def case_engine_comm(steps="3", mode="eager"):
     """Fused engine with the RCCL comm path (W ranks, nccl), prints final param checksums."""
     from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
@@ -245,12 +257,17 @@ def case_engine_comm(steps="3"):
     net = build_net(seed=3 + R, device=dev)
     dist.broadcast_parameters(net)
     ds = synthetic_mnist(512 * W, seed=0, device=dev)
-    eng = LeNetTrainStep(net, batch_size=64, comm=dist.engine_comm())
+    eng = LeNetTrainStep(net, batch_size=64, comm=dist.engine_comm(), force_comm=True)
     eng.bind_dataset(ds.images, ds.labels)
     s = DistributedSampler(ds, num_replicas=W, rank=R, shuffle=False)
     eng.set_epoch_indices(s.indices_tensor())
-    for _ in range(int(steps)):
-        eng.step()
+    if mode == "graph":
+        eng.capture()
+        for _ in range(int(steps)):
+            eng.replay()
+    else:
+        for _ in range(int(steps)):
+            eng.step()
     torch.cuda.synchronize()
     emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()]})
     dist.destroy_process_group()

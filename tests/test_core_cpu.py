@@ -169,3 +169,15 @@ def test_kernels_library_built_for_gfx950():
     assert lib, "kernel extension not built (run __graft_entry__.build())"
     blob = open(lib[0], "rb").read()
     assert b"gfx950" in blob            # the embedded HIP fat binary targets gfx950
+
+
+def test_flat_bind_keeps_existing_grads():
+    """Optimizers bind lazily after the first backward: the grads computed so far must survive."""
+    from pytorch_distributed_example_amd.parallel.flat import FlatLayout
+    net = build_net(seed=0)
+    F.cross_entropy(net(torch.randn(2, 1, 28, 28)), torch.tensor([1, 2])).backward()
+    before = {n: p.grad.clone() for n, p in net.named_parameters()}
+    lay = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [[n for n, _ in net.named_parameters()]])
+    lay.bind(net)
+    for n, p in net.named_parameters():
+        assert torch.equal(p.grad, before[n])

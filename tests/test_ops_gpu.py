@@ -1,0 +1,189 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (generic ops, fused optimizers) and the
+distributed GPU path at W=1 (RCCL communicator, engine comm path, DDP over nccl, CLI fused run)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_example_amd import ops
+from pytorch_distributed_example_amd._ext import kernels, loaded_native_libraries
+from pytorch_distributed_example_amd.ops import generic as G
+from pytorch_distributed_example_amd.models import build_net
+from pytorch_distributed_example_amd.optim import SGD, Adam, AdamW
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _close(a, b, tol=2e-4):
+    err = (a.double() - b.double()).abs().max().item()
+    scale = b.double().abs().max().item() + 1e-6
+    assert err <= tol * max(1.0, scale), (err, scale)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (128, 500, 800), (77, 33, 65), (256, 256, 256), (5, 1000, 3)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm(M, N, K, ta, tb):
+    torch.manual_seed(0)
+    A = torch.randn(K, M, device=dev) if ta else torch.randn(M, K, device=dev)
+    B = torch.randn(N, K, device=dev) if tb else torch.randn(K, N, device=dev)
+    C = torch.randn(M, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    ref = (A.t() if ta else A) @ (B.t() if tb else B) + 0.5 * C + bias
+    out = C.clone()
+    kernels().gemm(A, B, out, bias, M, N, K, A.shape[1], B.shape[1], N, ta, tb, 0, 0, 0, 1, 1.0, 0.5, 1, False,
+                   False)
+    _close(out, ref)
+    out2 = torch.empty(M, N, device=dev)
+    kernels().gemm(A, B, out2, None, M, N, K, A.shape[1], B.shape[1], N, ta, tb, 0, 0, 0, 1, 1.0, 0.0, 0, True,
+                   False)
+    _close(out2, ((A.t() if ta else A) @ (B.t() if tb else B)).relu())
+
+
+def test_linear_fwd_bwd():
+    torch.manual_seed(1)
+    x = torch.randn(37, 800, device=dev, requires_grad=True)
+    w = torch.randn(500, 800, device=dev, requires_grad=True)
+    b = torch.randn(500, device=dev, requires_grad=True)
+    g = torch.randn(37, 500, device=dev)
+    y = G.linear(x, w, b)
+    y.backward(g)
+    x2, w2, b2 = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    y2 = F.linear(x2, w2, b2)
+    y2.backward(g)
+    _close(y, y2)
+    for a, r in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        _close(a, r)
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 28, 28, 20, 5), (3, 20, 12, 12, 50, 5), (2, 3, 9, 9, 4, 3)])
+def test_conv2d_fwd_bwd(shape):
+    N, C, H, W, O, k = shape
+    torch.manual_seed(2)
+    x = torch.randn(N, C, H, W, device=dev, requires_grad=True)
+    w = torch.randn(O, C, k, k, device=dev, requires_grad=True)
+    b = torch.randn(O, device=dev, requires_grad=True)
+    y = G.conv2d(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    x2, w2, b2 = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    y2 = F.conv2d(x2, w2, b2)
+    y2.backward(g)
+    _close(y, y2)
+    for a, r in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        _close(a, r, 5e-4)
+
+
+def test_relu_pool_logsoftmax_xent():
+    torch.manual_seed(3)
+    x = torch.randn(4, 6, 8, 8, device=dev, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_()
+    y = G.max_pool2d(G.relu(x))
+    y2 = F.max_pool2d(F.relu(x2), 2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    _close(y, y2)
+    _close(x.grad, x2.grad)
+    z = torch.randn(33, 10, device=dev, requires_grad=True)
+    z2 = z.detach().clone().requires_grad_()
+    lbl = torch.randint(0, 10, (33,), device=dev)
+    l1 = G.cross_entropy(G.log_softmax(z), lbl)
+    l2 = F.cross_entropy(F.log_softmax(z2, 1), lbl)
+    l1.backward()
+    l2.backward()
+    _close(l1, l2)
+    _close(z.grad, z2.grad)
+
+
+def test_net_autograd_path_matches_cpu():
+    net = build_net(seed=5, device=dev)
+    cpu = build_net(seed=5)
+    x = torch.randn(16, 1, 28, 28)
+    y = torch.randint(0, 10, (16,))
+    lg = ops.cross_entropy(net(x.to(dev)), y.to(dev))
+    lc = F.cross_entropy(cpu(x), y)
+    lg.backward()
+    lc.backward()
+    _close(lg.cpu(), lc, 1e-4)
+    for p, q in zip(net.parameters(), cpu.parameters()):
+        _close(p.grad.cpu(), q.grad, 1e-3)
+
+
+@pytest.mark.parametrize("opt_cls,ref_cls,kw", [
+    (Adam, torch.optim.Adam, dict(lr=1e-3)),
+    (AdamW, torch.optim.AdamW, dict(lr=1e-3, weight_decay=1e-2)),
+    (SGD, torch.optim.SGD, dict(lr=1e-2, momentum=0.9)),
+])
+def test_fused_optimizer_matches_torch(opt_cls, ref_cls, kw):
+    a = build_net(seed=1, device=dev)
+    b = build_net(seed=1, device=dev)
+    oa, ob = opt_cls(a.parameters(), **kw), ref_cls(b.parameters(), foreach=False, **kw)
+    torch.manual_seed(0)
+    for _ in range(5):
+        x = torch.randn(8, 1, 28, 28, device=dev)
+        y = torch.randint(0, 10, (8,), device=dev)
+        for net, opt in ((a, oa), (b, ob)):
+            opt.zero_grad()
+            F.cross_entropy(net(x), y).backward()
+            opt.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        d = (p - q).abs()
+        assert d.mean().item() < 1e-5 and d.max().item() < 5e-4
+
+
+def test_native_libraries_loaded():
+    from pytorch_distributed_example_amd._ext import runtime
+    runtime()
+    libs = loaded_native_libraries()
+    assert any("_kernels" in p for p in libs) and any("_runtime" in p for p in libs), libs
+
+
+def _mp(case, *args):
+    sys.path.insert(0, os.path.dirname(__file__))
+    from _mp import run_ranks
+    return run_ranks(case, 1, *args)
+
+
+def test_rccl_world1_collectives():
+    rc, res, logs = _mp("collectives", "nccl", "env")
+    assert rc == 0, logs
+    assert res[0]["ok"]
+
+
+def test_ddp_nccl_world1():
+    rc, res, logs = _mp("ddp", "nccl", "0.05", "3")
+    assert rc == 0, logs
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_engine_comm_world1_matches_no_comm(mode):
+    rc, res, logs = _mp("engine_comm", "3", mode)
+    assert rc == 0, logs
+    from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
+    from pytorch_distributed_example_amd.engine import LeNetTrainStep
+    net = build_net(seed=3, device=dev)
+    ds = synthetic_mnist(512, seed=0, device=dev)
+    eng = LeNetTrainStep(net, batch_size=64)
+    eng.bind_dataset(ds.images, ds.labels)
+    eng.set_epoch_indices(DistributedSampler(ds, num_replicas=1, rank=0, shuffle=False).indices_tensor())
+    for _ in range(3):
+        eng.step()
+    torch.cuda.synchronize()
+    ref = [p.detach().double().sum().item() for p in net.parameters()]
+    assert res[0]["params"] == pytest.approx(ref, rel=1e-6, abs=1e-6)
+
+
+def test_mnist_script_fused_gpu():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/mnist.py"), "-s", "1", "--epochs", "2",
+                          "--train-size", "4096", "--test-size", "1024", "--eval"], capture_output=True, text=True,
+                         timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = out.stdout.splitlines()
+    assert "device = cuda" in lines
+    ep = [l for l in lines if l.startswith("Epoch: ")]
+    assert len(ep) == 2
