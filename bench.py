@@ -38,7 +38,14 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--model", choices=["lenet", "gpt2", "resnet18"], default="lenet",
+                    help="lenet = the BASELINE headline (default); gpt2 / resnet18 = the driver-added configs")
+    ap.add_argument("--seq-len", type=int, default=1024, help="gpt2: sequence length")
+    ap.add_argument("--bucket-mb", type=float, default=64.0, help="gpt2/resnet18: DDP gradient bucket size")
     args = ap.parse_args()
+    if args.model != "lenet":
+        from bench_models import run_model_bench
+        return run_model_bench(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

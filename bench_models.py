@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Benchmarks of the driver-added configs (BASELINE.json ``configs``), same timing contract as
+``bench.py`` (W untimed warm-up steps, K timed steps between barrier + synchronize, max over ranks,
+one JSON line from rank 0):
+
+* ``--model gpt2``     GPT-2 small (124M), bf16, DDP over RCCL with large gradient buckets,
+                       fused AdamW (fp32 master), synthetic tokens; metric tokens/s (whole node).
+* ``--model resnet18`` ResNet-18, bf16 channels-last, synthetic 3x224x224 images, DDP, SGD+momentum;
+                       metric images/s (whole node).
+
+Invoked through ``python bench.py --model {gpt2,resnet18} ...``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+
+def _setup():
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_distributed_example_amd import dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
+    return torch, dist, rank, world, torch.device("cuda", local_rank)
+
+
+def _timed(torch, dist, world, step, warmup, steps):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def bench_gpt2(args):
+    torch, dist, rank, world, dev = _setup()
+    from pytorch_distributed_example_amd.models import GPTConfig, build_gpt2
+    from pytorch_distributed_example_amd.optim import AdamWMaster
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    B = args.batch_size if args.batch_size != 128 else 16      # per-GPU micro-batch (sequences)
+    T = args.seq_len
+    cfg = GPTConfig(block_size=max(1024, T))
+    model = build_gpt2(cfg, seed=args.seed, device=dev)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    opt = AdamWMaster(model.decay_groups(0.1), lr=6e-4, betas=(0.9, 0.95), max_grad_norm=1.0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + rank)
+    data = torch.randint(0, cfg.vocab_size, (8, B, T + 1), device=dev, generator=g)
+    it = [0]
+    losses = []
+
+    def step():
+        batch = data[it[0] % data.shape[0]]
+        it[0] += 1
+        opt.zero_grad()
+        loss = ddp(batch[:, :-1], batch[:, 1:])
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach())
+
+    elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
+    tokens = args.steps * B * T * world
+    tps = tokens / elapsed
+    flops = model.flops_per_token() * tps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "tokens/sec (whole node), GPT-2-small DDP",
+            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic uniform tokens, random-init weights",
+            "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
+                       "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", "bucket_mb": args.bucket_mb},
+            "model_tflops_per_gpu": round(flops / world / 1e12, 1),
+            "last_loss": round(float(losses[-1]), 4),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_model_bench(args):
+    if args.model == "gpt2":
+        return bench_gpt2(args)
+    if args.model == "resnet18":
+        from bench_resnet import bench_resnet18
+        return bench_resnet18(args)
+    raise ValueError(args.model)

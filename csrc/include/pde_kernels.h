@@ -64,6 +64,35 @@ hipError_t pde_bias_grad_nchw(const float* dy, int B, int O, long long P, float*
 hipError_t pde_colsum(const float* x, int M, int N, float* out, hipStream_t st);
 hipError_t pde_gather_rows(const float* src, const long long* idx, int n, int row_floats, float* out, hipStream_t st);
 
+
+// ---- transformer (transformer.hip) ----
+hipError_t pde_ln_fwd(const void* X, const void* G, const void* B, void* Y, float* mean, float* rstd, int N, int C,
+                      float eps, hipStream_t st);
+int pde_ln_bwd_blocks(int N);
+hipError_t pde_ln_bwd(const void* dY, const void* X, const float* mean, const float* rstd, const void* G,
+                      const void* dRes, void* dX, float* part, void* dG, void* dB, int N, int C, int accumulate,
+                      hipStream_t st);
+hipError_t pde_gelu_fwd(const void* X, void* Y, int64_t n, hipStream_t st);
+hipError_t pde_gelu_bwd(const void* dY, const void* X, void* dX, int64_t n, hipStream_t st);
+hipError_t pde_xent_bf16(void* logits, const int64_t* tgt, int N, int Vp, int V, float scale, float* loss_rows,
+                         int write_grad, hipStream_t st);
+hipError_t pde_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int N, int T, int C,
+                         hipStream_t st);
+hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* dwpe, float* acc, uint8_t* touched,
+                         int N, int T, int C, int Vp, int accumulate_pos, hipStream_t st);
+hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st);
+hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m, float* v, int64_t n, float lr,
+                            float b1, float b2, float eps, float wd, float grad_scale, int step,
+                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st);
+hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
+
+// ---- attention (attention.hip) ----
+hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
+                        int T, int H, float scale, hipStream_t st);
+hipError_t pde_attn_bwd(const void* q, const void* k, const void* v, int ldq, const void* o, const void* dout,
+                        int ldo, const float* lse, float* Dd, void* dq, void* dk, void* dv, int B, int T, int H,
+                        float scale, hipStream_t st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,565 @@
+// Transformer (GPT-2) kernels for gfx950: LayerNorm fwd/bwd, tanh-GELU fwd/bwd, fused vocab
+// softmax-cross-entropy (loss + dlogits in one pass pair), token+position embedding fwd/bwd, and
+// the AdamW step on bf16 model weights with fp32 master weights (+ device-side grad-norm clipping).
+//
+// All activations/weights are bf16 (raw uint16); statistics and optimizer state are fp32.  Rows are
+// processed one wave (64 lanes) per row with 8- or 16-byte vector accesses; per-lane columns are
+// fixed (chunk c = lane + 64 j) so LayerNorm's dgamma/dbeta accumulate in registers across rows.
+#include "pde_hip.h"
+#include "pde_bf16.h"
+#include "pde_kernels.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------- LayerNorm
+template <int NCH>
+__global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ X, const bf16_t* __restrict__ G,
+                                                const bf16_t* __restrict__ Bt, bf16_t* __restrict__ Y,
+                                                float* __restrict__ mean_out, float* __restrict__ rstd_out, int N,
+                                                int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;  // wave-uniform
+  const int nc = C >> 2;
+  const uint2* xr = reinterpret_cast<const uint2*>(X + (size_t)row * C);
+  const uint2* g4 = reinterpret_cast<const uint2*>(G);
+  const uint2* b4 = reinterpret_cast<const uint2*>(Bt);
+  float v[NCH][4], gg[NCH][4], bb[NCH][4];
+  uint2 wx[NCH], wg[NCH], wb[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {  // issue every load first (clamped index, no branch)
+    const int c = min(lane + 64 * j, nc - 1);
+    wx[j] = xr[c];
+    wg[j] = g4[c];
+    wb[j] = b4[c];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const bool ok = lane + 64 * j < nc;
+    unpack4(wx[j], v[j]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += ok ? v[j][e] : 0.f;
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const bool ok = lane + 64 * j < nc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[j][e] - mean;
+      q += ok ? d * d : 0.f;
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+  uint2* yr = reinterpret_cast<uint2*>(Y + (size_t)row * C);
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = lane + 64 * j;
+    unpack4(wg[j], gg[j]);
+    unpack4(wb[j], bb[j]);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * gg[j][e] + bb[j][e];
+    if (c < nc) yr[c] = pack4(o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dX = rstd * (gy - mean(gy) - xhat * mean(gy * xhat)) (+ dRes), gy = dY * gamma.
+// Block = 4 waves x RPW rows each; dgamma / dbeta partial sums per block -> part[blk][2][C].
+template <int NCH>
+__global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                const bf16_t* __restrict__ G, const bf16_t* __restrict__ dRes,
+                                                bf16_t* __restrict__ dX, float* __restrict__ part, int N, int C,
+                                                int rpw) {
+  extern __shared__ float sh[];  // [4][2][C]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nc = C >> 2;
+  float gg[NCH][4], dg[NCH][4], db[NCH][4];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = min(lane + 64 * j, nc - 1);
+    unpack4(reinterpret_cast<const uint2*>(G)[c], gg[j]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dg[j][e] = db[j][e] = 0.f;
+  }
+  const int row0 = blockIdx.x * 4 * rpw;
+  for (int i = 0; i < rpw; ++i) {
+    const int row = row0 + w + 4 * i;
+    if (row >= N) break;  // wave-uniform
+    const uint2* dyr = reinterpret_cast<const uint2*>(dY + (size_t)row * C);
+    const uint2* xr = reinterpret_cast<const uint2*>(X + (size_t)row * C);
+    uint2 wdy[NCH], wx[NCH], wr[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = min(lane + 64 * j, nc - 1);
+      wdy[j] = dyr[c];
+      wx[j] = xr[c];
+      wr[j] = dRes ? reinterpret_cast<const uint2*>(dRes + (size_t)row * C)[c] : make_uint2(0u, 0u);
+    }
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NCH][4], gy[NCH][4];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const bool ok = lane + 64 * j < nc;
+      float dy[4], x[4];
+      unpack4(wdy[j], dy);
+      unpack4(wx[j], x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[j][e] = (x[e] - mu) * rs;
+        gy[j][e] = ok ? dy[e] * gg[j][e] : 0.f;
+        a += gy[j][e];
+        b += gy[j][e] * xh[j][e];
+        dg[j][e] += ok ? dy[e] * xh[j][e] : 0.f;
+        db[j][e] += ok ? dy[e] : 0.f;
+      }
+    }
+    a = wave_sum(a) / (float)C;
+    b = wave_sum(b) / (float)C;
+    uint2* dxr = reinterpret_cast<uint2*>(dX + (size_t)row * C);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = lane + 64 * j;
+      float r[4], o[4];
+      unpack4(wr[j], r);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rs * (gy[j][e] - a - xh[j][e] * b) + r[e];
+      if (c < nc) dxr[c] = pack4(o);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nc) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sh[(w * 2 + 0) * C + 4 * c + e] = dg[j][e];
+        sh[(w * 2 + 1) * C + 4 * c + e] = db[j][e];
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 2 * C; k += 256) {
+    const float s = sh[k] + sh[2 * C + k] + sh[4 * C + k] + sh[6 * C + k];
+    part[(size_t)blockIdx.x * 2 * C + k] = s;
+  }
+}
+
+// Sum per-block partials: out[k] = sum_b part[b][k], k < 2C; writes dgamma | dbeta as bf16 (or
+// accumulates into them when accumulate != 0).  Block = 64 columns x 4 row-groups.
+__global__ __launch_bounds__(256) void k_ln_reduce(const float* __restrict__ part, int nblk, int C2,
+                                                   bf16_t* __restrict__ dG, bf16_t* __restrict__ dB, int C,
+                                                   int accumulate) {
+  __shared__ float sh[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int kc = min(k, C2 - 1);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = w;
+  for (; b + 12 < nblk; b += 16) {
+    s0 += part[(size_t)b * C2 + kc];
+    s1 += part[(size_t)(b + 4) * C2 + kc];
+    s2 += part[(size_t)(b + 8) * C2 + kc];
+    s3 += part[(size_t)(b + 12) * C2 + kc];
+  }
+  for (; b < nblk; b += 4) s0 += part[(size_t)b * C2 + kc];
+  sh[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && k < C2) {
+    float t = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
+    bf16_t* dst = k < C ? dG + k : dB + (k - C);
+    if (accumulate) t += bf2f(*dst);
+    *dst = f2bf(t);
+  }
+}
+
+// ---------------------------------------------------------------------------------- GELU (tanh)
+__device__ __forceinline__ float gelu_t(float x, float* dgelu) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
+  if (dgelu) *dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  return 0.5f * x * (1.f + t);
+}
+
+__global__ __launch_bounds__(256) void k_gelu_fwd(const uint4* __restrict__ X, uint4* __restrict__ Y, int64_t n8) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    unpack8(X[i], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_t(v[e], nullptr);
+    Y[i] = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gelu_bwd(const uint4* __restrict__ dY, const uint4* __restrict__ X,
+                                                  uint4* __restrict__ dX, int64_t n8) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float x[8], g[8];
+    unpack8(X[i], x);
+    unpack8(dY[i], g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float d;
+      gelu_t(x[e], &d);
+      g[e] *= d;
+    }
+    dX[i] = pack8(g);
+  }
+}
+
+// ---------------------------------------------------------------------------------- softmax-CE
+// One block per row of logits [N, Vp] (bf16).  Pass 1: online max / sum-exp over the V real columns;
+// pass 2 overwrites the row IN PLACE with dlogits = (softmax - onehot) * scale (padding columns -> 0).
+// Target < 0 = ignore_index: loss 0, zero gradient.
+__device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+  m = mn;
+}
+
+__global__ __launch_bounds__(256) void k_xent_bf16(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt, int Vp,
+                                                   int V, float scale, float* __restrict__ loss_rows,
+                                                   int write_grad) {
+  __shared__ float shm[4], shs[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint4* Lr = reinterpret_cast<uint4*>(L + (size_t)row * Vp);
+  const int nch = Vp >> 3;
+  const int64_t t = tgt[row];
+  const float xt = (t >= 0 && t < V) ? bf2f(L[(size_t)row * Vp + t]) : 0.f;
+  float m = -INFINITY, s = 0.f;
+  int c = tid;
+  for (; c + 768 < nch; c += 1024) {  // 4 loads in flight per thread
+    uint4 q[4] = {Lr[c], Lr[c + 256], Lr[c + 512], Lr[c + 768]};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float v[8];
+      unpack8(q[u], v);
+      const int col0 = (c + 256 * u) * 8;
+      float bm = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bm = fmaxf(bm, col0 + e < V ? v[e] : -INFINITY);
+      float bs = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bs += col0 + e < V ? __expf(v[e] - bm) : 0.f;
+      ms_combine(m, s, bm, bs);
+    }
+  }
+  for (; c < nch; c += 256) {
+    float v[8];
+    unpack8(Lr[c], v);
+    const int col0 = c * 8;
+    float bm = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bm = fmaxf(bm, col0 + e < V ? v[e] : -INFINITY);
+    float bs = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs += col0 + e < V ? __expf(v[e] - bm) : 0.f;
+    ms_combine(m, s, bm, bs);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    ms_combine(m, s, m2, s2);
+  }
+  if (lane == 0) {
+    shm[w] = m;
+    shs[w] = s;
+  }
+  __syncthreads();
+  m = shm[0];
+  s = shs[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) ms_combine(m, s, shm[k], shs[k]);
+  const float lse = m + __logf(s);
+  const bool valid = t >= 0 && t < V;
+  if (tid == 0) loss_rows[row] = valid ? lse - xt : 0.f;
+  if (!write_grad) return;
+  const float sc = valid ? scale : 0.f;
+  for (c = tid; c < nch; c += 256) {
+    float v[8];
+    unpack8(Lr[c], v);
+    const int col0 = c * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = col0 + e;
+      const float p = col < V ? __expf(v[e] - lse) : 0.f;
+      v[e] = (p - (col == t ? 1.f : 0.f)) * sc;
+    }
+    Lr[c] = pack8(v);
+  }
+}
+
+// ---------------------------------------------------------------------------------- embeddings
+__global__ __launch_bounds__(256) void k_embed_fwd(const int64_t* __restrict__ idx, const bf16_t* __restrict__ wte,
+                                                   const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int N,
+                                                   int T, int C) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int64_t tok = idx[row];
+  const int pos = row % T;
+  const uint2* a = reinterpret_cast<const uint2*>(wte + (size_t)tok * C);
+  const uint2* b = reinterpret_cast<const uint2*>(wpe + (size_t)pos * C);
+  uint2* o = reinterpret_cast<uint2*>(out + (size_t)row * C);
+  for (int c = lane; c < (C >> 2); c += 64) {
+    float x[4], y[4];
+    unpack4(a[c], x);
+    unpack4(b[c], y);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] += y[e];
+    o[c] = pack4(x);
+  }
+}
+
+// dwpe[t, :] = sum_b dX[b*T + t, :]  (thread per (t, 4-column chunk); no atomics)
+__global__ __launch_bounds__(256) void k_embed_bwd_pos(const bf16_t* __restrict__ dX, bf16_t* __restrict__ dwpe,
+                                                       int N, int T, int C, int accumulate) {
+  const int nc = C >> 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= T * nc) return;
+  const int t = i / nc, c = i % nc;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = t; r < N; r += T) {
+    float x[4];
+    unpack4(reinterpret_cast<const uint2*>(dX + (size_t)r * C)[c], x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += x[e];
+  }
+  uint2* d = reinterpret_cast<uint2*>(dwpe + (size_t)t * C) + c;
+  if (accumulate) {
+    float o[4];
+    unpack4(*d, o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += o[e];
+  }
+  *d = pack4(acc);
+}
+
+// token rows: fp32 atomics into a scratch table + a per-row touched flag
+__global__ __launch_bounds__(256) void k_embed_bwd_tok(const bf16_t* __restrict__ dX, const int64_t* __restrict__ idx,
+                                                       float* __restrict__ acc, uint8_t* __restrict__ touched, int N,
+                                                       int C) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int64_t tok = idx[row];
+  if (lane == 0) touched[tok] = 1;
+  float* a = acc + (size_t)tok * C;
+  for (int c = lane; c < (C >> 2); c += 64) {
+    float x[4];
+    unpack4(reinterpret_cast<const uint2*>(dX + (size_t)row * C)[c], x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(a + 4 * c + e, x[e]);
+  }
+}
+
+// dwte[v] += acc[v] for touched rows; resets acc / touched for the next step (no memset needed)
+__global__ __launch_bounds__(256) void k_embed_tok_merge(float* __restrict__ acc, uint8_t* __restrict__ touched,
+                                                         bf16_t* __restrict__ dwte, int Vp, int C) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= Vp || !touched[row]) return;
+  float4* a = reinterpret_cast<float4*>(acc + (size_t)row * C);
+  uint2* d = reinterpret_cast<uint2*>(dwte + (size_t)row * C);
+  for (int c = lane; c < (C >> 2); c += 64) {
+    float4 v = a[c];
+    float o[4];
+    unpack4(d[c], o);
+    o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
+    d[c] = pack4(o);
+    a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (lane == 0) touched[row] = 0;
+}
+
+// ---------------------------------------------------------------------------------- optimizer
+// sum of squares of a bf16 buffer (times scale^2) accumulated into *out (one atomic per block)
+__global__ __launch_bounds__(256) void k_sumsq_bf16(const uint2* __restrict__ g, int64_t n4, float scale,
+                                                    float* __restrict__ out) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float v[4];
+    unpack4(g[i], v);
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (sh[0] + sh[1] + sh[2] + sh[3]) * scale * scale);
+}
+
+// AdamW (torch semantics, decoupled decay) on fp32 master weights; writes the bf16 model copy.
+// decay_blk (nullable): per-64-element flag (flat layouts align every parameter to 64 elements).
+// clip_sumsq (nullable): device sum of squared (scaled) grads -> coef = min(1, max_norm / (norm + 1e-6)).
+__global__ __launch_bounds__(256) void k_adamw_master(float* __restrict__ master, uint2* __restrict__ p16,
+                                                      const uint2* __restrict__ g16, float4* __restrict__ m4,
+                                                      float4* __restrict__ v4, int64_t n4, float lr, float b1,
+                                                      float b2, float eps, float wd, float grad_scale, int step,
+                                                      const uint8_t* __restrict__ decay_blk,
+                                                      const float* __restrict__ clip_sumsq, float max_norm) {
+  float gs = grad_scale;
+  if (clip_sumsq) {
+    const float norm = sqrtf(*clip_sumsq);
+    gs *= fminf(1.f, max_norm / (norm + 1e-6f));
+  }
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  float4* mp = reinterpret_cast<float4*>(master);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 p = mp[i], m = m4[i], v = v4[i];
+    float g[4];
+    unpack4(g16[i], g);
+    const float dec = (decay_blk == nullptr || decay_blk[i >> 4]) ? (1.f - lr * wd) : 1.f;
+    float* pp = &p.x;
+    float* mm = &m.x;
+    float* vv = &v.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gg = g[e] * gs;
+      pp[e] *= dec;
+      mm[e] = mm[e] + (gg - mm[e]) * (1.f - b1);
+      vv[e] = vv[e] * b2 + (1.f - b2) * gg * gg;
+      const float denom = sqrtf(vv[e]) / bc2s + eps;
+      pp[e] -= step_size * mm[e] / denom;
+    }
+    mp[i] = p;
+    m4[i] = m;
+    v4[i] = v;
+    p16[i] = pack4(pp);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_f32_to_bf16(const float4* __restrict__ x, uint2* __restrict__ y, int64_t n4) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 v = x[i];
+    y[i] = pack4(&v.x);
+  }
+}
+
+inline int grid_for(int64_t n, int per_block, int cap = 4096) {
+  int64_t g = (n + per_block - 1) / per_block;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ launchers
+extern "C" {
+
+hipError_t pde_ln_fwd(const void* X, const void* G, const void* B, void* Y, float* mean, float* rstd, int N, int C,
+                      float eps, hipStream_t st) {
+  const int nch = (C / 4 + 63) / 64;
+  dim3 grid((N + 3) / 4);
+#define LNF(K)                                                                                          \
+  case K:                                                                                               \
+    hipLaunchKernelGGL(k_ln_fwd<K>, grid, dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)G,          \
+                       (const bf16_t*)B, (bf16_t*)Y, mean, rstd, N, C, eps);                            \
+    break;
+  switch (nch) {
+    LNF(1) LNF(2) LNF(3) LNF(4) LNF(5) LNF(6) LNF(7) LNF(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef LNF
+  return hipGetLastError();
+}
+
+int pde_ln_bwd_blocks(int N) {
+  const int rpw = (N + 4 * 256 - 1) / (4 * 256);
+  return (N + 4 * rpw - 1) / (4 * rpw);
+}
+
+hipError_t pde_ln_bwd(const void* dY, const void* X, const float* mean, const float* rstd, const void* G,
+                      const void* dRes, void* dX, float* part, void* dG, void* dB, int N, int C, int accumulate,
+                      hipStream_t st) {
+  const int nch = (C / 4 + 63) / 64;
+  const int rpw = (N + 4 * 256 - 1) / (4 * 256);
+  const int nblk = (N + 4 * rpw - 1) / (4 * rpw);
+  const size_t lds = (size_t)8 * C * sizeof(float);
+#define LNB(K)                                                                                          \
+  case K:                                                                                               \
+    hipLaunchKernelGGL(k_ln_bwd<K>, dim3(nblk), dim3(256), lds, st, (const bf16_t*)dY, (const bf16_t*)X, \
+                       mean, rstd, (const bf16_t*)G, (const bf16_t*)dRes, (bf16_t*)dX, part, N, C, rpw); \
+    break;
+  switch (nch) {
+    LNB(1) LNB(2) LNB(3) LNB(4) LNB(5) LNB(6) LNB(7) LNB(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef LNB
+  hipLaunchKernelGGL(k_ln_reduce, dim3((2 * C + 63) / 64), dim3(256), 0, st, part, nblk, 2 * C, (bf16_t*)dG,
+                     (bf16_t*)dB, C, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t pde_gelu_fwd(const void* X, void* Y, int64_t n, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(k_gelu_fwd, dim3(grid_for(n8, 256)), dim3(256), 0, st, (const uint4*)X, (uint4*)Y, n8);
+  return hipGetLastError();
+}
+
+hipError_t pde_gelu_bwd(const void* dY, const void* X, void* dX, int64_t n, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(k_gelu_bwd, dim3(grid_for(n8, 256)), dim3(256), 0, st, (const uint4*)dY, (const uint4*)X,
+                     (uint4*)dX, n8);
+  return hipGetLastError();
+}
+
+hipError_t pde_xent_bf16(void* logits, const int64_t* tgt, int N, int Vp, int V, float scale, float* loss_rows,
+                         int write_grad, hipStream_t st) {
+  hipLaunchKernelGGL(k_xent_bf16, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale, loss_rows,
+                     write_grad);
+  return hipGetLastError();
+}
+
+hipError_t pde_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int N, int T, int C,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_embed_fwd, dim3((N + 3) / 4), dim3(256), 0, st, idx, (const bf16_t*)wte, (const bf16_t*)wpe,
+                     (bf16_t*)out, N, T, C);
+  return hipGetLastError();
+}
+
+hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* dwpe, float* acc, uint8_t* touched,
+                         int N, int T, int C, int Vp, int accumulate_pos, hipStream_t st) {
+  hipLaunchKernelGGL(k_embed_bwd_pos, dim3((T * (C / 4) + 255) / 256), dim3(256), 0, st, (const bf16_t*)dX,
+                     (bf16_t*)dwpe, N, T, C, accumulate_pos);
+  hipLaunchKernelGGL(k_embed_bwd_tok, dim3((N + 3) / 4), dim3(256), 0, st, (const bf16_t*)dX, idx, acc, touched, N,
+                     C);
+  hipLaunchKernelGGL(k_embed_tok_merge, dim3((Vp + 3) / 4), dim3(256), 0, st, acc, touched, (bf16_t*)dwte, Vp, C);
+  return hipGetLastError();
+}
+
+hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(k_sumsq_bf16, dim3(grid_for(n4, 256, 1024)), dim3(256), 0, st, (const uint2*)g, n4, scale,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m, float* v, int64_t n, float lr,
+                            float b1, float b2, float eps, float wd, float grad_scale, int step,
+                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(k_adamw_master, dim3(grid_for(n4, 256, 2048)), dim3(256), 0, st, master, (uint2*)p16,
+                     (const uint2*)g16, (float4*)m, (float4*)v, n4, lr, b1, b2, eps, wd, grad_scale, step, decay_blk,
+                     clip_sumsq, max_norm);
+  return hipGetLastError();
+}
+
+hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(k_f32_to_bf16, dim3(grid_for(n4, 256)), dim3(256), 0, st, (const float4*)x, (uint2*)y, n4);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -9,6 +9,7 @@ import torch.nn.functional as F
 
 from .lenet_fused import LeNetFunction, lenet_forward, pack_conv2_weight  # noqa: F401
 from . import generic  # noqa: F401
+from . import transformer  # noqa: F401
 
 
 def linear(x, weight, bias=None):

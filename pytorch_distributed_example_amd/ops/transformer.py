@@ -1,0 +1,223 @@
+"""Transformer ops (bf16) over the HIP kernels of ``csrc/kernels/transformer.hip`` / ``attention.hip``.
+
+GPU tensors always run the framework kernels (no silent fallback: a missing extension raises).
+CPU tensors run the plain PyTorch definition of the same op -- used by the CPU test-suite to check
+model plumbing, and as the fp32 numerics reference of the GPU tests.
+
+Plain GEMMs (the c_attn / c_proj / c_fc projections and the tied LM head) are library GEMMs
+(``torch.matmul`` -> hipBLASLt on ROCm); everything around them is ours: LayerNorm, GELU, causal
+flash attention, the fused vocab softmax-cross-entropy that overwrites logits with dlogits in place
+(so the [N, 50304] logits tensor is written once and never re-materialised), and embeddings.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .._ext import kernels
+
+_BF16 = torch.bfloat16
+
+
+def _gpu(t):
+    return t.is_cuda
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# --------------------------------------------------------------------------------------- LayerNorm
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xc = _c(x)
+        C = xc.shape[-1]
+        N = xc.numel() // C
+        y = torch.empty_like(xc)
+        mean = torch.empty(N, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(N, device=x.device, dtype=torch.float32)
+        kernels().ln_fwd(xc, w, b, y, mean, rstd, eps)
+        ctx.save_for_backward(xc, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        C = x.shape[-1]
+        N = x.numel() // C
+        K = kernels()
+        dx = torch.empty_like(x)
+        part = torch.empty(K.ln_bwd_blocks(N) * 2 * C, device=x.device, dtype=torch.float32)
+        dw = torch.empty(C, device=x.device, dtype=w.dtype)
+        db = torch.empty(C, device=x.device, dtype=w.dtype)
+        K.ln_bwd(_c(dy), x, mean, rstd, w, None, dx, part, dw, db, False)
+        return dx, dw, db, None
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    if _gpu(x):
+        return LayerNormFn.apply(x, weight, bias, eps)
+    return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+
+
+# --------------------------------------------------------------------------------------- GELU
+class GeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        xc = _c(x)
+        y = torch.empty_like(xc)
+        kernels().gelu_fwd(xc, y)
+        ctx.save_for_backward(xc)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        kernels().gelu_bwd(_c(dy), x, dx)
+        return dx
+
+
+def gelu(x):
+    """tanh-approximate GELU (GPT-2's ``gelu_new``)."""
+    if _gpu(x):
+        return GeluFn.apply(x)
+    return F.gelu(x, approximate="tanh")
+
+
+# --------------------------------------------------------------------------------------- attention
+class CausalAttentionFn(torch.autograd.Function):
+    """qkv: [B, T, 3*H*64] (the c_attn output, read in place) -> y: [B, T, H*64]."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_head):
+        qkv = _c(qkv)
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        q, k, v = qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
+        o = torch.empty(B, T, C, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(B * n_head * T, device=qkv.device, dtype=torch.float32)
+        scale = 1.0 / math.sqrt(C // n_head)
+        kernels().attn_fwd(q, k, v, o, lse, n_head, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.n_head, ctx.scale = n_head, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        do = _c(do)
+        dqkv = torch.empty_like(qkv)
+        Dd = torch.empty(B * ctx.n_head * T, device=qkv.device, dtype=torch.float32)
+        sl = [slice(0, C), slice(C, 2 * C), slice(2 * C, 3 * C)]
+        q, k, v = (qkv[:, :, s] for s in sl)
+        dq, dk, dv = (dqkv[:, :, s] for s in sl)
+        kernels().attn_bwd(q, k, v, o, do, lse, Dd, dq, dk, dv, ctx.n_head, ctx.scale)
+        return dqkv, None
+
+
+def causal_attention(qkv, n_head: int):
+    if _gpu(qkv):
+        C = qkv.shape[-1] // 3
+        if C // n_head != 64:
+            raise NotImplementedError("flash attention kernel: head_dim 64")
+        return CausalAttentionFn.apply(qkv, n_head)
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    q, k, v = qkv.split(C, dim=2)
+    q, k, v = (t.view(B, T, n_head, C // n_head).transpose(1, 2) for t in (q, k, v))
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    return y.transpose(1, 2).reshape(B, T, C)
+
+
+# --------------------------------------------------------------------------------------- embeddings
+_EMB_SCRATCH = {}
+
+
+def _emb_scratch(device, Vp, C):
+    key = (device, Vp, C)
+    s = _EMB_SCRATCH.get(key)
+    if s is None:
+        s = (torch.zeros(Vp, C, device=device, dtype=torch.float32), torch.zeros(Vp, device=device, dtype=torch.uint8))
+        _EMB_SCRATCH[key] = s
+    return s
+
+
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe):
+        B, T = idx.shape
+        C = wte.shape[1]
+        idx = _c(idx.long())
+        out = torch.empty(B, T, C, device=wte.device, dtype=wte.dtype)
+        kernels().embed_fwd(idx, wte, wpe, out, T)
+        ctx.save_for_backward(idx)
+        ctx.shapes = (wte.shape, wpe.shape, T)
+        return out
+
+    @staticmethod
+    def backward(ctx, dx):
+        (idx,) = ctx.saved_tensors
+        wte_shape, wpe_shape, T = ctx.shapes
+        dwte = torch.zeros(wte_shape, device=dx.device, dtype=dx.dtype)
+        dwpe = torch.zeros(wpe_shape, device=dx.device, dtype=dx.dtype)
+        acc, touched = _emb_scratch(dx.device, wte_shape[0], wte_shape[1])
+        kernels().embed_bwd(_c(dx), idx, dwte, dwpe, acc, touched, T, False)
+        return None, dwte, dwpe
+
+
+def embedding(idx, wte, wpe):
+    if _gpu(wte):
+        return EmbeddingFn.apply(idx, wte, wpe)
+    T = idx.shape[1]
+    return F.embedding(idx, wte) + wpe[:T].unsqueeze(0)
+
+
+# --------------------------------------------------------------------------------------- LM head + CE
+class LMHeadLossFn(torch.autograd.Function):
+    """mean cross-entropy of logits = h @ W^T over the first V columns of W ([Vp, C], padded vocab).
+
+    Forward runs the GEMM and the fused softmax-CE kernel, which overwrites the logits buffer with
+    dlogits = (softmax - onehot) / N; backward is two GEMMs from that buffer."""
+
+    @staticmethod
+    def forward(ctx, h, w, targets, V):
+        C = h.shape[-1]
+        h2 = _c(h.reshape(-1, C))
+        N = h2.shape[0]
+        logits = torch.matmul(h2, w.t())                    # [N, Vp] bf16 (hipBLASLt)
+        rows = torch.empty(N, device=h.device, dtype=torch.float32)
+        tg = _c(targets.reshape(-1).long())
+        kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
+        tot = torch.empty(1, device=h.device, dtype=torch.float32)
+        kernels().colsum(rows, N, 1, tot)
+        ctx.save_for_backward(h2, w, logits)
+        ctx.hshape = h.shape
+        return (tot / N).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        h2, w, dlogits = ctx.saved_tensors
+        if not (isinstance(g, torch.Tensor) and g.numel() == 1):
+            raise RuntimeError("LM head loss expects a scalar gradient")
+        dl = dlogits if float(g) == 1.0 else dlogits * g.to(dlogits.dtype)
+        dh = torch.matmul(dl, w)                             # [N, C]
+        dw = torch.matmul(dl.t(), h2)                        # [Vp, C]
+        return dh.reshape(ctx.hshape), dw, None, None
+
+
+def lm_head_loss(h, w, targets, V: int):
+    if _gpu(h):
+        return LMHeadLossFn.apply(h, w, targets, V)
+    logits = torch.matmul(h, w.t())[..., :V].float()
+    return F.cross_entropy(logits.reshape(-1, V), targets.reshape(-1))
+
+
+def linear(x, w, b=None):
+    """Projection GEMM (hipBLASLt on GPU, bias fused in the epilogue)."""
+    return F.linear(x, w, b)

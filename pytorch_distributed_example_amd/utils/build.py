@@ -83,7 +83,8 @@ def _targets():
         ),
         "_kernels": dict(
             sources=[(s, hip_dev) for s in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))]
-            + [(os.path.join(CSRC, "ops_bindings.cpp"), torch_cpp)],
+            + [(os.path.join(CSRC, "ops_bindings.cpp"), torch_cpp)]
+            + [(s, torch_cpp) for s in sorted(glob.glob(os.path.join(CSRC, "bind_*.cpp")))],
             link=["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-L" + tlib,
                   "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
                   "-l:libamdhip64.so"] + rpath,

@@ -1,0 +1,197 @@
+"""Transformer kernels (bf16) vs plain PyTorch fp32 references of the same ops, and GPT-2 model /
+optimizer parity (GPU bf16 vs CPU fp32 with identical weights)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_example_amd.ops import transformer as T
+from pytorch_distributed_example_amd.models import GPTConfig, build_gpt2
+from pytorch_distributed_example_amd.optim import AdamWMaster
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N,C", [(300, 768), (64, 1000), (5, 128), (17, 2048)])
+def test_layernorm(N, C):
+    torch.manual_seed(0)
+    x = (torch.randn(N, C) * 2 + 0.5).to(dev, torch.bfloat16).requires_grad_()
+    w = (1 + 0.1 * torch.randn(C)).to(dev, torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(C)).to(dev, torch.bfloat16).requires_grad_()
+    y = T.layer_norm(x, w, b)
+    g = torch.randn(N, C).to(dev, torch.bfloat16)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(g.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    assert rel_err(b.grad, br.grad) < 2e-2
+
+
+def test_gelu():
+    torch.manual_seed(1)
+    x = (torch.randn(4096) * 3).to(dev, torch.bfloat16).requires_grad_()
+    y = T.gelu(x)
+    g = torch.randn(4096).to(dev, torch.bfloat16)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    yr = F.gelu(xr, approximate="tanh")
+    yr.backward(g.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,V,Vp", [(37, 1000, 1024), (8, 50257, 50304)])
+def test_lm_head_loss(N, V, Vp):
+    torch.manual_seed(2)
+    C = 64
+    h = torch.randn(N, C).to(dev, torch.bfloat16).requires_grad_()
+    w = (0.5 * torch.randn(Vp, C)).to(dev, torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (N,), device=dev)
+    loss = T.lm_head_loss(h, w, tgt, V)
+    loss.backward()
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    lr = F.cross_entropy((hr @ wr.t())[:, :V], tgt)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 2e-2 * max(1.0, abs(lr.item()))
+    assert rel_err(h.grad, hr.grad) < 3e-2
+    assert rel_err(w.grad, wr.grad) < 3e-2
+    assert w.grad[V:].abs().max().item() == 0.0        # padded vocab rows get no gradient
+
+
+def test_embedding():
+    torch.manual_seed(3)
+    B, Tn, C, Vp = 4, 128, 128, 512
+    idx = torch.randint(0, 40, (B, Tn), device=dev)   # many repeats -> exercises the atomic path
+    wte = torch.randn(Vp, C).to(dev, torch.bfloat16).requires_grad_()
+    wpe = torch.randn(Tn, C).to(dev, torch.bfloat16).requires_grad_()
+    x = T.embedding(idx, wte, wpe)
+    g = torch.randn(B, Tn, C).to(dev, torch.bfloat16)
+    x.backward(g)
+    wter, wper = wte.detach().float().requires_grad_(), wpe.detach().float().requires_grad_()
+    xr = F.embedding(idx, wter) + wper.unsqueeze(0)
+    xr.backward(g.float())
+    assert rel_err(x, xr) < 1e-2
+    assert rel_err(wte.grad, wter.grad) < 2e-2
+    assert rel_err(wpe.grad, wper.grad) < 2e-2
+    # scratch is left clean: a second backward gives the same result
+    wte.grad = None
+    T.embedding(idx, wte, wpe).backward(g)
+    assert rel_err(wte.grad, wter.grad) < 2e-2
+
+
+def _attn_ref(qkv, H):
+    B, Tn, C3 = qkv.shape
+    C = C3 // 3
+    q, k, v = qkv.float().split(C, dim=2)
+    q, k, v = (t.reshape(B, Tn, H, C // H).transpose(1, 2) for t in (q, k, v))
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(C // H)
+    mask = torch.triu(torch.ones(Tn, Tn, dtype=torch.bool, device=qkv.device), 1)
+    s = s.masked_fill(mask, float("-inf"))
+    y = torch.softmax(s, -1) @ v
+    return y.transpose(1, 2).reshape(B, Tn, C)
+
+
+@pytest.mark.parametrize("B,Tn,H", [(2, 256, 3), (1, 128, 1), (1, 1024, 12)])
+def test_flash_attention(B, Tn, H):
+    torch.manual_seed(4)
+    C = 64 * H
+    qkv = torch.randn(B, Tn, 3 * C).to(dev, torch.bfloat16).requires_grad_()
+    y = T.causal_attention(qkv, H)
+    g = torch.randn(B, Tn, C).to(dev, torch.bfloat16)
+    y.backward(g)
+    qr = qkv.detach().float().requires_grad_()
+    yr = _attn_ref(qr, H)
+    yr.backward(g.float())
+    assert rel_err(y, yr) < 2e-2
+    dq, dk, dv = qkv.grad.split(C, dim=2)
+    rq, rk, rv = qr.grad.split(C, dim=2)
+    assert rel_err(dv, rv) < 3e-2
+    assert rel_err(dk, rk) < 3e-2
+    assert rel_err(dq, rq) < 3e-2
+
+
+def _tiny_cfg():
+    return GPTConfig(block_size=128, vocab_size=1000, padded_vocab=1024, n_layer=2, n_head=2, n_embd=128)
+
+
+def test_gpt2_gpu_matches_cpu_fp32():
+    cfg = _tiny_cfg()
+    g = build_gpt2(cfg, seed=0, device=dev)
+    c = build_gpt2(cfg, seed=0, dtype=torch.float32)
+    with torch.no_grad():
+        for pc, pg in zip(c.parameters(), g.parameters()):
+            pc.copy_(pg.float())          # identical (bf16-representable) weights
+    torch.manual_seed(5)
+    idx = torch.randint(0, cfg.vocab_size, (2, 128))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 128))
+    lg = g(idx.to(dev), tgt.to(dev))
+    lc = c(idx, tgt)
+    lg.backward()
+    lc.backward()
+    assert abs(lg.item() - lc.item()) < 3e-2
+    for (n, pg), pc in zip(g.named_parameters(), c.parameters()):
+        cos = F.cosine_similarity(pg.grad.float().flatten().cpu(), pc.grad.flatten(), dim=0).item()
+        assert cos > 0.98, (n, cos)
+
+
+def test_adamw_master_matches_torch():
+    torch.manual_seed(6)
+    p16 = [torch.randn(64, 33).to(dev, torch.bfloat16).requires_grad_(), torch.randn(100).to(dev, torch.bfloat16)
+           .requires_grad_()]
+    ref = [p.detach().float().clone().requires_grad_() for p in p16]
+    opt = AdamWMaster([{"params": [p16[0]], "weight_decay": 0.1}, {"params": [p16[1]], "weight_decay": 0.0}],
+                      lr=1e-2, betas=(0.9, 0.95))
+    ropt = torch.optim.AdamW([{"params": [ref[0]], "weight_decay": 0.1}, {"params": [ref[1]], "weight_decay": 0.0}],
+                             lr=1e-2, betas=(0.9, 0.95), foreach=False)
+    for _ in range(4):
+        grads = [torch.randn_like(r) for r in ref]
+        for p, r, gg in zip(p16, ref, grads):
+            p.grad = gg.to(torch.bfloat16)
+            r.grad = p.grad.float()
+        opt.step()
+        ropt.step()
+    for p, r in zip(p16, ref):
+        st = opt.state[p]
+        assert torch.allclose(st["master"], r.detach(), atol=1e-5, rtol=1e-4)
+        assert rel_err(p, r) < 1e-2
+
+
+def test_adamw_master_clipping():
+    torch.manual_seed(7)
+    p = torch.randn(256).to(dev, torch.bfloat16).requires_grad_()
+    r = p.detach().float().clone().requires_grad_()
+    opt = AdamWMaster([p], lr=1e-2, weight_decay=0.0, max_grad_norm=0.5)
+    ropt = torch.optim.AdamW([r], lr=1e-2, weight_decay=0.0, betas=(0.9, 0.95), foreach=False)
+    g = torch.randn(256) * 3
+    p.grad = g.to(dev, torch.bfloat16)
+    r.grad = p.grad.float()
+    torch.nn.utils.clip_grad_norm_([r], 0.5)
+    opt.step()
+    ropt.step()
+    assert torch.allclose(opt.state[p]["master"], r.detach(), atol=1e-5, rtol=1e-4)
+
+
+def test_gpt2_trains():
+    cfg = _tiny_cfg()
+    m = build_gpt2(cfg, seed=1, device=dev)
+    opt = AdamWMaster(m.decay_groups(0.1), lr=3e-3, max_grad_norm=1.0)
+    torch.manual_seed(8)
+    idx = torch.randint(0, cfg.vocab_size, (4, 128), device=dev)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = m(idx, torch.roll(idx, -1, 1))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0], losses
