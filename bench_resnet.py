@@ -1,0 +1,55 @@
+"""ResNet-18 bf16 benchmark (``python bench.py --model resnet18``): synthetic 3x224x224 images,
+channels-last bf16, DDP over RCCL, fused BN+ReLU kernels, SGD(momentum 0.9, wd 5e-5) with fp32
+master weights.  Metric: images/s for the whole node (weak scaling: fixed per-GPU batch)."""
+from __future__ import annotations
+
+import json
+
+from bench_models import _setup, _timed
+
+
+def bench_resnet18(args):
+    torch, dist, rank, world, dev = _setup()
+    from pytorch_distributed_example_amd import ops
+    from pytorch_distributed_example_amd.models import build_resnet18
+    from pytorch_distributed_example_amd.optim import SGDMaster
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    B = args.batch_size if args.batch_size != 128 else 256
+    model = build_resnet18(seed=args.seed, device=dev)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    opt = SGDMaster(model.decay_groups(5e-5), lr=0.1, momentum=0.9)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + rank)
+    xs = torch.randn(2, B, 3, 224, 224, device=dev, generator=g).to(torch.bfloat16)
+    xs = [x.contiguous(memory_format=torch.channels_last) for x in xs]
+    ys = torch.randint(0, 1000, (2, B), device=dev, generator=g)
+    it = [0]
+    losses = []
+
+    def step():
+        i = it[0] % 2
+        it[0] += 1
+        opt.zero_grad()
+        loss = ops.cross_entropy(ddp(xs[i]).float(), ys[i])
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach())
+
+    elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
+    ips = args.steps * B * world / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node), ResNet-18 bf16 DDP",
+            "value": round(ips, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic 3x224x224 N(0,1) images, random labels, random-init weights",
+            "config": {"model": "ResNet-18 (11.69M params, torchvision layout)", "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
+                       "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", "bucket_mb": args.bucket_mb,
+                       "memory_format": "channels_last"},
+            "last_loss": round(float(losses[-1]), 4),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()

@@ -1,0 +1,103 @@
+// torch bindings of the ResNet kernels (csrc/kernels/resnet.hip): fused BatchNorm(+residual)+ReLU
+// over channels-last bf16 activations, and the SGD step with fp32 master weights.
+#include "pde_bind.h"
+#include "pde_kernels.h"
+
+namespace pde {
+namespace {
+
+int64_t nhwc_rows(const at::Tensor& x, const char* name) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == BF16, name, " must be a bf16 GPU tensor");
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels-last");
+    return x.size(0) * x.size(2) * x.size(3);
+  }
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), name, " must be [N, C] contiguous or 4-D channels-last");
+  return x.size(0);
+}
+
+void check_same(const at::Tensor& a, const at::Tensor& b, const char* name) {
+  TORCH_CHECK(a.sizes() == b.sizes() && a.strides() == b.strides() && a.scalar_type() == b.scalar_type(), name,
+              " must match the input's shape / layout / dtype");
+}
+
+void check_c(int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "batchnorm kernel: C must be 8 * a power of two <= 2048");
+}
+
+int64_t bn_blocks(int64_t M, int64_t C) { return pde_bn_blocks((int)M, (int)C); }
+
+void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta,
+            double eps, double momentum, const OptT& run_mean, const OptT& run_var, const at::Tensor& part,
+            const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift, bool relu,
+            bool training) {
+  const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
+  check_c(C);
+  check_same(x, y, "y");
+  const void* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_same(x, *res, "residual");
+    r = res->data_ptr();
+  }
+  check_cuda(gamma, "gamma", BF16, C);
+  check_cuda(beta, "beta", BF16, C);
+  float* rm = optr<float>(run_mean, "running_mean", F32, C);
+  float* rv = optr<float>(run_var, "running_var", F32, C);
+  if (training) check_cuda(part, "part", F32, (int64_t)pde_bn_blocks((int)M, (int)C) * 2 * C);
+  for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
+  hip_check(pde_bn_fwd(x.data_ptr(), r, y.data_ptr(), (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
+                       (float)momentum, rm, rv, ptr<float>(part), ptr<float>(mean), ptr<float>(rstd), ptr<float>(scale),
+                       ptr<float>(shift), relu, training, cur_stream()),
+            "bn_fwd");
+}
+
+void bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& x, const at::Tensor& gamma,
+            const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& part, const at::Tensor& coef,
+            const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dx, const OptT& dres, bool relu) {
+  const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
+  check_c(C);
+  check_same(x, dy, "dy");
+  check_same(x, y, "y");
+  check_same(x, dx, "dx");
+  void* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_same(x, *dres, "dres");
+    dr = dres->data_ptr();
+  }
+  check_cuda(gamma, "gamma", BF16, C);
+  check_cuda(mean, "mean", F32, C);
+  check_cuda(rstd, "rstd", F32, C);
+  check_cuda(part, "part", F32, (int64_t)pde_bn_blocks((int)M, (int)C) * 2 * C);
+  check_cuda(coef, "coef", F32, 3 * C);
+  check_cuda(dgamma, "dgamma", BF16, C);
+  check_cuda(dbeta, "dbeta", BF16, C);
+  hip_check(pde_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), (int)M, (int)C, gamma.data_ptr(), ptr<float>(mean),
+                       ptr<float>(rstd), ptr<float>(part), ptr<float>(coef), dgamma.data_ptr(), dbeta.data_ptr(),
+                       dx.data_ptr(), dr, relu, cur_stream()),
+            "bn_bwd");
+}
+
+void sgd_master(const at::Tensor& master, const at::Tensor& p16, const at::Tensor& g16, const at::Tensor& buf,
+                double lr, double momentum, double wd, bool nesterov, double grad_scale, const OptT& decay_blk) {
+  const int64_t n = master.numel();
+  TORCH_CHECK(n % 64 == 0, "sgd_master: flat buffers are padded to 64 elements");
+  check_cuda(master, "master", F32);
+  check_cuda(p16, "param_bf16", BF16, n);
+  check_cuda(g16, "grad_bf16", BF16, n);
+  check_cuda(buf, "momentum_buffer", F32, n);
+  const uint8_t* db = optr<uint8_t>(decay_blk, "decay_blk", U8, n / 64);
+  hip_check(pde_sgd_master(ptr<float>(master), p16.data_ptr(), g16.data_ptr(), ptr<float>(buf), n, (float)lr,
+                           (float)momentum, (float)wd, nesterov, (float)grad_scale, db, cur_stream()),
+            "sgd_master");
+}
+
+}  // namespace
+
+void register_resnet(pybind11::module& m) {
+  m.def("bn_blocks", &bn_blocks);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("sgd_master", &sgd_master);
+}
+
+}  // namespace pde

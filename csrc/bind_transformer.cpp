@@ -130,6 +130,12 @@ void f32_to_bf16(const at::Tensor& x, const at::Tensor& y) {
   hip_check(pde_f32_to_bf16(ptr<float>(x), y.data_ptr(), x.numel(), cur_stream()), "f32_to_bf16");
 }
 
+void sum_f32(const at::Tensor& x, const at::Tensor& out) {
+  check_cuda(x, "x", F32);
+  check_cuda(out, "out", F32, 1);
+  hip_check(pde_sum_f32(ptr<float>(x), (int)x.numel(), ptr<float>(out), cur_stream()), "sum_f32");
+}
+
 // q/k/v: views into a [B, T, ld] bf16 buffer (column offset = section start); o: [B, T, H*64]
 void check_qkv(const at::Tensor& t, const char* name, int64_t B, int64_t T, int64_t H) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == BF16, name, " must be a bf16 GPU tensor");
@@ -192,6 +198,7 @@ void register_transformer(pybind11::module& m) {
         py::arg("step"), py::arg("decay_blk") = py::none(), py::arg("clip_sumsq") = py::none(),
         py::arg("max_norm") = 1.0);
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("sum_f32", &sum_f32);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }

@@ -85,6 +85,7 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
                             float b1, float b2, float eps, float wd, float grad_scale, int step,
                             const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st);
 hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
+hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st);
 
 // ---- attention (attention.hip) ----
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
@@ -92,6 +93,18 @@ hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, vo
 hipError_t pde_attn_bwd(const void* q, const void* k, const void* v, int ldq, const void* o, const void* dout,
                         int ldo, const float* lse, float* Dd, void* dq, void* dk, void* dv, int B, int T, int H,
                         float scale, hipStream_t st);
+
+
+// ---- resnet (resnet.hip) ----
+int pde_bn_blocks(int M, int C);
+hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
+                      float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
+                      float* rstd, float* scale, float* shift, int relu, int training, hipStream_t st);
+hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
+                      const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
+                      int relu, hipStream_t st);
+hipError_t pde_sgd_master(float* master, void* p16, const void* g16, float* buf, int64_t n, float lr, float momentum,
+                          float wd, int nesterov, float grad_scale, const uint8_t* decay_blk, hipStream_t st);
 
 #ifdef __cplusplus
 }

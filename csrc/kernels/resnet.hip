@@ -1,0 +1,300 @@
+// ResNet kernels for gfx950: training-mode BatchNorm over NHWC bf16 activations fused with the
+// residual add and ReLU (forward: stats -> finalize -> apply; backward: reduce -> finalize -> apply),
+// and the SGD(momentum) step on bf16 weights with fp32 master weights.
+//
+// NHWC = rows of C channels.  A 256-thread block owns a contiguous row range; thread t handles the
+// 8-channel chunk t % (C/8) of rows t / (C/8) + k*RP (RP = 256 / (C/8)), so per-channel partial sums
+// stay in registers and one LDS pass folds the RP row-lanes.  Partials [nblk][2C] are reduced by a
+// per-channel finalize kernel that also produces the fused per-channel coefficients of the apply
+// pass (y = x*scale + shift (+res), relu; dx = A*dy' + B*x + Cc, dy' = dy*(y>0)).
+#include "pde_hip.h"
+#include "pde_bf16.h"
+#include "pde_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ void bn_geom(int C, int& CP, int& RP) {
+  CP = C >> 3;
+  RP = 256 / CP;
+}
+
+// ------------------------------------------------------------------------------- forward stats
+__global__ __launch_bounds__(256) void k_bn_stats(const uint4* __restrict__ X, int M, int C, int rows_per_block,
+                                                  float* __restrict__ part) {
+  extern __shared__ float sh[];  // [RP][2][C]
+  int CP, RP;
+  bn_geom(C, CP, RP);
+  const int tid = threadIdx.x, c8 = tid % CP, rl = tid / CP;
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rl < RP) {
+    int r = r0 + rl;
+    for (; r + RP < r1; r += 2 * RP) {  // two rows in flight
+      float v[8], w[8];
+      unpack8(X[(size_t)r * CP + c8], v);
+      unpack8(X[(size_t)(r + RP) * CP + c8], w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += v[e] + w[e];
+        q[e] += v[e] * v[e] + w[e] * w[e];
+      }
+    }
+    for (; r < r1; r += RP) {
+      float v[8];
+      unpack8(X[(size_t)r * CP + c8], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += v[e];
+        q[e] += v[e] * v[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sh[(rl * 2 + 0) * C + c8 * 8 + e] = s[e];
+      sh[(rl * 2 + 1) * C + c8 * 8 + e] = q[e];
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < 2 * C; k += 256) {
+    const int which = k / C, c = k % C;
+    float t = 0.f;
+    for (int j = 0; j < RP; ++j) t += sh[(j * 2 + which) * C + c];
+    part[(size_t)blockIdx.x * 2 * C + k] = t;
+  }
+}
+
+// per channel: mean / biased var -> rstd, running-stat update (unbiased var), scale / shift
+__global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int M,
+                                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                                     float eps, float momentum, float* __restrict__ run_mean,
+                                                     float* __restrict__ run_var, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, float* __restrict__ scale,
+                                                     float* __restrict__ shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;  // fp64 accumulation of the (few hundred) block partials
+  for (int b = 0; b < nblk; ++b) {
+    s += part[(size_t)b * 2 * C + c];
+    q += part[(size_t)b * 2 * C + C + c];
+  }
+  const double mean = s / M;
+  const double var = fmax(q / M - mean * mean, 0.0);
+  const float rstd = rsqrtf((float)var + eps);
+  if (run_mean) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * M / (double)max(M - 1, 1));
+  }
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  const float g = bf2f(gamma[c]), bt = bf2f(beta[c]);
+  scale[c] = g * rstd;
+  shift[c] = bt - (float)mean * g * rstd;
+}
+
+// y = x*scale + shift (+ res), optional relu
+__global__ __launch_bounds__(256) void k_bn_apply(const uint4* __restrict__ X, const uint4* __restrict__ R,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  uint4* __restrict__ Y, int64_t n8, int CP, int relu) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(i % CP) * 8;
+    float v[8], r[8];
+    unpack8(X[i], v);
+    if (R) unpack8(R[i], r);
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + c0), s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(shift + c0), h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = v[e] * sc[e] + sf[e] + (R ? r[e] : 0.f);
+      v[e] = relu ? fmaxf(o, 0.f) : o;
+    }
+    Y[i] = pack8(v);
+  }
+}
+
+// ------------------------------------------------------------------------------- backward
+// part[blk] = (sum dy', sum dy' * xhat) per channel, dy' = dy * (y > 0) when relu
+__global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__ dY, const uint4* __restrict__ Y,
+                                                       const uint4* __restrict__ X, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, int M, int C,
+                                                       int rows_per_block, int relu, float* __restrict__ part) {
+  extern __shared__ float sh[];
+  int CP, RP;
+  bn_geom(C, CP, RP);
+  const int tid = threadIdx.x, c8 = tid % CP, rl = tid / CP;
+  float s[8], q[8], mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s[e] = q[e] = 0.f;
+    mu[e] = mean[c8 * 8 + e];
+    rs[e] = rstd[c8 * 8 + e];
+  }
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rl < RP) {
+    for (int r = r0 + rl; r < r1; r += RP) {
+      const size_t i = (size_t)r * CP + c8;
+      float g[8], x[8], y[8];
+      unpack8(dY[i], g);
+      unpack8(X[i], x);
+      if (relu) unpack8(Y[i], y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = relu ? (y[e] > 0.f ? g[e] : 0.f) : g[e];
+        s[e] += d;
+        q[e] += d * (x[e] - mu[e]) * rs[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sh[(rl * 2 + 0) * C + c8 * 8 + e] = s[e];
+      sh[(rl * 2 + 1) * C + c8 * 8 + e] = q[e];
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < 2 * C; k += 256) {
+    const int which = k / C, c = k % C;
+    float t = 0.f;
+    for (int j = 0; j < RP; ++j) t += sh[(j * 2 + which) * C + c];
+    part[(size_t)blockIdx.x * 2 * C + k] = t;
+  }
+}
+
+// dgamma = sum dy'*xhat, dbeta = sum dy'; dx = A*dy' + B*x + Cc with A = g*rstd,
+// B = -A*rstd*mean(dy'xhat), Cc = -A*mean(dy') - B*mean
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float* __restrict__ part, int nblk, int C, int M,
+                                                         const bf16_t* __restrict__ gamma,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, bf16_t* __restrict__ dgamma,
+                                                         bf16_t* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f, q = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    s += part[(size_t)b * 2 * C + c];
+    q += part[(size_t)b * 2 * C + C + c];
+  }
+  dgamma[c] = f2bf(q);
+  dbeta[c] = f2bf(s);
+  const float A = bf2f(gamma[c]) * rstd[c];
+  const float Bc = -A * rstd[c] * (q / M);
+  coef[c] = A;
+  coef[C + c] = Bc;
+  coef[2 * C + c] = -A * (s / M) - Bc * mean[c];
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint4* __restrict__ dY, const uint4* __restrict__ Y,
+                                                      const uint4* __restrict__ X, const float* __restrict__ coef,
+                                                      uint4* __restrict__ dX, uint4* __restrict__ dR, int64_t n8,
+                                                      int C, int relu) {
+  const int CP = C >> 3;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(i % CP) * 8;
+    float g[8], x[8], y[8], o[8];
+    unpack8(dY[i], g);
+    unpack8(X[i], x);
+    if (relu) unpack8(Y[i], y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = relu ? (y[e] > 0.f ? g[e] : 0.f) : g[e];
+      g[e] = d;
+      o[e] = coef[c0 + e] * d + coef[C + c0 + e] * x[e] + coef[2 * C + c0 + e];
+    }
+    dX[i] = pack8(o);
+    if (dR) dR[i] = pack8(g);
+  }
+}
+
+// ------------------------------------------------------------------------------- SGD (master)
+// torch.optim.SGD semantics (coupled weight decay, dampening 0): g' = g*s + wd*p; buf = mom*buf + g'
+// (buf starts at 0, which equals torch's buf = g' on the first step); p -= lr * (nesterov ? g' + mom*buf : buf)
+__global__ __launch_bounds__(256) void k_sgd_master(float* __restrict__ master, uint2* __restrict__ p16,
+                                                    const uint2* __restrict__ g16, float4* __restrict__ buf, int64_t n4,
+                                                    float lr, float momentum, float wd, int nesterov, float grad_scale,
+                                                    const uint8_t* __restrict__ decay_blk) {
+  float4* mp = reinterpret_cast<float4*>(master);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 p = mp[i], b = buf[i];
+    float g[4];
+    unpack4(g16[i], g);
+    const float w = (decay_blk == nullptr || decay_blk[i >> 4]) ? wd : 0.f;
+    float* pp = &p.x;
+    float* bb = &b.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gg = g[e] * grad_scale + w * pp[e];
+      bb[e] = momentum * bb[e] + gg;
+      pp[e] -= lr * (nesterov ? gg + momentum * bb[e] : bb[e]);
+    }
+    mp[i] = p;
+    buf[i] = b;
+    p16[i] = pack4(pp);
+  }
+}
+
+inline int grid_cap(int64_t n, int cap) {
+  int64_t g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int pde_bn_blocks(int M, int C) {
+  // ~2 blocks per CU, each at least a few row-lane strides long
+  const int rp = 256 / (C / 8);
+  int nblk = 512;
+  const int min_rows = rp * 8;
+  if ((M + nblk - 1) / nblk < min_rows) nblk = (M + min_rows - 1) / min_rows;
+  return nblk < 1 ? 1 : nblk;
+}
+
+hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
+                      float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
+                      float* rstd, float* scale, float* shift, int relu, int training, hipStream_t st) {
+  if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
+  const int CP = C / 8, RP = 256 / CP;
+  if (training) {
+    const int nblk = pde_bn_blocks(M, C);
+    const int rpb = (M + nblk - 1) / nblk;
+    hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)x,
+                       M, C, rpb, part);
+    hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, M,
+                       (const bf16_t*)gamma, (const bf16_t*)beta, eps, momentum, run_mean, run_var, mean, rstd, scale,
+                       shift);
+  }
+  const int64_t n8 = (int64_t)M * CP;
+  hipLaunchKernelGGL(k_bn_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)x, (const uint4*)res,
+                     scale, shift, (uint4*)y, n8, CP, relu);
+  return hipGetLastError();
+}
+
+hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
+                      const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
+                      int relu, hipStream_t st) {
+  if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
+  const int CP = C / 8, RP = 256 / CP;
+  const int nblk = pde_bn_blocks(M, C);
+  const int rpb = (M + nblk - 1) / nblk;
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
+                     (const uint4*)dy, (const uint4*)y, (const uint4*)x, mean, rstd, M, C, rpb, relu, part);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, M,
+                     (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
+  const int64_t n8 = (int64_t)M * CP;
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dy, (const uint4*)y,
+                     (const uint4*)x, coef, (uint4*)dx, (uint4*)dres, n8, C, relu);
+  return hipGetLastError();
+}
+
+hipError_t pde_sgd_master(float* master, void* p16, const void* g16, float* buf, int64_t n, float lr, float momentum,
+                          float wd, int nesterov, float grad_scale, const uint8_t* decay_blk, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(k_sgd_master, dim3(grid_cap(n4, 2048)), dim3(256), 0, st, master, (uint2*)p16,
+                     (const uint2*)g16, (float4*)buf, n4, lr, momentum, wd, nesterov, grad_scale, decay_blk);
+  return hipGetLastError();
+}
+
+}  // extern "C"

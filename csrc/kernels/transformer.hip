@@ -448,6 +448,21 @@ __global__ __launch_bounds__(256) void k_f32_to_bf16(const float4* __restrict__ 
   }
 }
 
+// out[0] = sum(x[0..n)) (one 1024-thread block; n up to a few 1e5 -- loss rows)
+__global__ __launch_bounds__(1024) void k_sum_f32(const float* __restrict__ x, int n, float* __restrict__ out) {
+  __shared__ float sh[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < 16 ? sh[threadIdx.x] : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) out[0] = t;
+  }
+}
+
 inline int grid_for(int64_t n, int per_block, int cap = 4096) {
   int64_t g = (n + per_block - 1) / per_block;
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -553,6 +568,11 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
   hipLaunchKernelGGL(k_adamw_master, dim3(grid_for(n4, 256, 2048)), dim3(256), 0, st, master, (uint2*)p16,
                      (const uint2*)g16, (float4*)m, (float4*)v, n4, lr, b1, b2, eps, wd, grad_scale, step, decay_blk,
                      clip_sumsq, max_norm);
+  return hipGetLastError();
+}
+
+hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_f32, dim3(1), dim3(1024), 0, st, x, n, out);
   return hipGetLastError();
 }
 

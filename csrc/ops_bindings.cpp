@@ -370,6 +370,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("arch") = "gfx950";
   namespace py = pybind11;
   pde::register_transformer(m);
+  pde::register_resnet(m);
   m.def("lenet_conv_fwd", &lenet_conv_fwd, py::arg("X"), py::arg("idx"), py::arg("step"), py::arg("nbatches"),
         py::arg("stride"), py::arg("labels_all"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wt2"),
         py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("cur_row"),

@@ -1,0 +1,111 @@
+"""ResNet-18 (bf16, channels-last) -- driver-added config of BASELINE.json ("ResNet-18 bf16 on
+synthetic 3x224x224, DDP 8xMI355X").  Same architecture / parameter names as torchvision's
+``resnet18`` (conv1/bn1, layer1..layer4 of BasicBlocks with downsample, fc), so state_dicts
+interchange; BatchNorm+residual+ReLU run as fused HIP kernels (``ops.resnet``), convolutions as
+MIOpen convolutions on channels-last bf16.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as tnn
+import torch.nn.functional as F
+
+from ..ops.resnet import batch_norm_act
+
+
+class BN(tnn.Module):
+    """BatchNorm2d with torchvision's parameter / buffer names; running stats stay fp32."""
+
+    def __init__(self, C, momentum=0.1, eps=1e-5, zero_init=False):
+        super().__init__()
+        self.weight = tnn.Parameter(torch.zeros(C) if zero_init else torch.ones(C))
+        self.bias = tnn.Parameter(torch.zeros(C))
+        self.register_buffer("running_mean", torch.zeros(C))
+        self.register_buffer("running_var", torch.ones(C))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        self.momentum, self.eps = momentum, eps
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        # keep running statistics fp32 when the module is cast to bf16
+        self.running_mean.data = self.running_mean.data.float()
+        self.running_var.data = self.running_var.data.float()
+        return self
+
+    def forward(self, x, residual=None, relu=True):
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
+                              self.momentum, self.eps, residual, relu)
+
+
+def _conv(cin, cout, k, stride=1, pad=0):
+    c = tnn.Conv2d(cin, cout, k, stride, pad, bias=False)
+    tnn.init.kaiming_normal_(c.weight, mode="fan_out", nonlinearity="relu")
+    return c
+
+
+class BasicBlock(tnn.Module):
+    expansion = 1
+
+    def __init__(self, cin, cout, stride=1, zero_init_residual=False):
+        super().__init__()
+        self.conv1 = _conv(cin, cout, 3, stride, 1)
+        self.bn1 = BN(cout)
+        self.conv2 = _conv(cout, cout, 3, 1, 1)
+        self.bn2 = BN(cout, zero_init=zero_init_residual)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = tnn.Sequential(_conv(cin, cout, 1, stride), BN(cout))
+
+    def forward(self, x):
+        if self.downsample is not None:
+            idt = self.downsample[1](self.downsample[0](x), relu=False)
+        else:
+            idt = x
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), residual=idt, relu=True)
+
+
+class ResNet(tnn.Module):
+    def __init__(self, layers=(2, 2, 2, 2), num_classes=1000, zero_init_residual=False):
+        super().__init__()
+        self.conv1 = _conv(3, 64, 7, 2, 3)
+        self.bn1 = BN(64)
+        widths = (64, 128, 256, 512)
+        cin = 64
+        for i, (w, n) in enumerate(zip(widths, layers)):
+            blocks = []
+            for j in range(n):
+                blocks.append(BasicBlock(cin, w, 2 if (j == 0 and i > 0) else 1, zero_init_residual))
+                cin = w
+            setattr(self, f"layer{i + 1}", tnn.Sequential(*blocks))
+        self.fc = tnn.Linear(512, num_classes)
+        bound = 1 / math.sqrt(512)
+        tnn.init.uniform_(self.fc.weight, -bound, bound)
+        tnn.init.uniform_(self.fc.bias, -bound, bound)
+
+    def forward(self, x):
+        x = self.bn1(self.conv1(x))
+        x = F.max_pool2d(x, 3, 2, 1)
+        for i in range(1, 5):
+            x = getattr(self, f"layer{i}")(x)
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+    def decay_groups(self, weight_decay: float):
+        """SGD groups: conv / fc weights decay; BN parameters and biases do not."""
+        decay = [p for n, p in self.named_parameters() if p.dim() > 1]
+        nodecay = [p for n, p in self.named_parameters() if p.dim() <= 1]
+        return [{"params": decay, "weight_decay": weight_decay}, {"params": nodecay, "weight_decay": 0.0}]
+
+
+def build_resnet18(num_classes=1000, seed=0, device=None, dtype=torch.bfloat16) -> ResNet:
+    torch.manual_seed(seed)
+    m = ResNet((2, 2, 2, 2), num_classes)
+    m = m.to(device=device, dtype=dtype)
+    if device is not None and torch.device(device).type == "cuda":
+        m = m.to(memory_format=torch.channels_last)
+    return m

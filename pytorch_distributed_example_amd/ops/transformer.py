@@ -195,7 +195,7 @@ class LMHeadLossFn(torch.autograd.Function):
         tg = _c(targets.reshape(-1).long())
         kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
         tot = torch.empty(1, device=h.device, dtype=torch.float32)
-        kernels().colsum(rows, N, 1, tot)
+        kernels().sum_f32(rows, tot)
         ctx.save_for_backward(h2, w, logits)
         ctx.hshape = h.shape
         return (tot / N).reshape(())

@@ -1,17 +1,17 @@
-"""AdamW for bf16 models with fp32 master weights: one fused HIP launch per step (+1 for clipping).
+"""Optimizers for bf16 models with fp32 master weights: one fused HIP launch per step.
 
-The model's parameters are bf16 (what the GEMMs and the gradient all-reduce move); this optimizer
-owns fp32 master copies, exp_avg and exp_avg_sq as flat buffers aligned with the parameters' flat
-layout (shared with DDP's buckets when the model is wrapped first), so the update
+The model's parameters are bf16 (what the GEMMs / convolutions and the gradient all-reduce move);
+these optimizers own fp32 master copies and their moment buffers as flat buffers aligned with the
+parameters' flat layout (shared with DDP's buckets when the model is wrapped first), so an update is
+one streaming pass with no host synchronisation:
 
-    g = grad * grad_scale * min(1, max_norm / ||grad||)        (global-norm clipping, on device)
-    p32 = p32 * (1 - lr*wd[group]) - lr * m_hat / (sqrt(v_hat) + eps)
-    p16 = bf16(p32)
+* ``AdamWMaster``: g = grad * grad_scale * min(1, max_norm / ||grad||) (global-norm clipping computed
+  on device), decoupled weight decay, torch.optim.AdamW math; writes p32 and bf16(p32).
+* ``SGDMaster``:   torch.optim.SGD math (momentum, coupled weight decay, optional nesterov).
 
-is a single streaming pass over ~15 bytes/parameter with no host synchronisation.  Per-group weight
-decay is a per-64-element flag table (every parameter starts on a 64-element boundary).  State is
-exposed in torch.optim.AdamW's ``state_dict`` layout (exp_avg / exp_avg_sq / step per parameter)
-plus ``master`` (fp32 weights).
+Per-group weight decay is a per-64-element flag table (every parameter starts on a 64-element
+boundary of the flat layout).  State is exposed in torch.optim's ``state_dict`` layout
+(exp_avg / exp_avg_sq / momentum_buffer / step per parameter) plus ``master`` (fp32 weights).
 """
 from __future__ import annotations
 
@@ -21,27 +21,27 @@ from .._ext import kernels
 from ..parallel.flat import FlatLayout, shared_flat
 
 
-class AdamWMaster(torch.optim.Optimizer):
-    def __init__(self, params, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=None,
-                 grad_scale: float = 1.0):
-        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+class _MasterBase(torch.optim.Optimizer):
+    _state_keys: tuple = ()
+
+    def __init__(self, params, defaults, grad_scale: float):
         super().__init__(params, defaults)
-        self.max_grad_norm = max_grad_norm
         self.grad_scale = grad_scale
         self._flat = None
         self._step = 0
-        hp = {(g["lr"], tuple(g["betas"]), g["eps"]) for g in self.param_groups}
+        hp = {tuple((k, tuple(v) if isinstance(v, (list, tuple)) else v) for k, v in g.items()
+                    if k not in ("params", "weight_decay")) for g in self.param_groups}
         if len(hp) != 1:
-            raise ValueError("AdamWMaster: lr / betas / eps must be equal across groups (weight_decay may differ)")
+            raise ValueError(f"{type(self).__name__}: hyper-parameters other than weight_decay must be equal "
+                             "across groups")
 
-    # ------------------------------------------------------------------ flat state
     def _all_params(self):
         return [p for g in self.param_groups for p in g["params"]]
 
     def _build(self):
         params = self._all_params()
         if not all(p.is_cuda and p.dtype == torch.bfloat16 for p in params):
-            raise TypeError("AdamWMaster: bf16 GPU parameters expected")
+            raise TypeError(f"{type(self).__name__}: bf16 GPU parameters expected")
         tag = shared_flat(params)
         if tag is None:
             named = {f"p{i}": p for i, p in enumerate(params)}
@@ -53,13 +53,10 @@ class AdamWMaster(torch.optim.Optimizer):
         if n % 64:
             raise ValueError("flat buffer must be padded to 64 elements")
         dev = fp.device
-        master = fp.float()
-        m = torch.zeros(n, device=dev, dtype=torch.float32)
-        v = torch.zeros(n, device=dev, dtype=torch.float32)
         decay = torch.zeros(n // 64, dtype=torch.uint8)
         wd_values = {g["weight_decay"] for g in self.param_groups if g["weight_decay"] != 0.0}
         if len(wd_values) > 1:
-            raise ValueError("AdamWMaster: at most one non-zero weight_decay value")
+            raise ValueError("at most one non-zero weight_decay value across groups")
         self._wd = wd_values.pop() if wd_values else 0.0
         for g in self.param_groups:
             if g["weight_decay"] == 0.0:
@@ -67,14 +64,16 @@ class AdamWMaster(torch.optim.Optimizer):
             for p in g["params"]:
                 s = layout.slots[p._pde_flat[3]]
                 decay[s.offset // 64:(s.offset + s.numel + 63) // 64] = 1
-        self._flat = dict(layout=layout, p=fp, g=fg, master=master, m=m, v=v, decay=decay.to(dev),
+        bufs = {"master": fp.float()}
+        for k in self._state_keys:
+            bufs[k] = torch.zeros(n, device=dev, dtype=torch.float32)
+        self._flat = dict(layout=layout, p=fp, g=fg, bufs=bufs, decay=decay.to(dev),
                           sumsq=torch.zeros(1, device=dev, dtype=torch.float32))
         for p in params:
             st = self.state[p]
             name = p._pde_flat[3]
-            st["exp_avg"] = layout.view(m, name)
-            st["exp_avg_sq"] = layout.view(v, name)
-            st["master"] = layout.view(master, name)
+            for k, buf in bufs.items():
+                st[k] = layout.view(buf, name)
             st["step"] = torch.tensor(float(self._step))
 
     def _sync_grads(self):
@@ -88,14 +87,15 @@ class AdamWMaster(torch.optim.Optimizer):
                 v.copy_(p.grad)
                 p.grad = v
 
-    # ------------------------------------------------------------------ API
     def zero_grad(self, set_to_none: bool = False):
         if self._flat is not None:
             self._flat["g"].zero_()
         else:
             for p in self._all_params():
-                if p.grad is not None:
-                    p.grad = None
+                p.grad = None
+
+    def _kernel(self):  # pragma: no cover - abstract
+        raise NotImplementedError
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -106,25 +106,11 @@ class AdamWMaster(torch.optim.Optimizer):
         if self._flat is None:
             self._build()
         self._sync_grads()
-        f = self._flat
-        K = kernels()
-        clip = None
-        if self.max_grad_norm is not None:
-            f["sumsq"].zero_()
-            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"])
-            clip = f["sumsq"]
         self._step += 1
-        g0 = self.param_groups[0]
-        b1, b2 = g0["betas"]
-        K.adamw_master(f["master"], f["p"], f["g"], f["m"], f["v"], g0["lr"], b1, b2, g0["eps"], self._wd,
-                       self.grad_scale, self._step, f["decay"], clip, float(self.max_grad_norm or 1.0))
+        self._kernel()
         for p in self._all_params():
             self.state[p]["step"] = torch.tensor(float(self._step))
         return loss
-
-    def grad_norm(self) -> float:
-        """Global grad norm of the last clipped step (host sync; for logging only)."""
-        return float(self._flat["sumsq"].sqrt()) if self._flat is not None else 0.0
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -134,11 +120,52 @@ class AdamWMaster(torch.optim.Optimizer):
         for p in self._all_params():
             st = self.state[p]
             name = p._pde_flat[3]
-            for k, buf in (("exp_avg", f["m"]), ("exp_avg_sq", f["v"]), ("master", f["master"])):
+            for k, buf in f["bufs"].items():
                 view = f["layout"].view(buf, name)
                 if k in st and isinstance(st[k], torch.Tensor) and st[k].data_ptr() != view.data_ptr():
                     view.copy_(st[k].to(view.device, view.dtype))
+                elif k == "master" and (k not in st or st[k].data_ptr() != view.data_ptr()):
+                    view.copy_(p.detach().float())
                 st[k] = view
             self._step = int(float(st.get("step", 0)))
-        # the bf16 weights follow the master copy
-        kernels().f32_to_bf16(f["master"], f["p"])
+        kernels().f32_to_bf16(f["bufs"]["master"], f["p"])     # the bf16 weights follow the master copy
+
+
+class AdamWMaster(_MasterBase):
+    _state_keys = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=None,
+                 grad_scale: float = 1.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay), grad_scale)
+        self.max_grad_norm = max_grad_norm
+
+    def _kernel(self):
+        f, K = self._flat, kernels()
+        clip = None
+        if self.max_grad_norm is not None:
+            f["sumsq"].zero_()
+            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"])
+            clip = f["sumsq"]
+        g0 = self.param_groups[0]
+        b1, b2 = g0["betas"]
+        K.adamw_master(f["bufs"]["master"], f["p"], f["g"], f["bufs"]["exp_avg"], f["bufs"]["exp_avg_sq"], g0["lr"],
+                       b1, b2, g0["eps"], self._wd, self.grad_scale, self._step, f["decay"], clip,
+                       float(self.max_grad_norm or 1.0))
+
+    def grad_norm(self) -> float:
+        """Global grad norm of the last clipped step (host sync; for logging only)."""
+        return float(self._flat["sumsq"].sqrt()) if self._flat is not None else 0.0
+
+
+class SGDMaster(_MasterBase):
+    _state_keys = ("momentum_buffer",)
+
+    def __init__(self, params, lr=0.1, momentum=0.9, weight_decay=0.0, nesterov=False, grad_scale: float = 1.0):
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov),
+                         grad_scale)
+
+    def _kernel(self):
+        f = self._flat
+        g0 = self.param_groups[0]
+        kernels().sgd_master(f["bufs"]["master"], f["p"], f["g"], f["bufs"]["momentum_buffer"], g0["lr"],
+                             g0["momentum"], self._wd, g0["nesterov"], self.grad_scale, f["decay"])
