@@ -77,6 +77,33 @@ void bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& x, cons
             "bn_bwd");
 }
 
+void maxpool3s2_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& arg) {
+  nhwc_rows(x, "x");
+  nhwc_rows(y, "y");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(1) % 8 == 0, "maxpool: 4-D channels-last, C % 8 == 0");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.size(0) == N && y.size(1) == C && y.size(2) == (H - 1) / 2 + 1 && y.size(3) == (W - 1) / 2 + 1,
+              "maxpool: y must be [N, C, (H-1)/2+1, (W-1)/2+1]");
+  TORCH_CHECK(arg.is_cuda() && arg.scalar_type() == U8 && arg.numel() == y.numel() && arg.is_contiguous(),
+              "maxpool: arg must be a uint8 buffer of y.numel()");
+  hip_check(pde_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), (int)N, (int)C, (int)H, (int)W,
+                               (int)y.size(2), (int)y.size(3), cur_stream()),
+            "maxpool3s2_fwd");
+}
+
+void maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, const at::Tensor& dx) {
+  nhwc_rows(dy, "dy");
+  nhwc_rows(dx, "dx");
+  const int64_t N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1 &&
+                  C % 8 == 0,
+              "maxpool bwd: shape mismatch");
+  TORCH_CHECK(arg.is_cuda() && arg.scalar_type() == U8 && arg.numel() == dy.numel(), "maxpool bwd: arg");
+  hip_check(pde_maxpool3s2_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), (int)N, (int)C, (int)H, (int)W,
+                               (int)dy.size(2), (int)dy.size(3), cur_stream()),
+            "maxpool3s2_bwd");
+}
+
 void sgd_master(const at::Tensor& master, const at::Tensor& p16, const at::Tensor& g16, const at::Tensor& buf,
                 double lr, double momentum, double wd, bool nesterov, double grad_scale, const OptT& decay_blk) {
   const int64_t n = master.numel();
@@ -98,6 +125,8 @@ void register_resnet(pybind11::module& m) {
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("sgd_master", &sgd_master);
+  m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
 }
 
 }  // namespace pde

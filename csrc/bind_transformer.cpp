@@ -130,6 +130,18 @@ void f32_to_bf16(const at::Tensor& x, const at::Tensor& y) {
   hip_check(pde_f32_to_bf16(ptr<float>(x), y.data_ptr(), x.numel(), cur_stream()), "f32_to_bf16");
 }
 
+int64_t colsum_bf16_splits(int64_t C) { return pde_colsum_bf16_splits((int)C); }
+
+void colsum_bf16(const at::Tensor& x, const at::Tensor& part, const at::Tensor& out) {
+  check_cuda(x, "x", BF16);
+  const int64_t C = x.size(-1), N = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "colsum_bf16: C % 8");
+  check_cuda(part, "part", F32, (int64_t)pde_colsum_bf16_splits((int)C) * C);
+  check_cuda(out, "out", BF16, C);
+  hip_check(pde_colsum_bf16(x.data_ptr(), (int)N, (int)C, ptr<float>(part), out.data_ptr(), cur_stream()),
+            "colsum_bf16");
+}
+
 void sum_f32(const at::Tensor& x, const at::Tensor& out) {
   check_cuda(x, "x", F32);
   check_cuda(out, "out", F32, 1);
@@ -199,6 +211,8 @@ void register_transformer(pybind11::module& m) {
         py::arg("max_norm") = 1.0);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("sum_f32", &sum_f32);
+  m.def("colsum_bf16_splits", &colsum_bf16_splits);
+  m.def("colsum_bf16", &colsum_bf16);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }

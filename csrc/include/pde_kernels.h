@@ -86,6 +86,8 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
                             const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st);
 hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
 hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st);
+int pde_colsum_bf16_splits(int C);
+hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, hipStream_t st);
 
 // ---- attention (attention.hip) ----
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
@@ -103,6 +105,10 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
                       int relu, hipStream_t st);
+hipError_t pde_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int C, int H, int W, int OH, int OW,
+                              hipStream_t st);
+hipError_t pde_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int C, int H, int W, int OH, int OW,
+                              hipStream_t st);
 hipError_t pde_sgd_master(float* master, void* p16, const void* g16, float* buf, int64_t n, float lr, float momentum,
                           float wd, int nesterov, float grad_scale, const uint8_t* decay_blk, hipStream_t st);
 

@@ -65,47 +65,81 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint4* __restrict__ X, i
   }
 }
 
+// Sum the [nblk][2C] partials of the 64 channels [64*blockIdx.x, +64): 1024 threads = 64 channel
+// lanes x 16 waves striding over the partial rows (4 independent accumulators each), LDS fold.
+__device__ __forceinline__ void fold_partials(const float* __restrict__ part, int nblk, int C, int c, float& s,
+                                              float& q) {
+  __shared__ float sh[16][2][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cc = min(c, C - 1);
+  float s0 = 0.f, s1 = 0.f, q0 = 0.f, q1 = 0.f;
+  int b = w;
+  for (; b + 16 < nblk; b += 32) {
+    s0 += part[(size_t)b * 2 * C + cc];
+    q0 += part[(size_t)b * 2 * C + C + cc];
+    s1 += part[(size_t)(b + 16) * 2 * C + cc];
+    q1 += part[(size_t)(b + 16) * 2 * C + C + cc];
+  }
+  for (; b < nblk; b += 16) {
+    s0 += part[(size_t)b * 2 * C + cc];
+    q0 += part[(size_t)b * 2 * C + C + cc];
+  }
+  sh[w][0][lane] = s0 + s1;
+  sh[w][1][lane] = q0 + q1;
+  __syncthreads();
+  s = 0.f;
+  q = 0.f;
+  if (w == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      s += sh[k][0][lane];
+      q += sh[k][1][lane];
+    }
+  }
+}
+
 // per channel: mean / biased var -> rstd, running-stat update (unbiased var), scale / shift
-__global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int M,
-                                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
-                                                     float eps, float momentum, float* __restrict__ run_mean,
-                                                     float* __restrict__ run_var, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, float* __restrict__ scale,
-                                                     float* __restrict__ shift) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;  // fp64 accumulation of the (few hundred) block partials
-  for (int b = 0; b < nblk; ++b) {
-    s += part[(size_t)b * 2 * C + c];
-    q += part[(size_t)b * 2 * C + C + c];
-  }
-  const double mean = s / M;
-  const double var = fmax(q / M - mean * mean, 0.0);
-  const float rstd = rsqrtf((float)var + eps);
+__global__ __launch_bounds__(1024) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int M,
+                                                      const bf16_t* __restrict__ gamma,
+                                                      const bf16_t* __restrict__ beta, float eps, float momentum,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s, q;
+  fold_partials(part, nblk, C, c, s, q);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const float mean = s / M;
+  const float var = fmaxf(q / M - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
   if (run_mean) {
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * M / (double)max(M - 1, 1));
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * ((float)M / (float)max(M - 1, 1));
   }
-  mean_out[c] = (float)mean;
+  mean_out[c] = mean;
   rstd_out[c] = rstd;
   const float g = bf2f(gamma[c]), bt = bf2f(beta[c]);
   scale[c] = g * rstd;
-  shift[c] = bt - (float)mean * g * rstd;
+  shift[c] = bt - mean * g * rstd;
 }
 
-// y = x*scale + shift (+ res), optional relu
+// y = x*scale + shift (+ res), optional relu.  The grid stride is a multiple of C/8, so each
+// thread's channel chunk is fixed: its 8 scale / shift values are loaded once.
 __global__ __launch_bounds__(256) void k_bn_apply(const uint4* __restrict__ X, const uint4* __restrict__ R,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
                                                   uint4* __restrict__ Y, int64_t n8, int CP, int relu) {
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(i % CP) * 8;
+  const int64_t i0 = blockIdx.x * 256ll + threadIdx.x;
+  const int c0 = (int)(i0 & (CP - 1)) * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c0 + e];
+    sf[e] = shift[c0 + e];
+  }
+  for (int64_t i = i0; i < n8; i += (int64_t)gridDim.x * 256) {
     float v[8], r[8];
     unpack8(X[i], v);
     if (R) unpack8(R[i], r);
-    const float4 s0 = *reinterpret_cast<const float4*>(scale + c0), s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(shift + c0), h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float o = v[e] * sc[e] + sf[e] + (R ? r[e] : 0.f);
@@ -164,18 +198,16 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__
 
 // dgamma = sum dy'*xhat, dbeta = sum dy'; dx = A*dy' + B*x + Cc with A = g*rstd,
 // B = -A*rstd*mean(dy'xhat), Cc = -A*mean(dy') - B*mean
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float* __restrict__ part, int nblk, int C, int M,
-                                                         const bf16_t* __restrict__ gamma,
-                                                         const float* __restrict__ mean,
-                                                         const float* __restrict__ rstd, bf16_t* __restrict__ dgamma,
-                                                         bf16_t* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f, q = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    s += part[(size_t)b * 2 * C + c];
-    q += part[(size_t)b * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restrict__ part, int nblk, int C, int M,
+                                                          const bf16_t* __restrict__ gamma,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          bf16_t* __restrict__ dgamma, bf16_t* __restrict__ dbeta,
+                                                          float* __restrict__ coef) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s, q;
+  fold_partials(part, nblk, C, c, s, q);
+  if (threadIdx.x >= 64 || c >= C) return;
   dgamma[c] = f2bf(q);
   dbeta[c] = f2bf(s);
   const float A = bf2f(gamma[c]) * rstd[c];
@@ -190,8 +222,16 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint4* __restrict__ 
                                                       uint4* __restrict__ dX, uint4* __restrict__ dR, int64_t n8,
                                                       int C, int relu) {
   const int CP = C >> 3;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(i % CP) * 8;
+  const int64_t i0 = blockIdx.x * 256ll + threadIdx.x;
+  const int c0 = (int)(i0 & (CP - 1)) * 8;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ca[e] = coef[c0 + e];
+    cb[e] = coef[C + c0 + e];
+    cc[e] = coef[2 * C + c0 + e];
+  }
+  for (int64_t i = i0; i < n8; i += (int64_t)gridDim.x * 256) {
     float g[8], x[8], y[8], o[8];
     unpack8(dY[i], g);
     unpack8(X[i], x);
@@ -200,10 +240,92 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint4* __restrict__ 
     for (int e = 0; e < 8; ++e) {
       const float d = relu ? (y[e] > 0.f ? g[e] : 0.f) : g[e];
       g[e] = d;
-      o[e] = coef[c0 + e] * d + coef[C + c0 + e] * x[e] + coef[2 * C + c0 + e];
+      o[e] = ca[e] * d + cb[e] * x[e] + cc[e];
     }
     dX[i] = pack8(o);
     if (dR) dR[i] = pack8(g);
+  }
+}
+
+// ------------------------------------------------------------------------------- max-pool 3x3 / 2, pad 1
+// NHWC bf16.  Forward keeps the window argmax (0..8, first maximum in scan order like ATen) as one
+// byte per element; backward GATHERS: each input element sums the <= 2x2 windows that cover it and
+// chose it -- no atomics.
+__global__ __launch_bounds__(256) void k_maxpool3s2_fwd(const uint4* __restrict__ X, uint4* __restrict__ Y,
+                                                        uint2* __restrict__ A, int N, int H, int W, int OH, int OW,
+                                                        int CP) {
+  const int64_t total = (int64_t)N * OH * OW * CP;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(t % CP);
+    int64_t p = t / CP;
+    const int ow = (int)(p % OW);
+    p /= OW;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      arg[e] = 0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+        float v[8];
+        unpack8(X[(((int64_t)n * H + ihc) * W + iwc) * CP + c8], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool better = ok && v[e] > best[e];
+          best[e] = better ? v[e] : best[e];
+          arg[e] = better ? (uint32_t)(kh * 3 + kw) : arg[e];
+        }
+      }
+    }
+    Y[t] = pack8(best);
+    A[t] = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
+                      arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool3s2_bwd(const uint4* __restrict__ dY, const uint2* __restrict__ A,
+                                                        uint4* __restrict__ dX, int N, int H, int W, int OH, int OW,
+                                                        int CP) {
+  const int64_t total = (int64_t)N * H * W * CP;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(t % CP);
+    int64_t p = t / CP;
+    const int iw = (int)(p % W);
+    p /= W;
+    const int ih = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int oh0 = ih / 2, ow0 = iw / 2;  // candidates: oh in {oh0, oh0 + 1 if ih odd}, same for ow
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh0 + a, ow = ow0 + b;
+        const bool ok = (a == 0 || (ih & 1)) && (b == 0 || (iw & 1)) && oh < OH && ow < OW;
+        const int ohc = min(oh, OH - 1), owc = min(ow, OW - 1);
+        const int64_t o = (((int64_t)n * OH + ohc) * OW + owc) * CP + c8;
+        float g[8];
+        unpack8(dY[o], g);
+        const uint2 ar = A[o];
+        const uint32_t want = (uint32_t)((ih - (2 * ohc - 1)) * 3 + (iw - (2 * owc - 1)));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ae = ((e < 4 ? ar.x : ar.y) >> (8 * (e & 3))) & 0xffu;
+          acc[e] += (ok && ae == want) ? g[e] : 0.f;
+        }
+      }
+    }
+    dX[t] = pack8(acc);
   }
 }
 
@@ -262,7 +384,7 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
     const int rpb = (M + nblk - 1) / nblk;
     hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)x,
                        M, C, rpb, part);
-    hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, M,
+    hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                        (const bf16_t*)gamma, (const bf16_t*)beta, eps, momentum, run_mean, run_var, mean, rstd, scale,
                        shift);
   }
@@ -281,11 +403,29 @@ hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C
   const int rpb = (M + nblk - 1) / nblk;
   hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
                      (const uint4*)dy, (const uint4*)y, (const uint4*)x, mean, rstd, M, C, rpb, relu, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, M,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
   const int64_t n8 = (int64_t)M * CP;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dy, (const uint4*)y,
                      (const uint4*)x, coef, (uint4*)dx, (uint4*)dres, n8, C, relu);
+  return hipGetLastError();
+}
+
+hipError_t pde_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int C, int H, int W, int OH, int OW,
+                              hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(k_maxpool3s2_fwd, dim3(grid_cap(total, 8192)), dim3(256), 0, st, (const uint4*)x, (uint4*)y,
+                     (uint2*)arg, N, H, W, OH, OW, C / 8);
+  return hipGetLastError();
+}
+
+hipError_t pde_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int C, int H, int W, int OH, int OW,
+                              hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(k_maxpool3s2_bwd, dim3(grid_cap(total, 8192)), dim3(256), 0, st, (const uint4*)dy,
+                     (const uint2*)arg, (uint4*)dx, N, H, W, OH, OW, C / 8);
   return hipGetLastError();
 }
 

@@ -448,6 +448,62 @@ __global__ __launch_bounds__(256) void k_f32_to_bf16(const float4* __restrict__ 
   }
 }
 
+// Column sums of a [N, C] bf16 matrix (bias gradients): grid (ceil(C/256), RS); a block sums 256
+// columns (32 x 8-column chunks) over its N/RS rows with 8 row-lanes -> part[RS][C] fp32; then
+// k_colsum_finish folds the RS partial rows into bf16.
+__global__ __launch_bounds__(256) void k_colsum_bf16_part(const uint4* __restrict__ X, int N, int C,
+                                                          float* __restrict__ part) {
+  __shared__ float sh[8][256];
+  const int CP = C >> 3;
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c8 = min(blockIdx.x * 32 + cl, CP - 1);
+  const int rows = (N + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows, r1 = min(N, r0 + rows);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int r = r0 + rl;
+  for (; r + 24 < r1; r += 32) {
+    uint4 q[4] = {X[(size_t)r * CP + c8], X[(size_t)(r + 8) * CP + c8], X[(size_t)(r + 16) * CP + c8],
+                  X[(size_t)(r + 24) * CP + c8]};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float v[8];
+      unpack8(q[u], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+  for (; r < r1; r += 8) {
+    float v[8];
+    unpack8(X[(size_t)r * CP + c8], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sh[rl][cl * 8 + e] = acc[e];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += sh[k][threadIdx.x];
+    part[(size_t)blockIdx.y * C + col] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__ part, int RS, int C,
+                                                       bf16_t* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s0 = 0.f, s1 = 0.f;
+  int k = 0;
+  for (; k + 1 < RS; k += 2) {
+    s0 += part[(size_t)k * C + c];
+    s1 += part[(size_t)(k + 1) * C + c];
+  }
+  if (k < RS) s0 += part[(size_t)k * C + c];
+  out[c] = f2bf(s0 + s1);
+}
+
 // out[0] = sum(x[0..n)) (one 1024-thread block; n up to a few 1e5 -- loss rows)
 __global__ __launch_bounds__(1024) void k_sum_f32(const float* __restrict__ x, int n, float* __restrict__ out) {
   __shared__ float sh[16];
@@ -568,6 +624,20 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
   hipLaunchKernelGGL(k_adamw_master, dim3(grid_for(n4, 256, 2048)), dim3(256), 0, st, master, (uint2*)p16,
                      (const uint2*)g16, (float4*)m, (float4*)v, n4, lr, b1, b2, eps, wd, grad_scale, step, decay_blk,
                      clip_sumsq, max_norm);
+  return hipGetLastError();
+}
+
+int pde_colsum_bf16_splits(int C) {
+  const int cb = (C + 255) / 256;
+  const int rs = 512 / cb;
+  return rs < 1 ? 1 : (rs > 128 ? 128 : rs);
+}
+
+hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int rs = pde_colsum_bf16_splits(C);
+  hipLaunchKernelGGL(k_colsum_bf16_part, dim3((C + 255) / 256, rs), dim3(256), 0, st, (const uint4*)x, N, C, part);
+  hipLaunchKernelGGL(k_colsum_finish, dim3((C + 255) / 256), dim3(256), 0, st, part, rs, C, (bf16_t*)out);
   return hipGetLastError();
 }
 

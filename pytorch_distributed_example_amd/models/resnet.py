@@ -12,7 +12,7 @@ import torch
 import torch.nn as tnn
 import torch.nn.functional as F
 
-from ..ops.resnet import batch_norm_act
+from ..ops.resnet import batch_norm_act, max_pool3s2
 
 
 class BN(tnn.Module):
@@ -89,7 +89,7 @@ class ResNet(tnn.Module):
 
     def forward(self, x):
         x = self.bn1(self.conv1(x))
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = max_pool3s2(x)
         for i in range(1, 5):
             x = getattr(self, f"layer{i}")(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -75,3 +75,32 @@ def batch_norm_act(x, gamma, beta, running_mean, running_var, training: bool, mo
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
+
+
+class MaxPool3s2Fn(torch.autograd.Function):
+    """3x3 / stride 2 / pad 1 max-pool over channels-last bf16 (ResNet stem)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, C, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+        arg = torch.empty(y.numel(), device=x.device, dtype=torch.uint8)
+        kernels().maxpool3s2_fwd(x, y, arg)
+        ctx.save_for_backward(arg)
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.xshape
+        dx = torch.empty(N, C, H, W, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        kernels().maxpool3s2_bwd(dy.contiguous(memory_format=torch.channels_last), arg, dx)
+        return dx
+
+
+def max_pool3s2(x):
+    if x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0:
+        return MaxPool3s2Fn.apply(x.contiguous(memory_format=torch.channels_last))
+    return F.max_pool2d(x, 3, 2, 1)

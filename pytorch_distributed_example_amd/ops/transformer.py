@@ -218,6 +218,62 @@ def lm_head_loss(h, w, targets, V: int):
     return F.cross_entropy(logits.reshape(-1, V), targets.reshape(-1))
 
 
+def _splitk(N: int, out: int, fin: int) -> int:
+    """Split-K factor of the weight-gradient GEMM dW[out, in] = dY^T X (K = tokens).
+
+    With K = 16k tokens and out*in <= a few M the library GEMM has fewer output tiles than the chip
+    has CUs; splitting K into S batched GEMMs (+ one small reduction) fills all 256 CUs.  Factors
+    measured on MI355X for GPT-2 small (tools/gemm_bench.py -> profiles/gemm_bench_gpt2.jsonl):
+    768x2304 / 768x768 best at 8, 768x3072 / 3072x768 at 4, the LM head (38.6M outputs) at 1."""
+    if out * fin >= 16 << 20:
+        return 1
+    S = 8 if out * fin <= 2 << 20 else 4
+    while S > 1 and (N % S or N // S < 512):
+        S //= 2
+    return S
+
+
+def _wgrad(dy2, x2):
+    N, out = dy2.shape
+    fin = x2.shape[1]
+    S = _splitk(N, out, fin)
+    if S == 1:
+        return torch.matmul(dy2.t(), x2)
+    part = torch.bmm(dy2.view(S, N // S, out).transpose(1, 2), x2.view(S, N // S, fin))
+    return part.sum(0)
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b on bf16: forward = library GEMM with the bias in its epilogue; backward =
+    dgrad GEMM, split-K wgrad GEMM, and the framework's column-sum kernel for the bias gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        out, fin = w.shape
+        dy2 = _c(dy.reshape(-1, out))
+        x2 = _c(x.reshape(-1, fin))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dy2, w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dy2, x2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            K = kernels()
+            part = torch.empty(K.colsum_bf16_splits(out) * out, device=dy.device, dtype=torch.float32)
+            db = torch.empty(out, device=dy.device, dtype=dy.dtype)
+            K.colsum_bf16(dy2, part, db)
+        return dx, dw, db
+
+
 def linear(x, w, b=None):
-    """Projection GEMM (hipBLASLt on GPU, bias fused in the epilogue)."""
+    """Projection GEMM (library GEMM on GPU; split-K weight gradients, HIP bias-gradient kernel)."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and w.shape[0] % 8 == 0:
+        return LinearFn.apply(x, w, b)
     return F.linear(x, w, b)

@@ -195,3 +195,21 @@ def test_gpt2_trains():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.parametrize("N,fin,fout", [(16384, 768, 2304), (4096, 3072, 768), (300, 64, 1000), (64, 40, 24)])
+def test_linear_splitk_and_bias_grad(N, fin, fout):
+    torch.manual_seed(10)
+    x = torch.randn(N, fin).to(dev, torch.bfloat16).requires_grad_()
+    w = (torch.randn(fout, fin) / fin ** 0.5).to(dev, torch.bfloat16).requires_grad_()
+    b = torch.randn(fout).to(dev, torch.bfloat16).requires_grad_()
+    y = T.linear(x, w, b)
+    g = torch.randn(N, fout).to(dev, torch.bfloat16)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.linear(xr, wr, br)
+    yr.backward(g.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    assert rel_err(b.grad, br.grad) < 2e-2
