@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import dist, ops
+from ..utils import profiling as prof
 
 
 class Average(object):
@@ -110,14 +111,18 @@ class Trainer(object):
             data = data.to(self.device)
             label = label.to(self.device)
 
-            output = self.net(data)
-            loss = _loss_fn(output, label)
+            with prof.range("forward"):
+                output = self.net(data)
+                loss = _loss_fn(output, label)
 
             self.optimizer.zero_grad()
-            loss.backward()
+            with prof.range("backward"):
+                loss.backward()
             if self.distributed and self.manual_average:
-                self.average_gradients()
-            self.optimizer.step()
+                with prof.range("average_gradients"):
+                    self.average_gradients()
+            with prof.range("optimizer"):
+                self.optimizer.step()
 
             train_loss.update(loss, data.size(0))
             train_acc.update(output, label)

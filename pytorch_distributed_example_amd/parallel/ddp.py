@@ -30,6 +30,7 @@ import torch
 from torch import nn
 
 from .. import dist
+from ..utils import profiling as prof
 from .flat import FlatLayout, reverse_order_buckets
 
 
@@ -124,7 +125,8 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, bk: _Bucket):
         view = self.flat_grads[bk.start:bk.end]
-        bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+        with prof.range(f"ddp.bucket{bk.index}.all_reduce"):
+            bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
 
     def _finalize(self):
         for bk in self.buckets:

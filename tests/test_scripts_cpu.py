@@ -94,3 +94,15 @@ def test_read_stats(tmp_path):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/read_stats.py"), prof, "10"],
                          capture_output=True, text=True, timeout=60)
     assert out.returncode == 0 and "tottime" in out.stdout
+
+
+def test_toy_via_torchrun():
+    """The driver's multi-GPU launcher path: torch.distributed.run owns MASTER_PORT (agent store)."""
+    port = free_port()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "scripts/toy.py"), "--steps", "2", "--sleep", "0"], cwd=ROOT,
+                         capture_output=True, text=True, env=ENV, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.replace("rank:", "\nrank:").splitlines() if l.startswith("rank:")]
+    _check_toy(lines, 3, 2)
