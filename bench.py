@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch-size", type=int, default=128, help="per-GPU batch (reference default 128)")
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph (graph mode)")
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--seed", type=int, default=0)
@@ -79,16 +80,21 @@ def main():
     nfull = idx.numel() // args.batch_size
     eng.set_epoch_indices(idx[: nfull * args.batch_size])   # full batches only: every timed step is B=128
 
+    S = max(1, args.graph_steps)
+
     def run(n):
         if args.mode == "graph":
-            for _ in range(n):
-                eng.replay()
+            for _ in range(n // S):
+                eng.replay(steps=S)             # S steps per replay
+            for _ in range(n % S):
+                eng.replay(steps=1)
         else:
             for _ in range(n):
                 eng.step()
 
     if args.mode == "graph":
-        eng.capture()
+        eng.capture(steps=S)
+        eng.capture(steps=1)
     run(args.warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only
@@ -130,7 +136,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "optimizer": "Adam(lr=1e-3)",
-                "mode": args.mode,
+                "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
                 "grad_allreduce": "none" if world == 1 else ("bucketed-overlap" if not args.no_overlap else "flat"),
             },
             "stock_torch_same_hw_w1_images_per_s": STOCK_TORCH_W1,

@@ -22,7 +22,7 @@ hipError_t pde_lenet_head_bwd(const float* H1, int B, const float* W2, const flo
                               float* dZ1, hipStream_t st);
 hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, const float* dZ2, const float* W1,
                             int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, const float* row_loss,
-                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg,
+                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg, int part,
                             hipStream_t st);
 hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, const uint8_t* A1,
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,

@@ -441,14 +441,15 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
                                                 float* __restrict__ gW2, float* __restrict__ gb2,
                                                 const float* __restrict__ row_loss, const int* __restrict__ row_hit,
                                                 double* __restrict__ loss_sum, unsigned long long* __restrict__ correct,
-                                                int dbg) {
+                                                int dbg, int part) {
   // dbg (ablation only): 1 skip role C, 2 skip role A, 4 skip role B
+  // part: 0 = all roles in one launch, 1 = role C only (critical path), 2 = roles A+B only (side stream)
   __shared__ float red[4][16][17];
   __shared__ float scratch[4];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, kg = l >> 4;
   const int mtiles = (B + 15) / 16;
   const int nC = mtiles * 50, nA = 32 * 13;
-  int bid = blockIdx.x;
+  int bid = blockIdx.x + (part == 2 ? nC : 0);
   if (bid < nC) {
     if (dbg & 1) return;
     // ---- role C: dP2 tile (mt, nt) over K = 500 (hidden); wave w takes K-chunks w, w+4, ... ----
@@ -862,11 +863,12 @@ hipError_t pde_lenet_head_bwd(const float* H1, int B, const float* W2, const flo
 
 hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, const float* dZ2, const float* W1,
                             int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, const float* row_loss,
-                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg,
+                            const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg, int part,
                             hipStream_t st) {
-  const int nblk = ((B + 15) / 16) * 50 + 32 * 13 + 8;
+  const int nC = ((B + 15) / 16) * 50, nAB = 32 * 13 + 8;
+  const int nblk = part == 1 ? nC : (part == 2 ? nAB : nC + nAB);
   hipLaunchKernelGGL(k_fc_bwd, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2,
-                     row_loss, row_hit, loss_sum, correct, dbg);
+                     row_loss, row_hit, loss_sum, correct, dbg, part);
   return hipGetLastError();
 }
 

@@ -125,7 +125,8 @@ void lenet_head_bwd(const at::Tensor& H1, int64_t B, const at::Tensor& W2, const
 void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& dZ1, const at::Tensor& dZ2,
                   const at::Tensor& W1, int64_t B, const at::Tensor& dP2m, const at::Tensor& gW1, const at::Tensor& gb1,
                   const at::Tensor& gW2, const at::Tensor& gb2, const OptT& row_loss, const OptT& row_hit,
-                  const OptT& loss_sum, const OptT& correct, int64_t dbg) {
+                  const OptT& loss_sum, const OptT& correct, int64_t dbg, int64_t part) {
+  TORCH_CHECK(part >= 0 && part <= 2, "lenet_fc_bwd: part must be 0 (all), 1 (dP2) or 2 (weight grads)");
   check_cuda(P2, "P2", F32, B * 800);
   check_cuda(H1, "H1", F32, B * 500);
   check_cuda(dZ1, "dZ1", F32, B * 500);
@@ -140,7 +141,8 @@ void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& 
                              ptr<float>(dP2m), ptr<float>(gW1), ptr<float>(gb1), ptr<float>(gW2), ptr<float>(gb2),
                              optr<float>(row_loss, "row_loss", F32, B), optr<int>(row_hit, "row_hit", I32, B),
                              optr<double>(loss_sum, "loss_sum", F64, 1),
-                             optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, cur_stream()),
+                             optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, (int)part,
+                             cur_stream()),
             "lenet_fc_bwd");
 }
 
@@ -380,7 +382,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_head_bwd", &lenet_head_bwd);
   m.def("lenet_fc_bwd", &lenet_fc_bwd, py::arg("P2"), py::arg("H1"), py::arg("dZ1"), py::arg("dZ2"), py::arg("W1"),
         py::arg("B"), py::arg("dP2m"), py::arg("gW1"), py::arg("gb1"), py::arg("gW2"), py::arg("gb2"),
-        py::arg("row_loss"), py::arg("row_hit"), py::arg("loss_sum"), py::arg("correct"), py::arg("dbg") = 0);
+        py::arg("row_loss"), py::arg("row_hit"), py::arg("loss_sum"), py::arg("correct"), py::arg("dbg") = 0,
+        py::arg("part") = 0);
   m.def("lenet_conv_bwd", &lenet_conv_bwd, py::arg("X"), py::arg("rows"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("gW2c"), py::arg("gb2c"),
         py::arg("c1_nrep") = 1, py::arg("c1_rep_stride") = 0, py::arg("dbg") = 0);

@@ -93,7 +93,9 @@ class LeNetTrainStep:
         self.eval_loss = torch.zeros(1, device=dev, dtype=torch.float64)
         self.eval_correct = torch.zeros(1, device=dev, dtype=torch.int64)
         self.comm_stream = torch.cuda.Stream(device=dev) if self.comm_on else None
-        self._ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self._ev = {k: torch.cuda.Event() for k in ("fc", "conv", "fc_done")}
+        self.bucket_ranges = [tuple(r) for r in self.layout.bucket_ranges]
+        assert self.bucket_ranges[0][0] == 0 and self.bucket_ranges[1][0] >= self.bucket_ranges[0][1]
         self.X = self.Y = self.idx = None
         self.nbatches = 0
         self.graphs = {}
@@ -120,7 +122,32 @@ class LeNetTrainStep:
         self.counters[1].zero_()
 
     # ------------------------------------------------------------------ the step
+    def _opt(self, lo: int, hi: int, conv: bool):
+        """Fused optimizer update of the flat range [lo, hi) (one bucket or everything).  The conv
+        range carries the conv2 weight repack (Wt2) and the conv1 gradient-replica fold."""
+        K, sl = self.K, slice(lo, hi)
+        pack_off = self.pack_off - lo if conv else -1
+        fold_off = self.c1_off - lo if conv else -1
+        pack = self.Wt2 if conv else None
+        scale = 1.0 / self.world
+        if self.optimizer == "adam":
+            K.adam_flat(self.params[sl], self.grads[sl], self.m[sl], self.v[sl], self.lr, self.betas[0],
+                        self.betas[1], self.eps, self.wd, False, scale, self.counters, self.arrive, -1, pack_off,
+                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE)
+        else:
+            K.sgd_flat(self.params[sl], self.grads[sl], self.m[sl], self.lr, self.momentum, 0.0, self.wd, False,
+                       scale, self.counters, self.arrive, -1, pack_off, pack, fold_off, C1_STRIDE, C1_NREP,
+                       C1_STRIDE)
+
     def _launch(self, B: int):
+        """One step on the current stream: conv_fwd -> fc1 -> head -> fc_bwd -> conv_bwd -> opt.
+
+        With a comm group and ``overlap``, bucket 0 (fc grads, complete after fc_bwd) is all-reduced
+        on the comm stream while conv_bwd runs; bucket 1 after conv_bwd; the optimizer waits for both.
+
+        (Measured and rejected: moving the fc weight-gradient roles and the fc-bucket optimizer to a
+        side stream beside conv_bwd -- conv_bwd already fills the GPU, so it slowed from 24 to 31 us,
+        and the two cross-stream joins cost 5-7 us each: 91 us/step vs 81 us single-stream.)"""
         K, p, g = self.K, self.p, self.g
         K.lenet_conv_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
                          p["conv1.weight"], p["conv1.bias"], self.Wt2, p["conv2.bias"], self.P1, self.A1, self.P2,
@@ -128,35 +155,40 @@ class LeNetTrainStep:
         K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1, self.counters)   # bumps counters
         K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], self.cur_lbl, 1.0 / B, None, self.dZ2, self.dZ1,
                      self.row_loss, self.row_hit, None, None)
-        K.lenet_fc_bwd(self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
-                       g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], self.row_loss, self.row_hit, self.loss_sum,
-                       self.correct)
+        fc_args = (self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
+                   g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], self.row_loss, self.row_hit, self.loss_sum,
+                   self.correct)
+        conv_args = (self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
+                     self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE)
         cur = torch.cuda.current_stream(self.device)
+        ev, cs = self._ev, self.comm_stream
+        K.lenet_fc_bwd(*fc_args)
         if self.comm_on and self.overlap:
-            self._ev[0].record(cur)
-            self.comm_stream.wait_event(self._ev[0])
-            with torch.cuda.stream(self.comm_stream):
+            ev["fc"].record(cur)
+            cs.wait_event(ev["fc"])
+            with torch.cuda.stream(cs):
                 self.comm.all_reduce_(self.bucket_grads[0])
-        K.lenet_conv_bwd(self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
-                         self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE)
-        if self.comm_on:
-            self._ev[1].record(cur)
-            self.comm_stream.wait_event(self._ev[1])
-            with torch.cuda.stream(self.comm_stream):
-                if not self.overlap:
-                    self.comm.all_reduce_(self.grads)
-                else:
-                    self.comm.all_reduce_(self.bucket_grads[1])
-            cur.wait_stream(self.comm_stream)
-        scale = 1.0 / self.world
-        if self.optimizer == "adam":
-            K.adam_flat(self.params, self.grads, self.m, self.v, self.lr, self.betas[0], self.betas[1], self.eps,
-                        self.wd, False, scale, self.counters, self.arrive, -1, self.pack_off, self.Wt2,
-                        self.c1_off, C1_STRIDE, C1_NREP, C1_STRIDE)
-        else:
-            K.sgd_flat(self.params, self.grads, self.m, self.lr, self.momentum, 0.0, self.wd, False, scale,
-                       self.counters, self.arrive, -1, self.pack_off, self.Wt2,
-                       self.c1_off, C1_STRIDE, C1_NREP, C1_STRIDE)
+        K.lenet_conv_bwd(*conv_args)
+        if not self.comm_on:
+            self._opt(0, self.params.numel(), True)
+            return
+        ev["conv"].record(cur)
+        cs.wait_event(ev["conv"])
+        if not self.overlap:
+            with torch.cuda.stream(cs):
+                self.comm.all_reduce_(self.grads)
+            cur.wait_stream(cs)
+            self._opt(0, self.params.numel(), True)
+            return
+        # the fc-bucket update (94 % of the parameters) runs while the conv bucket is being reduced
+        ev["fc_done"].record(cs)
+        with torch.cuda.stream(cs):
+            self.comm.all_reduce_(self.bucket_grads[1])
+        (a0, a1), (b0, b1) = self.bucket_ranges
+        cur.wait_event(ev["fc_done"])
+        self._opt(a0, a1, False)
+        cur.wait_stream(cs)
+        self._opt(b0, b1, True)
 
     def _batch_size_at(self, b: int) -> int:
         return self.B if b < self.nfull else self.tail
@@ -165,8 +197,10 @@ class LeNetTrainStep:
         """Run one training step eagerly (B defaults to the full batch size)."""
         self._launch(B or self.B)
 
-    def capture(self, B: Optional[int] = None, warmup: int = 0):
-        """Capture one step of batch size B into a hipGraph (replayed by ``replay``)."""
+    def capture(self, B: Optional[int] = None, warmup: int = 0, steps: int = 1):
+        """Capture ``steps`` consecutive steps of batch size B into one hipGraph (replayed by
+        ``replay``).  Every step reads its batch position / optimizer step from device counters, so
+        a multi-step graph is just the step chain repeated; it amortises the per-replay launch cost."""
         B = B or self.B
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -176,16 +210,18 @@ class LeNetTrainStep:
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._launch(B)
-        self.graphs[B] = g
+            for _ in range(steps):
+                self._launch(B)
+        self.graphs[(B, steps)] = g
         return g
 
-    def replay(self, B: Optional[int] = None):
+    def replay(self, B: Optional[int] = None, steps: int = 1):
+        """Run ``steps`` steps through the (captured on first use) graph of that many steps."""
         B = B or self.B
-        g = self.graphs.get(B)
+        g = self.graphs.get((B, steps))
         if g is None:
-            g = self.capture(B)
-            # capturing does not execute: run the captured step now so call semantics stay "one step"
+            g = self.capture(B, steps=steps)
+            # capturing does not execute: replay now so call semantics stay "steps steps"
         g.replay()
 
     # ------------------------------------------------------------------ epochs / meters
