@@ -448,12 +448,24 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
   __shared__ float scratch[4];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, kg = l >> 4;
   const int mtiles = (B + 15) / 16;
-  const int nC = mtiles * 50, nA = 32 * 13;
-  int bid = blockIdx.x + (part == 2 ? nC : 0);
-  if (bid < nC) {
+  const int nC = mtiles * 50, nA = 32 * 51;
+  // grid order [B | C | A] (part 1: [C], part 2: [B | A]): role B's blocks carry the longest serial
+  // chain (K = batch MFMA), so they are dispatched first instead of after the 800+ C/A blocks.
+  constexpr int nB = 32;
+  const int h = blockIdx.x;
+  int role, bid;
+  if (part == 1) { role = 1; bid = h; }
+  else if (h < nB) { role = 0; bid = h; }
+  else if (part == 2) { role = 2; bid = h - nB; }
+  else if (h < nB + nC) { role = 1; bid = h - nB; }
+  else { role = 2; bid = h - nB - nC; }
+  if (role == 1) {
     if (dbg & 1) return;
     // ---- role C: dP2 tile (mt, nt) over K = 500 (hidden); wave w takes K-chunks w, w+4, ... ----
-    const int mt = bid / 50, nt = bid % 50;
+    // XCD-aware order: the mtiles blocks reading one W1 column slab (16 x 500) get consecutive
+    // logical ids, i.e. the same XCD and its L2 (nC and the role offsets are multiples of 8).
+    const int L = (nC % 8 == 0) ? xcd_remap(bid, nC) : bid;
+    const int nt = L / mtiles, mt = L % mtiles;
     const int row = mt * 16 + (l & 15), n = nt * 16 + (l & 15);
     const float am = row < B ? 1.f : 0.f;
     const float* arow = dZ1 + (size_t)min(row, B - 1) * kHid;
@@ -486,84 +498,81 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
     }
     return;
   }
-  bid -= nC;
-  if (bid < nA) {
+  if (role == 2) {
     if (dbg & 2) return;
     // ---- role A: [dW1|db1] tile (mt over 500, nt over 800 + bias tile 50), K = batch ----
-    const int mt = bid / 13, nt = (bid % 13) * 4 + w;
-    if (nt > 50) return;
+    // XCD-aware order: the 32 blocks sharing one P2 column group (B x 64) are consecutive logical
+    // ids on one XCD (hardware deals block h to XCD h % 8; nC and nA are multiples of 8).
+    // One 16 x 16 tile per block; the 4 waves split K = batch into 32-row slices (8 loads of each
+    // operand per lane; a wave streaming all 128 rows made this role a long serial chain), LDS fold.
+    const int L = (nC % 8 == 0) ? xcd_remap(bid, nA) : bid;
+    const int mt = L % 32, nt = L / 32;                // nt 0..50 (50 = bias tile: ones column)
     const int m = mt * 16 + (l & 15), n = nt * 16 + (l & 15);
     const int mc = min(m, kHid - 1), nc = min(n, kFeat - 1);
     const float mm = m < kHid ? 1.f : 0.f;
-    const bool bias_tile = nt == 50;                  // wave-uniform
+    const bool bias_tile = nt == 50;                  // block-uniform
     const float ones = (n == kFeat) ? 1.f : 0.f;
     f32x4 acc0 = {0.f}, acc1 = {0.f};
-    for (int b0 = 0; b0 < B; b0 += kBChunk) {
-      float av[kBChunk / 4], bvv[kBChunk / 4];
+    for (int b0 = 32 * w; b0 < B; b0 += 128) {
+      float av[8], bvv[8];
 #pragma unroll
-      for (int i = 0; i < kBChunk / 4; ++i) {
+      for (int i = 0; i < 8; ++i) {
         const int r = b0 + 4 * i + kg, rc = min(r, B - 1);
         av[i] = dZ1[(size_t)rc * kHid + mc] * (r < B ? mm : 0.f);
-      }
-      if (!bias_tile) {
-#pragma unroll
-        for (int i = 0; i < kBChunk / 4; ++i) {
-          const int rc = min(b0 + 4 * i + kg, B - 1);
-          bvv[i] = P2[(size_t)rc * kFeat + nc];
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < kBChunk / 4; ++i) bvv[i] = ones;
+        bvv[i] = bias_tile ? ones : P2[(size_t)rc * kFeat + nc];
       }
 #pragma unroll
-      for (int i = 0; i < kBChunk / 4; i += 2) {
+      for (int i = 0; i < 8; i += 2) {
         acc0 = mfma16x16x4(av[i], bvv[i], acc0);
         acc1 = mfma16x16x4(av[i + 1], bvv[i + 1], acc1);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gm = mt * 16 + (l >> 4) * 4 + r;
-      const float v = acc0[r] + acc1[r];
+    for (int r = 0; r < 4; ++r) red[w][(l >> 4) * 4 + r][l & 15] = acc0[r] + acc1[r];
+    __syncthreads();
+    {
+      const int i = t >> 4, j = t & 15, gm = mt * 16 + i, gn = nt * 16 + j;
+      const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j];
       if (gm < kHid) {
-        if (!bias_tile) gW1[(size_t)gm * kFeat + n] = v;
-        else if (n == kFeat) gb1[gm] = v;
+        if (!bias_tile) gW1[(size_t)gm * kFeat + gn] = v;
+        else if (gn == kFeat) gb1[gm] = v;
       }
     }
     return;
   }
-  bid -= nA;
   if (dbg & 4) return;
-  // ---- role B: [dW2|db2] tile nt (columns 16nt..16nt+15 over 500 + ones column 500), K = batch ----
+  // ---- role B: [dW2|db2] column tile nt = bid (columns 16nt..16nt+15 over 500 + ones column 500).
+  // One block per tile, the 4 waves split K = batch into 32-row slices (8 loads of each operand
+  // per lane instead of 64: in-step, one wave streaming the whole batch took ~12 us), LDS fold.
   {
-    const int nt = bid * 4 + w;                        // 0..31
+    const int nt = bid;                                // 0..31
     const int n = nt * 16 + (l & 15), nc = min(n, kHid - 1);
     const int c = l & 15, cc = min(c, kCls - 1);
     const float cm = c < kCls ? 1.f : 0.f;
     const float hm = n < kHid ? 1.f : 0.f, ones = n == kHid ? 1.f : 0.f;
     f32x4 acc0 = {0.f}, acc1 = {0.f};
-    for (int b0 = 0; b0 < B; b0 += kBChunk) {
-      float av[kBChunk / 4], bvv[kBChunk / 4];
+    for (int b0 = 32 * w; b0 < B; b0 += 128) {
+      float av[8], bvv[8];
 #pragma unroll
-      for (int i = 0; i < kBChunk / 4; ++i) {
+      for (int i = 0; i < 8; ++i) {
         const int r = b0 + 4 * i + kg, rc = min(r, B - 1);
         av[i] = dZ2[(size_t)rc * kCls + cc] * (r < B ? cm : 0.f);
         bvv[i] = H1[(size_t)rc * kHid + nc] * hm + ones;
       }
 #pragma unroll
-      for (int i = 0; i < kBChunk / 4; i += 2) {
+      for (int i = 0; i < 8; i += 2) {
         acc0 = mfma16x16x4(av[i], bvv[i], acc0);
         acc1 = mfma16x16x4(av[i + 1], bvv[i + 1], acc1);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ci = (l >> 4) * 4 + r;
-      const float v = acc0[r] + acc1[r];
-      if (ci < kCls) {
-        if (n < kHid) gW2[ci * kHid + n] = v;
-        else if (n == kHid) gb2[ci] = v;
-      }
+    for (int r = 0; r < 4; ++r) red[w][(l >> 4) * 4 + r][l & 15] = acc0[r] + acc1[r];
+    __syncthreads();
+    if (t < 160) {                                     // 10 classes x 16 columns
+      const int ci = t >> 4, j = t & 15, gn = nt * 16 + j;
+      const float v = red[0][ci][j] + red[1][ci][j] + red[2][ci][j] + red[3][ci][j];
+      if (gn < kHid) gW2[ci * kHid + gn] = v;
+      else if (gn == kHid) gb2[ci] = v;
     }
   }
   if (bid == 0 && row_loss && loss_sum) {
@@ -608,7 +617,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
                                                   const float* __restrict__ W2c, int B,
                                                   float* __restrict__ gW1c, float* __restrict__ gb1c,
                                                   float* __restrict__ gW2c, float* __restrict__ gb2c,
-                                                  int c1_nrep, int c1_rep_stride, int dbg) {
+                                                  int c1_nrep, int c1_rep_stride, const float* __restrict__ row_loss,
+                                                  const int* __restrict__ row_hit, double* __restrict__ loss_sum,
+                                                  unsigned long long* __restrict__ correct, int dbg) {
   // conv1 grads go to replica (b % c1_nrep) at a stride of c1_rep_stride floats (the consumer folds
   // the replicas): 128 images adding into 520 addresses was the single largest cost (17 us).
   // dbg (ablation only; 0 in production): 1 skip role W, 2 skip role D, 4 no global atomics,
@@ -620,6 +631,36 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
   const float4* Gv = reinterpret_cast<const float4*>(dP2m);
   const uint4* Av = reinterpret_cast<const uint4*>(A2);
   int bid = blockIdx.x;
+  if (loss_sum != nullptr) {
+    // block 0: fold the head's per-row loss / hit into the device meters.  It rides along this
+    // ~20 us kernel (dispatched first) instead of ending fc_bwd's critical chain with two more
+    // dependent global round trips (measured: +7 us in-step there).
+    if (bid == 0) {
+      float ls = 0.f, hs = 0.f;
+      for (int r = t; r < B; r += 512) {
+        ls += row_loss[r];
+        hs += (float)row_hit[r];
+      }
+      ls = wave_sum(ls);
+      hs = wave_sum(hs);
+      if (l == 0) {
+        smem[w] = ls;
+        smem[8 + w] = hs;
+      }
+      __syncthreads();
+      if (t == 0) {
+        float tl = 0.f, th = 0.f;
+        for (int k = 0; k < 8; ++k) {
+          tl += smem[k];
+          th += smem[8 + k];
+        }
+        loss_sum[0] += (double)tl;
+        correct[0] += (unsigned long long)(th + 0.5f);
+      }
+      return;
+    }
+    bid -= 1;
+  }
   if (bid < nW) {
     if (dbg & 1) return;
     const int ig = bid >> 4, kp = bid & 15;
@@ -865,7 +906,7 @@ hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, 
                             int B, float* dP2m, float* gW1, float* gb1, float* gW2, float* gb2, const float* row_loss,
                             const int* row_hit, double* loss_sum, unsigned long long* correct, int dbg, int part,
                             hipStream_t st) {
-  const int nC = ((B + 15) / 16) * 50, nAB = 32 * 13 + 8;
+  const int nC = ((B + 15) / 16) * 50, nAB = 32 * 51 + 32;
   const int nblk = part == 1 ? nC : (part == 2 ? nAB : nC + nAB);
   hipLaunchKernelGGL(k_fc_bwd, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2,
                      row_loss, row_hit, loss_sum, correct, dbg, part);
@@ -874,11 +915,14 @@ hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, 
 
 hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, const uint8_t* A1,
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,
-                              float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride, int dbg,
-                              hipStream_t st) {
-  const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B;
+                              float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride,
+                              const float* row_loss, const int* row_hit, double* loss_sum,
+                              unsigned long long* correct, int dbg, hipStream_t st) {
+  const int meters = (loss_sum && correct && row_loss && row_hit) ? 1 : 0;
+  const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B + meters;
   hipLaunchKernelGGL(k_conv_bwd, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
-                     gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, dbg);
+                     gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, meters ? row_loss : nullptr,
+                     meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg);
   return hipGetLastError();
 }
 

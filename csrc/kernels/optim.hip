@@ -30,16 +30,25 @@ struct Fold {
 
 // Returns false for float4 groups that are replica storage (r >= 1): they are not parameters.
 // For canonical groups, sums the replicas into g4 (written back so p.grad holds the true gradient).
+constexpr int kMaxFold = 16;
+
 __device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long i, float4& gg) {
   if (fd.off < 0 || fd.nrep <= 1) return true;
-  const long long e = 4 * i - fd.off;
-  if (e < 0 || e >= (long long)fd.stride * fd.nrep) return true;
-  const long long r = e / fd.stride, o = e - r * fd.stride;
+  const long long e64 = 4 * i - fd.off;
+  if (e64 < 0 || e64 >= (long long)fd.stride * fd.nrep) return true;
+  const int e = (int)e64;                        // in range: 32-bit math (64-bit division is a call)
+  const int r = e / fd.stride, o = e - r * fd.stride;
   if (r > 0) return false;
   if (o < fd.len) {
-    for (int k = 1; k < fd.nrep; ++k) {
-      const float4 x = g4[i + (long long)k * (fd.stride / 4)];
-      gg.x += x.x; gg.y += x.y; gg.z += x.z; gg.w += x.w;
+    // all replica loads in flight at once (a dependent-looking loop here cost ~1 us per replica)
+    const int s4 = fd.stride / 4, last = fd.nrep - 1;
+    float4 x[kMaxFold - 1];
+#pragma unroll
+    for (int k = 1; k < kMaxFold; ++k) x[k - 1] = g4[i + (long long)min(k, last) * s4];
+#pragma unroll
+    for (int k = 1; k < kMaxFold; ++k) {
+      const float w = k <= last ? 1.f : 0.f;
+      gg.x += w * x[k - 1].x; gg.y += w * x[k - 1].y; gg.z += w * x[k - 1].z; gg.w += w * x[k - 1].w;
     }
     g4[i] = gg;
   }

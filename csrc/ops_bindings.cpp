@@ -149,7 +149,8 @@ void lenet_fc_bwd(const at::Tensor& P2, const at::Tensor& H1, const at::Tensor& 
 void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tensor& P1, const at::Tensor& A1,
                     const at::Tensor& dP2m, const at::Tensor& A2, const at::Tensor& W2c, int64_t B,
                     const at::Tensor& gW1c, const at::Tensor& gb1c, const at::Tensor& gW2c, const at::Tensor& gb2c,
-                    int64_t c1_nrep, int64_t c1_rep_stride, int64_t dbg) {
+                    int64_t c1_nrep, int64_t c1_rep_stride, const OptT& row_loss, const OptT& row_hit,
+                    const OptT& loss_sum, const OptT& correct, int64_t dbg) {
   check_cuda(X, "X", F32);
   check_cuda(rows, "rows", I32, B);
   check_cuda(P1, "P1", F32, B * 2880);
@@ -167,8 +168,10 @@ void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tenso
   check_cuda(gb2c, "gb2c", F32, 50);
   hip_check(pde_lenet_conv_bwd(ptr<float>(X), ptr<int>(rows), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(dP2m),
                                ptr<uint8_t>(A2), ptr<float>(W2c), (int)B, ptr<float>(gW1c), ptr<float>(gb1c),
-                               ptr<float>(gW2c), ptr<float>(gb2c), (int)c1_nrep, (int)c1_rep_stride, (int)dbg,
-                               cur_stream()),
+                               ptr<float>(gW2c), ptr<float>(gb2c), (int)c1_nrep, (int)c1_rep_stride,
+                               optr<float>(row_loss, "row_loss", F32, B), optr<int>(row_hit, "row_hit", I32, B),
+                               optr<double>(loss_sum, "loss_sum", F64, 1),
+                               optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, cur_stream()),
             "lenet_conv_bwd");
 }
 
@@ -183,7 +186,8 @@ void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, co
   check_cuda(m, "exp_avg", F32, n);
   if (fold_off >= 0 && fold_nrep > 1)
     TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
-                    fold_off + fold_stride * fold_nrep <= n, "bad gradient fold layout");
+                    fold_off + fold_stride * fold_nrep <= n && fold_nrep <= 16,
+                "bad gradient fold layout (at most 16 replicas)");
   check_cuda(v, "exp_avg_sq", F32, n);
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
   TORCH_CHECK(bump >= -1, "bump must be >= -1");
@@ -208,7 +212,8 @@ void sgd_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, d
   check_cuda(buf, "momentum_buffer", F32, momentum != 0.0 ? n : 0);
   if (fold_off >= 0 && fold_nrep > 1)
     TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
-                    fold_off + fold_stride * fold_nrep <= n, "bad gradient fold layout");
+                    fold_off + fold_stride * fold_nrep <= n && fold_nrep <= 16,
+                "bad gradient fold layout (at most 16 replicas)");
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
   TORCH_CHECK(bump >= -1, "bump must be >= -1");
   check_cuda(arrive, "arrive", I32, 1);
@@ -386,7 +391,9 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("part") = 0);
   m.def("lenet_conv_bwd", &lenet_conv_bwd, py::arg("X"), py::arg("rows"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("gW2c"), py::arg("gb2c"),
-        py::arg("c1_nrep") = 1, py::arg("c1_rep_stride") = 0, py::arg("dbg") = 0);
+        py::arg("c1_nrep") = 1, py::arg("c1_rep_stride") = 0, py::arg("row_loss") = py::none(),
+        py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(), py::arg("correct") = py::none(),
+        py::arg("dbg") = 0);
   m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("decoupled"), py::arg("grad_scale"), py::arg("step"),
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),

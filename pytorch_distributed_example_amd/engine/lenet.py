@@ -155,11 +155,12 @@ class LeNetTrainStep:
         K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1, self.counters)   # bumps counters
         K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], self.cur_lbl, 1.0 / B, None, self.dZ2, self.dZ1,
                      self.row_loss, self.row_hit, None, None)
+        # the loss / accuracy meters are folded by an extra block of conv_bwd (off fc_bwd's chain)
         fc_args = (self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
-                   g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], self.row_loss, self.row_hit, self.loss_sum,
-                   self.correct)
+                   g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], None, None, None, None)
         conv_args = (self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
-                     self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE)
+                     self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE,
+                     self.row_loss, self.row_hit, self.loss_sum, self.correct)
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)

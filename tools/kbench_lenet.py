@@ -38,12 +38,13 @@ def main():
 
     def fc_bwd(dbg):
         return lambda: K.lenet_fc_bwd(e.P2, e.H1, e.dZ1, e.dZ2, p["fc1.weight"], B, e.dP2m, g["fc1.weight"],
-                                      g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], e.row_loss, e.row_hit,
-                                      e.loss_sum, e.correct, dbg)
+                                      g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], None, None, None, None,
+                                      dbg)
 
     def conv_bwd(dbg):
         return lambda: K.lenet_conv_bwd(e.X, e.cur_row, e.P1, e.A1, e.dP2m, e.A2, p["conv2.weight"], B,
-                                        e.g_c1w_rep, e.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], 16, 576, dbg)
+                                        e.g_c1w_rep, e.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], 16, 576,
+                                        e.row_loss, e.row_hit, e.loss_sum, e.correct, dbg)
 
     variants = {
         "conv_fwd": conv_fwd(0),
@@ -73,6 +74,39 @@ def main():
         "adam": lambda: K.adam_flat(e.params, e.grads, e.m, e.v, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1.0, e.counters,
                                     e.arrive, -1, e.pack_off, e.Wt2, e.c1_off, 576, 16, 576),
     }
+    # whole-step variants: the real producer -> consumer chain (caches / XCD state as in training),
+    # with one kernel's roles ablated, to attribute in-step time (isolated launches of the same kernel
+    # back-to-back re-read hot inputs and can under-state it by ~2x).
+    def step(fc_dbg=0, cv_dbg=0, adam=True, fc_split=False):
+        def run():
+            conv_fwd(0)()
+            K.lenet_fc1_fwd(e.P2, B, p["fc1.weight"], p["fc1.bias"], e.H1, None)
+            K.lenet_head(e.H1, B, p["fc2.weight"], p["fc2.bias"], e.cur_lbl, 1.0 / B, None, e.dZ2, e.dZ1,
+                         e.row_loss, e.row_hit, None, None)
+            if fc_split:
+                for part in (1, 2):
+                    K.lenet_fc_bwd(e.P2, e.H1, e.dZ1, e.dZ2, p["fc1.weight"], B, e.dP2m, g["fc1.weight"],
+                                   g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], None, None, None, None,
+                                   0, part)
+            else:
+                fc_bwd(fc_dbg)()
+            conv_bwd(cv_dbg)()
+            if adam:
+                variants["adam"]()
+        return run
+
+    variants.update({
+        "STEP": step(),
+        "STEP fc onlyC": step(fc_dbg=6),
+        "STEP fc onlyA": step(fc_dbg=5),
+        "STEP fc onlyB": step(fc_dbg=3),
+        "STEP fc none": step(fc_dbg=7),
+        "STEP fc split C;AB": step(fc_split=True),
+        "STEP cv onlyW": step(cv_dbg=2),
+        "STEP cv onlyD": step(cv_dbg=1),
+        "STEP cv none": step(cv_dbg=3),
+        "STEP -adam": step(adam=False),
+    })
     # graph mode: G launches of a variant captured in one hipGraph -> GPU-side cost per launch
     # (kernel + boundary), free of the ~4 us host launch overhead of eager Python launches
     G = int(os.environ.get("KB_G", "20"))
