@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STAGE=${1:-all}
 # pytest rc 1 (= some test failed) still lets the later stages run; a crash / timeout (other rc) stops.
-run_tests() { timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; r=$?; [ $r -le 1 ]; }
+run_tests() { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; r=$?; [ $r -le 1 ]; }
 run_smoke() { timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1; }
 run_bench() {
   timeout -k 10 300 python bench.py --steps 2000 --warmup 200 > gpurun_out/bench_graph.json 2> gpurun_out/bench_graph.err &&
