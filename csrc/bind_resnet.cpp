@@ -118,6 +118,81 @@ void sgd_master(const at::Tensor& master, const at::Tensor& p16, const at::Tenso
             "sgd_master");
 }
 
+// ---- implicit-GEMM convolutions (conv.hip) ----
+struct ConvGeom {
+  int64_t Bn, C, H, W, N, R, S, OH, OW;
+};
+
+ConvGeom conv_geom(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == BF16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv: x must be a 4-D channels-last bf16 GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == BF16 && w.dim() == 4 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv: weight must be a 4-D channels-last bf16 GPU tensor");
+  ConvGeom g{x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(2), w.size(3), 0, 0};
+  TORCH_CHECK(w.size(1) == g.C, "conv: weight in-channels ", w.size(1), " != input channels ", g.C);
+  TORCH_CHECK(g.C % 64 == 0 && g.N % 64 == 0 && g.R * g.S <= 9 && (stride == 1 || stride == 2) && pad >= 0 &&
+                  pad < g.R,
+              "conv: needs C % 64 == 0, Cout % 64 == 0, kernel <= 3x3, stride 1 or 2");
+  g.OH = (g.H + 2 * pad - g.R) / stride + 1;
+  g.OW = (g.W + 2 * pad - g.S) / stride + 1;
+  TORCH_CHECK(g.OH > 0 && g.OW > 0, "conv: empty output");
+  TORCH_CHECK(g.Bn * std::max(g.H * g.W * g.C, g.OH * g.OW * g.N) * 2 < (int64_t(1) << 31),
+              "conv: tensors must be < 2 GiB (32-bit buffer offsets)");
+  return g;
+}
+
+int64_t conv_stats_blocks(int64_t M, int64_t N) { return pde_conv_fprop_mtiles((int)M, (int)N); }
+
+void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats, int64_t stride,
+                int64_t pad) {
+  const ConvGeom g = conv_geom(x, w, stride, pad);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == BF16 && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  y.size(0) == g.Bn && y.size(1) == g.N && y.size(2) == g.OH && y.size(3) == g.OW,
+              "conv: y must be channels-last bf16 [B, Cout, OH, OW]");
+  const int64_t M = g.Bn * g.OH * g.OW;
+  float* sp = optr<float>(stats, "stats", F32, conv_stats_blocks(M, g.N) * 2 * g.N);
+  hip_check(pde_conv_fprop(x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
+                           (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, cur_stream()),
+            "conv_fprop");
+}
+
+void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt, const at::Tensor& dx,
+                int64_t stride, int64_t pad) {
+  const ConvGeom g = conv_geom(dx, w, stride, pad);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
+              "conv dgrad: dy must be channels-last bf16 [B, Cout, OH, OW]");
+  check_cuda(wt, "wt", BF16, g.N * g.C * g.R * g.S);
+  hip_check(pde_conv_wtrans(w.data_ptr(), wt.data_ptr(), (int)g.N, (int)(g.R * g.S), (int)g.C, cur_stream()),
+            "conv_wtrans");
+  hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
+                           (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, cur_stream()),
+            "conv_dgrad");
+}
+
+int64_t conv_wgrad_splits(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  const ConvGeom g = conv_geom(x, w, stride, pad);
+  return pde_conv_wgrad_splits((int)g.Bn, (int)g.OH, (int)g.OW, (int)g.N, (int)(g.R * g.S), (int)g.C);
+}
+
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& part,
+                int64_t splits, const at::Tensor& dw, int64_t stride, int64_t pad) {
+  const ConvGeom g = conv_geom(x, w, stride, pad);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
+              "conv wgrad: dy must be channels-last bf16 [B, Cout, OH, OW]");
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == BF16 && dw.sizes() == w.sizes() &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv wgrad: dw must be a channels-last bf16 tensor shaped like the weight");
+  check_cuda(part, "part", F32, splits * g.N * g.R * g.S * g.C);
+  hip_check(pde_conv_wgrad(dy.data_ptr(), x.data_ptr(), ptr<float>(part), (int)splits, dw.data_ptr(), (int)g.Bn,
+                           (int)g.H, (int)g.W, (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad,
+                           (int)g.OH, (int)g.OW, cur_stream()),
+            "conv_wgrad");
+}
+
 }  // namespace
 
 void register_resnet(pybind11::module& m) {
@@ -127,6 +202,11 @@ void register_resnet(pybind11::module& m) {
   m.def("sgd_master", &sgd_master);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("conv_stats_blocks", &conv_stats_blocks);
+  m.def("conv_fprop", &conv_fprop);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad_splits", &conv_wgrad_splits);
+  m.def("conv_wgrad", &conv_wgrad);
 }
 
 }  // namespace pde

@@ -90,6 +90,17 @@ hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st);
 int pde_colsum_bf16_splits(int C);
 hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, hipStream_t st);
 
+// ---- implicit-GEMM bf16 convolutions, NHWC (conv.hip) ----
+int pde_conv_fprop_mtiles(int M, int N);
+hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, int Bn, int H, int W, int C, int N,
+                          int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
+hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStream_t st);
+hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int H, int W, int C, int N, int R, int S,
+                          int stride, int pad, int OH, int OW, hipStream_t st);
+int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C);
+hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,
+                          int C, int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
+
 // ---- attention (attention.hip) ----
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
                         int T, int H, float scale, hipStream_t st);

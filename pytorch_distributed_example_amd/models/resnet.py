@@ -1,8 +1,8 @@
 """ResNet-18 (bf16, channels-last) -- driver-added config of BASELINE.json ("ResNet-18 bf16 on
 synthetic 3x224x224, DDP 8xMI355X").  Same architecture / parameter names as torchvision's
 ``resnet18`` (conv1/bn1, layer1..layer4 of BasicBlocks with downsample, fc), so state_dicts
-interchange; BatchNorm+residual+ReLU run as fused HIP kernels (``ops.resnet``), convolutions as
-MIOpen convolutions on channels-last bf16.
+interchange; BatchNorm+residual+ReLU run as fused HIP kernels (``ops.resnet``); every convolution except the 3-channel
+stem is an implicit GEMM on bf16 MFMA (``csrc/kernels/conv.hip``), the stem a MIOpen convolution.
 """
 from __future__ import annotations
 
@@ -12,7 +12,7 @@ import torch
 import torch.nn as tnn
 import torch.nn.functional as F
 
-from ..ops.resnet import batch_norm_act, max_pool3s2
+from ..ops.resnet import batch_norm_act, conv2d_nhwc, max_pool3s2
 
 
 class BN(tnn.Module):
@@ -41,8 +41,15 @@ class BN(tnn.Module):
                               self.momentum, self.eps, residual, relu)
 
 
+class Conv2d(tnn.Conv2d):
+    """torch Conv2d (same parameter name / layout / init) whose forward runs the MFMA implicit GEMM."""
+
+    def forward(self, x):
+        return conv2d_nhwc(x, self.weight, self.stride[0], self.padding[0])
+
+
 def _conv(cin, cout, k, stride=1, pad=0):
-    c = tnn.Conv2d(cin, cout, k, stride, pad, bias=False)
+    c = Conv2d(cin, cout, k, stride, pad, bias=False)
     tnn.init.kaiming_normal_(c.weight, mode="fan_out", nonlinearity="relu")
     return c
 

@@ -5,8 +5,10 @@ Forward:  y = relu(bn(x) + res)   -- 3 launches: partial stats, per-channel fina
           update), one streaming apply pass.
 Backward: dy' = dy * (y > 0); dres = dy'; dx = BN backward of dy'  -- reduce, finalize (writes
           dgamma / dbeta), one streaming apply pass that also emits dres.
-The convolutions themselves are library convolutions (MIOpen through ``torch.nn.functional.conv2d``
-on channels-last bf16 tensors); CPU tensors use the PyTorch reference definition.
+Convolutions with C_in, C_out multiples of 64 and kernels up to 3x3 (every ResNet-18 conv but the
+3-channel stem) are implicit GEMMs on bf16 MFMA (``csrc/kernels/conv.hip``): fprop, phase-split
+dgrad and split-K wgrad.  The stem runs as a library (MIOpen) convolution; CPU tensors use the
+PyTorch reference definitions.
 """
 from __future__ import annotations
 
@@ -60,6 +62,53 @@ class BatchNormActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if ctx.has_res else None
         K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, ctx.relu)
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+class Conv2dNHWCFn(torch.autograd.Function):
+    """Bias-free conv2d over channels-last bf16 on the implicit-GEMM MFMA kernels."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        N, C, H, W = x.shape
+        O, _, R, S = w.shape
+        OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        y = torch.empty(N, O, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+        kernels().conv_fprop(x, w, y, None, stride, pad)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        K = kernels()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            wt = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
+            K.conv_dgrad(dy, w, wt, dx, ctx.stride, ctx.pad)
+        if ctx.needs_input_grad[1]:
+            splits = K.conv_wgrad_splits(x, w, ctx.stride, ctx.pad)
+            part = torch.empty(splits * w.numel(), device=w.device, dtype=torch.float32)
+            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            K.conv_wgrad(dy, x, w, part, splits, dw, ctx.stride, ctx.pad)
+        return dx, dw, None, None
+
+
+def igemm_eligible(x, w, stride: int, pad: int) -> bool:
+    """True when the MFMA implicit-GEMM kernels cover this convolution."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[2] * w.shape[3] <= 9
+            and stride in (1, 2) and 0 <= pad < w.shape[2])
+
+
+def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0):
+    """conv2d (no bias) for channels-last bf16 activations: MFMA implicit GEMM where eligible."""
+    if igemm_eligible(x, w, stride, pad):
+        return Conv2dNHWCFn.apply(x.contiguous(memory_format=torch.channels_last),
+                                  w.contiguous(memory_format=torch.channels_last), stride, pad)
+    return F.conv2d(x, w, None, stride, pad)
 
 
 def batch_norm_act(x, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,

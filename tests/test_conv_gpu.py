@@ -1,0 +1,89 @@
+"""Implicit-GEMM bf16 MFMA convolutions (csrc/kernels/conv.hip) vs a PyTorch fp32 reference of the
+same op on the same bf16-rounded operands: fprop, phase-split dgrad (stride 2 incl. 1x1 / stride 2
+with its all-zero phases), split-K wgrad, ragged pixel tiles, and the fused BatchNorm partial sums."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_example_amd._ext import kernels
+from pytorch_distributed_example_amd.ops.resnet import conv2d_nhwc, igemm_eligible
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+SHAPES = [
+    # B, Cin, H, W, Cout, k, stride, pad
+    (2, 64, 9, 9, 64, 3, 1, 1),
+    (3, 64, 12, 10, 128, 3, 2, 1),
+    (2, 64, 8, 8, 128, 1, 2, 0),
+    (2, 128, 7, 7, 128, 1, 1, 0),
+    (1, 256, 7, 7, 512, 3, 1, 1),
+    (5, 128, 13, 11, 256, 3, 2, 1),
+    (4, 64, 56, 56, 64, 3, 1, 1),      # ResNet-18 layer1 geometry
+    (2, 512, 7, 7, 512, 3, 1, 1),      # layer4
+]
+
+
+def cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def max_rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("B,C,H,W,N,k,s,p", SHAPES)
+def test_conv_fwd_bwd(B, C, H, W, N, k, s, p):
+    torch.manual_seed(B * 1000 + C + k)
+    x = cl(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16)).requires_grad_()
+    w = cl((torch.randn(N, C, k, k, device=dev) / (C * k * k) ** 0.5).to(torch.bfloat16)).requires_grad_()
+    assert igemm_eligible(x, w, s, p)
+    y = conv2d_nhwc(x, w, s, p)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    dy = cl(torch.randn_like(y))
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, s, p)
+    yr.backward(dy.float())
+    assert y.shape == yr.shape
+    assert max_rel(y, yr) < 1e-2
+    assert max_rel(x.grad, xr.grad) < 1e-2
+    assert max_rel(w.grad, wr.grad) < 1e-2
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_conv_exact_integer_data():
+    """Small integers are exact in bf16 and in fp32 accumulation: any indexing slip shows exactly."""
+    torch.manual_seed(7)
+    B, C, H, W, N = 3, 64, 6, 5, 128
+    x = cl(torch.randint(-1, 2, (B, C, H, W), device=dev).to(torch.bfloat16)).requires_grad_()
+    w = cl(torch.randint(-1, 2, (N, C, 3, 3), device=dev).to(torch.bfloat16)).requires_grad_()
+    y = conv2d_nhwc(x, w, 2, 1)
+    dy = cl(torch.randint(-1, 2, y.shape, device=dev).to(torch.bfloat16))
+    y.backward(dy)
+    xr, wr = x.detach().double().cpu().requires_grad_(), w.detach().double().cpu().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 2, 1)
+    yr.backward(dy.double().cpu())
+    assert torch.equal(y.double().cpu(), yr)
+    assert torch.equal(x.grad.double().cpu(), xr.grad)
+    assert torch.equal(w.grad.double().cpu(), wr.grad)
+
+
+@pytest.mark.parametrize("N", [64, 128])
+def test_conv_fprop_bn_stats(N):
+    torch.manual_seed(11)
+    K = kernels()
+    B, C, H, W = 3, 64, 10, 9
+    x = cl(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16))
+    w = cl((torch.randn(N, C, 3, 3, device=dev) / 24).to(torch.bfloat16))
+    y = cl(torch.empty(B, N, H, W, device=dev, dtype=torch.bfloat16))
+    M = B * H * W
+    nblk = K.conv_stats_blocks(M, N)
+    stats = torch.empty(nblk * 2 * N, device=dev)
+    K.conv_fprop(x, w, y, stats, 1, 1)
+    st = stats.view(nblk, 2, N).sum(0)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, N)
+    assert torch.allclose(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
