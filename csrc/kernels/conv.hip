@@ -505,11 +505,13 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int 
 }
 
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C) {
+  // ~2 blocks per CU in total and >= 16 pixel stages per block: enough parallelism without
+  // making the fp32 slab round trip (splits x N x T*C x 4 B, written and re-read) dominate.
   const int P = Bn * OH * OW, stages = (P + 63) / 64;
   const int BM = N % 128 == 0 ? 128 : 64, BN = 128;
   const int tiles = (N / BM) * ((T * C + BN - 1) / BN);
-  int splits = (2048 + tiles - 1) / tiles;               // aim at ~8 blocks per CU
-  splits = max(1, min(splits, stages / 8));               // >= 8 pixel stages per block
+  int splits = (512 + tiles - 1) / tiles;
+  splits = min(splits, stages / 16);
   return max(1, splits);
 }
 

@@ -35,7 +35,7 @@ class BN(tnn.Module):
         return self
 
     def forward(self, x, residual=None, relu=True):
-        if self.training:
+        if self.training and not getattr(self, "_counted_by_model", False):
             self.num_batches_tracked.add_(1)
         return batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                               self.momentum, self.eps, residual, relu)
@@ -94,7 +94,24 @@ class ResNet(tnn.Module):
         tnn.init.uniform_(self.fc.weight, -bound, bound)
         tnn.init.uniform_(self.fc.bias, -bound, bound)
 
+    def _bn_counters(self):
+        """All BN ``num_batches_tracked`` buffers as views of one int64 tensor, so a training forward
+        bumps them with one launch instead of 20 (re-linked after ``.to()`` / buffer replacement)."""
+        bns = [m for m in self.modules() if isinstance(m, BN)]
+        sh = self.__dict__.get("_nbt_shared")
+        ok = sh is not None and sh.device == bns[0].num_batches_tracked.device and all(
+            b.num_batches_tracked.data_ptr() == sh.data_ptr() + i * sh.element_size() for i, b in enumerate(bns))
+        if not ok:
+            sh = torch.stack([b.num_batches_tracked.detach() for b in bns])
+            for i, b in enumerate(bns):
+                b._buffers["num_batches_tracked"] = sh[i]
+                b._counted_by_model = True
+            self.__dict__["_nbt_shared"] = sh
+        return sh
+
     def forward(self, x):
+        if self.training:
+            self._bn_counters().add_(1)
         x = self.bn1(self.conv1(x))
         x = max_pool3s2(x)
         for i in range(1, 5):

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from .._ext import kernels
+from ..parallel.flat import flat_grad_slot
 
 
 class BatchNormActFn(torch.autograd.Function):
@@ -42,13 +43,13 @@ class BatchNormActFn(torch.autograd.Function):
                 rstd.copy_(r)
         K.bn_fwd(x, res, y, gamma, beta, eps, momentum, run_mean if training else None,
                  run_var if training else None, part, mean, rstd, scale, shift, relu, training)
-        ctx.save_for_backward(x, y, gamma, mean, rstd)
+        ctx.save_for_backward(x, y, gamma, beta, mean, rstd)
         ctx.relu, ctx.has_res = relu, res is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, gamma, mean, rstd = ctx.saved_tensors
+        x, y, gamma, beta, mean, rstd = ctx.saved_tensors
         K = kernels()
         C = x.shape[1]
         M = x.numel() // C
@@ -56,8 +57,10 @@ class BatchNormActFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
         part = torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev, dtype=torch.float32)
         coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
-        dgamma = torch.empty(C, device=dev, dtype=gamma.dtype)
-        dbeta = torch.empty(C, device=dev, dtype=gamma.dtype)
+        dgamma = flat_grad_slot(gamma)
+        dgamma = torch.empty(C, device=dev, dtype=gamma.dtype) if dgamma is None else dgamma
+        dbeta = flat_grad_slot(beta)
+        dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
         K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, ctx.relu)
@@ -91,7 +94,9 @@ class Conv2dNHWCFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             splits = K.conv_wgrad_splits(x, w, ctx.stride, ctx.pad)
             part = torch.empty(splits * w.numel(), device=w.device, dtype=torch.float32)
-            dw = torch.empty_like(w, memory_format=torch.channels_last)
+            dw = flat_grad_slot(w)
+            if dw is None or not dw.is_contiguous(memory_format=torch.channels_last):
+                dw = torch.empty_like(w, memory_format=torch.channels_last)
             K.conv_wgrad(dy, x, w, part, splits, dw, ctx.stride, ctx.pad)
         return dx, dw, None, None
 

@@ -87,8 +87,12 @@ class _MasterBase(torch.optim.Optimizer):
                 v.copy_(p.grad)
                 p.grad = v
 
-    def zero_grad(self, set_to_none: bool = False):
-        if self._flat is not None:
+    def zero_grad(self, set_to_none: bool = True):
+        """Default (torch semantics): gradients become None.  Ops that know the flat layout then write
+        the next gradients straight into the flat buffer (``parallel.flat.flat_grad_slot``) and
+        ``step`` zero-fills the slots of parameters that received none; ``set_to_none=False`` zeroes
+        the flat buffer and keeps the views."""
+        if self._flat is not None and not set_to_none:
             self._flat["g"].zero_()
         else:
             for p in self._all_params():

@@ -136,7 +136,7 @@ class DistributedDataParallel(nn.Module):
                 for n in bk.names:
                     p = self._params[n]
                     if p.grad is None:
-                        p.grad = self._grad_view(n)
+                        p.grad = self._grad_view(n).zero_()
                 self._launch(bk)
         for bk in self.buckets:
             bk.work.wait()

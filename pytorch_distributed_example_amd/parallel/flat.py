@@ -4,7 +4,10 @@ All parameters of a module are re-homed into ONE contiguous fp32 buffer (``p.dat
 and all gradients into a second one (``p.grad`` is a view).  Buckets are contiguous ranges of
 both buffers, so a bucket all-reduce is a single collective on a zero-copy view, and the fused
 optimizer updates every parameter in one launch.  Each tensor starts on a 64-element (256 B)
-boundary, so vectorised kernels and RCCL see aligned buffers.
+boundary, so vectorised kernels and RCCL see aligned buffers.  A 4-D parameter that is
+channels-last when bound keeps that layout: its slot stores [N][H][W][C] and every view of it
+(parameter, gradient, optimizer state) carries channels-last strides, so NHWC kernels read the
+weights in place and write weight gradients straight into the flat gradient buffer.
 """
 from __future__ import annotations
 
@@ -22,6 +25,7 @@ class Slot:
     offset: int
     numel: int
     shape: Tuple[int, ...]
+    channels_last: bool = False
 
 
 class FlatLayout:
@@ -71,10 +75,12 @@ class FlatLayout:
             if n not in self.param_names:
                 continue
             p = params[n]
-            v = flat_p[s.offset: s.offset + s.numel].view(s.shape)
+            s.channels_last = (p.dim() == 4 and not p.is_contiguous()
+                               and p.is_contiguous(memory_format=torch.channels_last))
+            v = self.view(flat_p, n)
             v.copy_(p.detach())
             p.data = v
-            gv = flat_g[s.offset: s.offset + s.numel].view(s.shape)
+            gv = self.view(flat_g, n)
             if p.grad is not None:          # binding after a backward (lazy optimizer init): keep the grad
                 gv.copy_(p.grad.detach())
             p.grad = gv
@@ -83,7 +89,11 @@ class FlatLayout:
 
     def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
         s = self.slots[name]
-        return flat[s.offset: s.offset + s.numel].view(s.shape)
+        v = flat[s.offset: s.offset + s.numel]
+        if s.channels_last:
+            n, c, h, w = s.shape
+            return v.view(n, h, w, c).permute(0, 3, 1, 2)
+        return v.view(s.shape)
 
     def bucket_view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
         a, b = self.bucket_ranges[i]
@@ -107,6 +117,19 @@ def reverse_order_buckets(named_shapes, cap_bytes: int, elem_bytes: int = 4):
     if cur:
         buckets.append(cur)
     return buckets
+
+
+def flat_grad_slot(p: torch.Tensor):
+    """Where an op should write ``p``'s gradient: a fresh view of ``p``'s flat gradient slot (same
+    shape and strides as ``p``) when ``p`` is flat-bound and has no gradient yet, else None.  The op
+    overwrites the whole view and returns it; autograd then adopts it as ``p.grad`` without a copy
+    (``AccumulateGrad`` steals a layout-matching gradient), so DDP buckets and the fused optimizers
+    see it in place."""
+    tag = getattr(p, "_pde_flat", None)
+    if tag is None or p.grad is not None:
+        return None
+    layout, _, fg, name = tag
+    return layout.view(fg, name)
 
 
 def shared_flat(params):

@@ -162,3 +162,28 @@ def test_maxpool3s2(shape):
     yr.backward(g.float())
     assert torch.equal(y.float(), yr)
     assert rel_err(x.grad, xr.grad) < 1e-2
+
+
+def test_resnet18_grads_land_in_flat_buffer():
+    """After the optimizer binds the flat buffers, conv weights stay channels-last and every
+    gradient of a step is written in place into the flat gradient buffer (no per-parameter copy)."""
+    from pytorch_distributed_example_amd.parallel.flat import shared_flat
+    m = build_resnet18(num_classes=10, seed=1, device=dev)
+    opt = SGDMaster(m.decay_groups(5e-5), lr=0.05, momentum=0.9)
+    torch.manual_seed(4)
+    x = torch.randn(4, 3, 64, 64, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=dev)
+    for _ in range(2):
+        opt.zero_grad()
+        F.cross_entropy(m(x).float(), y).backward()
+        if _ == 1:
+            layout, fp, fg = shared_flat(list(m.parameters()))
+            for n, p in m.named_parameters():
+                if n.startswith(("conv1.", "fc.")):
+                    continue                                 # library ops (stem conv, fc) are copied
+                assert p.grad.data_ptr() == layout.view(fg, p._pde_flat[3]).data_ptr(), n
+        opt.step()
+    for n, p in m.named_parameters():
+        if p.dim() == 4 and p.shape[2] > 1:
+            assert p.is_contiguous(memory_format=torch.channels_last), n
+    assert int(m.bn1.num_batches_tracked) == 2 and int(m.layer4[1].bn2.num_batches_tracked) == 2
