@@ -30,7 +30,7 @@ int64_t bn_blocks(int64_t M, int64_t C) { return pde_bn_blocks((int)M, (int)C); 
 void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta,
             double eps, double momentum, const OptT& run_mean, const OptT& run_var, const at::Tensor& part,
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift, bool relu,
-            bool training) {
+            bool training, int64_t pre_nblk) {
   const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
   check_c(C);
   check_same(x, y, "y");
@@ -43,11 +43,13 @@ void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at:
   check_cuda(beta, "beta", BF16, C);
   float* rm = optr<float>(run_mean, "running_mean", F32, C);
   float* rv = optr<float>(run_var, "running_var", F32, C);
-  if (training) check_cuda(part, "part", F32, (int64_t)pde_bn_blocks((int)M, (int)C) * 2 * C);
+  if (training)
+    check_cuda(part, "part", F32,
+               (pre_nblk > 0 ? pde_bn_part_rows((int)pre_nblk) : (int64_t)pde_bn_blocks((int)M, (int)C)) * 2 * C);
   for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
   hip_check(pde_bn_fwd(x.data_ptr(), r, y.data_ptr(), (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
                        (float)momentum, rm, rv, ptr<float>(part), ptr<float>(mean), ptr<float>(rstd), ptr<float>(scale),
-                       ptr<float>(shift), relu, training, cur_stream()),
+                       ptr<float>(shift), relu, training, (int)pre_nblk, cur_stream()),
             "bn_fwd");
 }
 
@@ -144,6 +146,8 @@ ConvGeom conv_geom(const at::Tensor& x, const at::Tensor& w, int64_t stride, int
 }
 
 int64_t conv_stats_blocks(int64_t M, int64_t N) { return pde_conv_fprop_mtiles((int)M, (int)N); }
+// rows to allocate for a conv-stats buffer that feeds bn_fwd (partials + the finalize's pre-fold)
+int64_t bn_part_rows(int64_t nblk) { return pde_bn_part_rows((int)nblk); }
 
 void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, const OptT& stats, int64_t stride,
                 int64_t pad) {
@@ -203,6 +207,8 @@ void register_resnet(pybind11::module& m) {
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv_stats_blocks", &conv_stats_blocks);
+  m.def("bn_part_rows", &bn_part_rows);
+  m.def("conv_set_stages", [](int64_t n) { pde_conv_set_stages((int)n); });
   m.def("conv_fprop", &conv_fprop);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad_splits", &conv_wgrad_splits);

@@ -91,6 +91,7 @@ int pde_colsum_bf16_splits(int C);
 hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, hipStream_t st);
 
 // ---- implicit-GEMM bf16 convolutions, NHWC (conv.hip) ----
+void pde_conv_set_stages(int nst);
 int pde_conv_fprop_mtiles(int M, int N);
 hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, int Bn, int H, int W, int C, int N,
                           int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
@@ -111,9 +112,10 @@ hipError_t pde_attn_bwd(const void* q, const void* k, const void* v, int ldq, co
 
 // ---- resnet (resnet.hip) ----
 int pde_bn_blocks(int M, int C);
+int pde_bn_part_rows(int pre_nblk);
 hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
                       float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
-                      float* rstd, float* scale, float* shift, int relu, int training, hipStream_t st);
+                      float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk, hipStream_t st);
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
                       int relu, hipStream_t st);

@@ -72,11 +72,45 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int row0, int col0) {
   return out;
 }
 
+// The same transposed read as inline asm, for loops with LDS-DMA in flight: hipcc puts a blanket
+// `s_waitcnt vmcnt(0)` before every ds_read_b64_tr_b16 builtin there (no memory operand to prove
+// it does not alias the DMA), which drains the prefetched stages.  The asm form is not tracked:
+// the caller waits with `lgkm_fence()` before using the fragments.
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ s4v ds_tr_asm(const char* p) {
+  s4v r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)(lds_char*)p));
+  return r;
+}
+__device__ __forceinline__ bf16x8 tr_frag_asm(const char* img, int row0, int col0) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int ch = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
+  const int r = row0 + 4 * h + q;
+  const s4v v0 = ds_tr_asm(img + toff(r, ch) + 8 * (p & 1));
+  const s4v v1 = ds_tr_asm(img + toff(r + 8, ch) + 8 * (p & 1));
+  bf16x8 out;
+  out[0] = v0[0]; out[1] = v0[1]; out[2] = v0[2]; out[3] = v0[3];
+  out[4] = v1[0]; out[5] = v1[1]; out[6] = v1[2]; out[7] = v1[3];
+  return out;
+}
+// wait for this wave's outstanding LDS reads; the sched_barrier keeps the MFMAs that consume
+// asm-loaded fragments from being hoisted above the wait (cdna_hip_programming.md §5.4 rule 18)
+__device__ __forceinline__ void lgkm_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // ============================================================================ fprop / dgrad
 struct Phase {
   int ph, pw, Hq, Wq, ntap;
-  signed char dh[9], dw[9], widx[9];
+  // per tap, packed into one dword so the wave-uniform lookup in the K loop is a scalar load
+  // (byte-sized kernarg elements become VECTOR loads, whose vmcnt wait would drain the in-flight
+  // LDS-DMA stages): bits 0-7 dh, 8-15 dw (signed), 16-23 weight tap index
+  int tap[9];
 };
+__host__ __device__ inline int pack_tap(int dh, int dw, int widx) {
+  return (dh & 0xff) | ((dw & 0xff) << 8) | (widx << 16);
+}
 struct IgemmArgs {
   const bf16_t* A;      // gather source NHWC [Bn][IH][IW][CA]
   const bf16_t* W;      // [NC][T][CA]
@@ -92,13 +126,38 @@ struct IgemmArgs {
 
 constexpr int kThreads = 256;
 
-template <int BM, int BN>
-__global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a) {
+// 16-byte buffer load straight into LDS (LDS-DMA): lane l of the wave writes lds + 16*l, the LDS
+// base must be wave-uniform; a global offset past the resource returns zeros.
+__device__ __forceinline__ void glds16(rsrc_t r, const char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+}
+// The lane -> (row, chunk) map that makes a glds wave-instruction (64 x 16 B, lane-linear in LDS)
+// fill one 8-row group of the toff() image: lane l writes 8-row group offset 16*l, i.e. row
+// (l>>2)&7 of the group and the chunk whose swizzled slot that is (g1 = parity of the group index).
+__device__ __forceinline__ int glds_row(int l) { return (l >> 2) & 7; }
+__device__ __forceinline__ int glds_chunk(int l, int g1) {
+  return 4 * (l >> 5) + ((l & 3) ^ ((((l >> 2) & 7) >> 2) | (g1 << 1)));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Pipeline: NST LDS stage buffers filled by LDS-DMA, NST-1 stages in flight ahead of the MFMAs.
+// Per stage: wait for this wave's DMA of the stage (counted vmcnt, never a blanket drain while a
+// younger stage is in flight), raw s_barrier (every wave's DMA for the stage has landed, and every
+// wave is done reading the buffer about to be refilled), issue the stage NST-1 ahead, compute.
+template <int BM, int BN, int NST>
+__global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs a) {
   constexpr int WN = BN / 64, WM = 4 / WN;
   static_assert(WM * 64 == BM, "wave grid must tile BM x BN with 64x64 wave tiles");
-  constexpr int AU = BM / 32, BU = BN / 32;         // 16-B chunks per thread per stage
+  constexpr int AI = BM / 32, BI = BN / 32;         // glds wave-instructions per wave per stage
+  constexpr int LPS = AI + BI;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int RS = BN * 2 + 16;                    // epilogue LDS row stride (bytes)
+  constexpr int EPI = BM * RS + 2 * WM * BN * 4;
+  constexpr int SMEM = NST * STAGE > EPI ? NST * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int nwg = gridDim.x;
@@ -114,12 +173,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a) {
   const int KT = P.ntap * CPT;
   const int ldw = a.T * a.CA;
 
-  // ---- per-thread gather rows (fixed for the whole K loop) ----
-  const int ch = t & 7;
-  int pix[AU], hb[AU], wb[AU];
+  // ---- per-thread gather rows: instruction i fills 8-row group 4i + w, this lane row glds_row ----
+  const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
+  int pix[AI], hb[AI], wb[AI];
 #pragma unroll
-  for (int u = 0; u < AU; ++u) {
-    const int m = m0 + (t >> 3) + 32 * u;
+  for (int u = 0; u < AI; ++u) {
+    const int m = m0 + 8 * (4 * u + w) + lrow;
     if (m < Mq) {
       const int b = m / (P.Hq * P.Wq), r2 = m % (P.Hq * P.Wq);
       const int hq = r2 / P.Wq, wq = r2 % P.Wq;
@@ -133,31 +192,25 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a) {
     }
   }
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), wr = make_rsrc(a.W, a.w_bytes);
-  uint32_t wrow[BU];
+  uint32_t wrow[BI];
 #pragma unroll
-  for (int v = 0; v < BU; ++v) wrow[v] = ((n0 + (t >> 3) + 32 * v) * ldw + ch * 8) * 2;
+  for (int v = 0; v < BI; ++v) wrow[v] = ((n0 + 8 * (4 * v + w) + lrow) * ldw + ch * 8) * 2;
 
-  uint4 ra[AU], rb[BU];
-  auto load_stage = [&](int kt) {
+  auto issue = [&](int kt, int buf) {
     const int tap = kt / CPT, c0 = (kt - tap * CPT) * 64;
-    const int dh = P.dh[tap], dw = P.dw[tap], wi = P.widx[tap];
+    const int tp = P.tap[tap];
+    const int dh = (int)(signed char)(tp & 0xff), dw = (int)(signed char)((tp >> 8) & 0xff), wi = tp >> 16;
+    const char* Ai = smem + buf * STAGE;
+    const char* Bi = Ai + ABYTES;
 #pragma unroll
-    for (int u = 0; u < AU; ++u) {
+    for (int u = 0; u < AI; ++u) {
       const int ih = hb[u] + dh, iw = wb[u] + dw;
       const bool ok = (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
       const uint32_t off = ((uint32_t)((pix[u] + ih * a.IW + iw) * a.CA + c0 + ch * 8)) * 2u;
-      ra[u] = bload16(ar, ok ? off : kOOB);
+      glds16(ar, Ai + (4 * u + w) * 1024, ok ? off : kOOB);
     }
 #pragma unroll
-    for (int v = 0; v < BU; ++v) rb[v] = bload16(wr, wrow[v] + (uint32_t)(wi * a.CA + c0) * 2u);
-  };
-  auto store_stage = [&](int buf) {
-    char* Ai = smem + buf * STAGE;
-    char* Bi = Ai + ABYTES;
-#pragma unroll
-    for (int u = 0; u < AU; ++u) *reinterpret_cast<uint4*>(Ai + toff((t >> 3) + 32 * u, ch)) = ra[u];
-#pragma unroll
-    for (int v = 0; v < BU; ++v) *reinterpret_cast<uint4*>(Bi + toff((t >> 3) + 32 * v, ch)) = rb[v];
+    for (int v = 0; v < BI; ++v) glds16(wr, Bi + (4 * v + w) * 1024, wrow[v] + (uint32_t)(wi * a.CA + c0) * 2u);
   };
 
   const int wm = w / WN, wn = w % WN, lr = l & 31, lh = l >> 5;
@@ -168,13 +221,24 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
 
   if (KT > 0) {
-    load_stage(0);
-    store_stage(0);
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NST - 1; ++s)
+      if (s < KT) issue(s, s);
+    int buf = 0;
     for (int kt = 0; kt < KT; ++kt) {
-      const bool more = kt + 1 < KT;
-      if (more) load_stage(kt + 1);
-      const char* Ai = smem + (kt & 1) * STAGE;
+      if constexpr (NST >= 3) {
+        if (kt + 1 < KT) wait_vm<LPS>();
+        else wait_vm<0>();
+      } else {
+        wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (kt + NST - 1 < KT) {
+        int nb = buf + NST - 1;
+        nb = nb >= NST ? nb - NST : nb;
+        issue(kt + NST - 1, nb);
+      }
+      const char* Ai = smem + buf * STAGE;
       const char* Bi = Ai + ABYTES;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -188,14 +252,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
       }
-      if (more) store_stage((kt + 1) & 1);
-      __syncthreads();
+      buf = buf + 1 == NST ? 0 : buf + 1;
     }
+    __syncthreads();                                   // every wave is done with the stage buffers
   }
 
   // ---- epilogue: bf16 tile through LDS, coalesced NHWC rows; optional BN partial stats ----
-  constexpr int RS = BN * 2 + 16;                    // padded LDS row stride (bytes)
-  static_assert(BM * RS + 2 * WM * BN * 4 <= 2 * STAGE, "epilogue LDS");
   char* ot = smem;
   float* sst = reinterpret_cast<float*>(smem + BM * RS);   // [WM][2][BN]
 #pragma unroll
@@ -271,16 +333,16 @@ struct WgradArgs {
   int P, stages_per_split, mtiles, ntiles;
 };
 
-template <int BM, int BN>
-__global__ __launch_bounds__(kThreads, 2) void k_wgrad(WgradArgs a) {
+template <int BM, int BN, int NST>
+__global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs a) {
   constexpr int WN = (BN / 64 >= 4) ? 4 : BN / 64;   // waves along the (tap, c) columns
   constexpr int WM = 4 / WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "wgrad tiling");
-  constexpr int AI = BM / 64, BI = BN / 64;          // 64-column images per operand
-  constexpr int ABYTES = AI * 8192, BBYTES = BI * 8192, STAGE = ABYTES + BBYTES;
-  constexpr int AU = BM / 32, BU = BN / 32;          // 16-B chunks per thread per stage (64 rows)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int ABYTES = (BM / 64) * 8192, BBYTES = (BN / 64) * 8192, STAGE = ABYTES + BBYTES;
+  constexpr int AI = BM / 32, BI = BN / 32;          // glds wave-instructions per wave per stage
+  constexpr int LPS = AI + BI;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
 
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
@@ -293,55 +355,40 @@ __global__ __launch_bounds__(kThreads, 2) void k_wgrad(WgradArgs a) {
   const int pend = min(a.P, pbeg + a.stages_per_split * 64);
   const int KT = (pend - pbeg + 63) / 64;
 
-  // chunk -> (pixel row, column chunk): dY rows hold BM/8 chunks, X rows BN/8 chunks
-  constexpr int ACPR = BM / 8, BCPR = BN / 8;
-  int xtap_r[BU], xtap_s[BU], xc[BU];
-  bool xcol_ok[BU];
+  // instruction u fills 8-row group (4u + w) % 8 of 64-column image (4u + w) / 8
+  const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
+  int xr_[BI], xs_[BI], xc_[BI];
 #pragma unroll
-  for (int v = 0; v < BU; ++v) {
-    const int c = t + kThreads * v, cc = c % BCPR;
-    const int col = k0 + cc * 8;
-    xcol_ok[v] = col < TC;
-    const int tap = min(col, TC - 1) / a.C;
-    xc[v] = min(col, TC - 1) - tap * a.C;
-    xtap_r[v] = tap / a.S - a.pad;
-    xtap_s[v] = tap % a.S - a.pad;
+  for (int v = 0; v < BI; ++v) {
+    const int col = k0 + ((4 * v + w) >> 3) * 64 + ch * 8;
+    const bool ok = col < TC;
+    const int cc = min(col, TC - 1);
+    const int tap = cc / a.C;
+    xc_[v] = cc - tap * a.C;
+    xr_[v] = ok ? tap / a.S - a.pad : -(1 << 20);    // a column past T*C reads zeros
+    xs_[v] = tap % a.S - a.pad;
   }
   const rsrc_t dyr = make_rsrc(a.dY, a.dy_bytes), xr = make_rsrc(a.X, a.x_bytes);
-  uint4 ra[AU], rb[BU];
-  auto load_stage = [&](int kt) {
+  auto issue = [&](int kt, int buf) {
     const int p0 = pbeg + kt * 64;
+    const char* Ai = smem + buf * STAGE;
+    const char* Bi = Ai + ABYTES;
 #pragma unroll
-    for (int u = 0; u < AU; ++u) {
-      const int c = t + kThreads * u, row = c / ACPR, cc = c % ACPR;
-      const int p = p0 + row;
-      ra[u] = bload16(dyr, p < pend ? (uint32_t)(p * a.N + n0 + cc * 8) * 2u : kOOB);
+    for (int u = 0; u < AI; ++u) {
+      const int q = 4 * u + w, p = p0 + 8 * (q & 7) + lrow;
+      const uint32_t off = (uint32_t)(p * a.N + n0 + (q >> 3) * 64 + ch * 8) * 2u;
+      glds16(dyr, Ai + q * 1024, p < pend ? off : kOOB);
     }
 #pragma unroll
-    for (int v = 0; v < BU; ++v) {
-      const int c = t + kThreads * v, row = c / BCPR;
-      const int p = p0 + row;
-      bool ok = p < pend && xcol_ok[v];
+    for (int v = 0; v < BI; ++v) {
+      const int q = 4 * v + w, p = p0 + 8 * (q & 7) + lrow;
       const int pp = min(p, a.P - 1);
-      const int b = pp / (a.OH * a.OW), r2 = pp % (a.OH * a.OW);
-      const int ih = (r2 / a.OW) * a.stride + xtap_r[v], iw = (r2 % a.OW) * a.stride + xtap_s[v];
-      ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
-      const uint32_t off = (uint32_t)(((b * a.IH + ih) * a.IW + iw) * a.C + xc[v]) * 2u;
-      rb[v] = bload16(xr, ok ? off : kOOB);
-    }
-  };
-  auto store_stage = [&](int buf) {
-    char* Ai = smem + buf * STAGE;
-    char* Bi = Ai + ABYTES;
-#pragma unroll
-    for (int u = 0; u < AU; ++u) {
-      const int c = t + kThreads * u, row = c / ACPR, cc = c % ACPR;
-      *reinterpret_cast<uint4*>(Ai + (cc >> 3) * 8192 + toff(row, cc & 7)) = ra[u];
-    }
-#pragma unroll
-    for (int v = 0; v < BU; ++v) {
-      const int c = t + kThreads * v, row = c / BCPR, cc = c % BCPR;
-      *reinterpret_cast<uint4*>(Bi + (cc >> 3) * 8192 + toff(row, cc & 7)) = rb[v];
+      const int b = pp / (a.OH * a.OW), r2 = pp - b * (a.OH * a.OW);
+      const int oh = r2 / a.OW, ow = r2 - oh * a.OW;
+      const int ih = oh * a.stride + xr_[v], iw = ow * a.stride + xs_[v];
+      const bool ok = p < pend && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      const uint32_t off = (uint32_t)(((b * a.IH + ih) * a.IW + iw) * a.C + xc_[v]) * 2u;
+      glds16(xr, Bi + q * 1024, ok ? off : kOOB);
     }
   };
 
@@ -353,34 +400,58 @@ __global__ __launch_bounds__(kThreads, 2) void k_wgrad(WgradArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
 
   if (KT > 0) {
-    load_stage(0);
-    store_stage(0);
-    __syncthreads();
-    for (int kt = 0; kt < KT; ++kt) {
-      const bool more = kt + 1 < KT;
-      if (more) load_stage(kt + 1);
-      const char* Ai = smem + (kt & 1) * STAGE;
-      const char* Bi = Ai + ABYTES;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 fa[TM], fb[TN];
+    for (int s = 0; s < NST - 1; ++s)
+      if (s < KT) issue(s, s);
+    int buf = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      if constexpr (NST >= 3) {
+        if (kt + 1 < KT) wait_vm<LPS>();
+        else wait_vm<0>();
+      } else {
+        wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (kt + NST - 1 < KT) {
+        int nb = buf + NST - 1;
+        nb = nb >= NST ? nb - NST : nb;
+        issue(kt + NST - 1, nb);
+      }
+      const char* Ai = smem + buf * STAGE;
+      const char* Bi = Ai + ABYTES;
+      // fragments of k-step s+1 are read while the MFMAs of k-step s run (two named register sets)
+      bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      auto rd = [&](int s, bf16x8* fa, bf16x8* fb) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int col = wm * (BM / WM) + i * 32;
-          fa[i] = tr_frag(Ai + (col >> 6) * 8192, 16 * s, col & 63);
+          fa[i] = tr_frag_asm(Ai + (col >> 6) * 8192, 16 * s, col & 63);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = wn * (BN / WN) + j * 32;
-          fb[j] = tr_frag(Bi + (col >> 6) * 8192, 16 * s, col & 63);
+          fb[j] = tr_frag_asm(Bi + (col >> 6) * 8192, 16 * s, col & 63);
         }
+      };
+      auto mm = [&](const bf16x8* fa, const bf16x8* fb) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
-      }
-      if (more) store_stage((kt + 1) & 1);
-      __syncthreads();
+      };
+      rd(0, fa0, fb0);
+      lgkm_fence();
+      rd(1, fa1, fb1);
+      mm(fa0, fb0);
+      lgkm_fence();
+      rd(2, fa0, fb0);
+      mm(fa1, fb1);
+      lgkm_fence();
+      rd(3, fa1, fb1);
+      mm(fa0, fb0);
+      lgkm_fence();
+      mm(fa1, fb1);
+      buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
   // D[n][k']: lane column k' = col + lr, registers = rows n
@@ -414,6 +485,8 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   *reinterpret_cast<uint2*>(dw + i) = pack4(f);
 }
 
+int g_conv_nst = 2;    // LDS pipeline depth of the conv kernels (2 or 3), pde_conv_set_stages
+
 template <int BM, int BN>
 hipError_t launch_igemm(IgemmArgs& a, hipStream_t st) {
   int maxm = 0;
@@ -421,7 +494,8 @@ hipError_t launch_igemm(IgemmArgs& a, hipStream_t st) {
   a.mtiles = (maxm + BM - 1) / BM;
   a.ntiles = a.NC / BN;
   const int grid = a.nphase * a.mtiles * a.ntiles;
-  hipLaunchKernelGGL((k_igemm<BM, BN>), dim3(grid), dim3(kThreads), 0, st, a);
+  if (g_conv_nst == 2) hipLaunchKernelGGL((k_igemm<BM, BN, 2>), dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((k_igemm<BM, BN, 3>), dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
@@ -433,6 +507,8 @@ hipError_t dispatch_igemm(IgemmArgs& a, hipStream_t st) {
 }  // namespace
 
 extern "C" {
+
+void pde_conv_set_stages(int nst) { g_conv_nst = nst == 3 ? 3 : 2; }
 
 int pde_conv_fprop_mtiles(int M, int N) { return N % 128 == 0 ? (M + 127) / 128 : (M + 255) / 256; }
 
@@ -454,9 +530,7 @@ hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, i
   for (int r = 0; r < R; ++r)
     for (int s = 0; s < S; ++s) {
       const int k = r * S + s;
-      P.dh[k] = (signed char)(r - pad);
-      P.dw[k] = (signed char)(s - pad);
-      P.widx[k] = (signed char)k;
+      P.tap[k] = pack_tap(r - pad, s - pad, k);
     }
   return dispatch_igemm(a, st);
 }
@@ -495,9 +569,8 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int 
         if (((nw % stride) + stride) % stride) continue;
         const int k = P.ntap++;
         // floor division of (possibly negative) exact multiples of stride
-        P.dh[k] = (signed char)(nh >= 0 ? nh / stride : -((-nh) / stride));
-        P.dw[k] = (signed char)(nw >= 0 ? nw / stride : -((-nw) / stride));
-        P.widx[k] = (signed char)(r * S + s);
+        P.tap[k] = pack_tap(nh >= 0 ? nh / stride : -((-nh) / stride), nw >= 0 ? nw / stride : -((-nw) / stride),
+                            r * S + s);
       }
     }
   }
@@ -533,10 +606,16 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   const int TC = a.T * C;
   if (N % 128 == 0) {
     a.mtiles = N / 128; a.ntiles = (TC + 127) / 128;
-    hipLaunchKernelGGL((k_wgrad<128, 128>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+    if (g_conv_nst == 2)
+      hipLaunchKernelGGL((k_wgrad<128, 128, 2>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_wgrad<128, 128, 3>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
   } else {
     a.mtiles = N / 64; a.ntiles = (TC + 127) / 128;
-    hipLaunchKernelGGL((k_wgrad<64, 128>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+    if (g_conv_nst == 2)
+      hipLaunchKernelGGL((k_wgrad<64, 128, 2>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_wgrad<64, 128, 3>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
   }
   PDE_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)N * TC;

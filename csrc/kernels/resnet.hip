@@ -98,6 +98,23 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   }
 }
 
+// out[y][c] = sum of partial rows [y*rows_per, (y+1)*rows_per) of part[nblk][W]: folds the many
+// per-tile partials of a conv epilogue (thousands of rows) before the per-channel finalize.
+__global__ __launch_bounds__(256) void k_fold_rows(const float* __restrict__ part, int nblk, int W, int rows_per,
+                                                   float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= W) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(nblk, r0 + rows_per);
+  float s0 = 0.f, s1 = 0.f;
+  int r = r0;
+  for (; r + 1 < r1; r += 2) {
+    s0 += part[(size_t)r * W + c];
+    s1 += part[(size_t)(r + 1) * W + c];
+  }
+  if (r < r1) s0 += part[(size_t)r * W + c];
+  out[(size_t)blockIdx.y * W + c] = s0 + s1;
+}
+
 // per channel: mean / biased var -> rstd, running-stat update (unbiased var), scale / shift
 __global__ __launch_bounds__(1024) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int M,
                                                       const bf16_t* __restrict__ gamma,
@@ -374,16 +391,33 @@ int pde_bn_blocks(int M, int C) {
   return nblk < 1 ? 1 : nblk;
 }
 
+constexpr int kFoldThreshold = 256, kFoldRows = 64;
+int pde_bn_part_rows(int pre_nblk) { return pre_nblk > kFoldThreshold ? pre_nblk + kFoldRows : pre_nblk; }
+
 hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
                       float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
-                      float* rstd, float* scale, float* shift, int relu, int training, hipStream_t st) {
+                      float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk,
+                      hipStream_t st) {
   if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
   const int CP = C / 8, RP = 256 / CP;
   if (training) {
-    const int nblk = pde_bn_blocks(M, C);
+    // pre_nblk > 0: `part` already holds [pre_nblk][2][C] partial sums (the producing convolution's
+    // epilogue, conv.hip), so the statistics pass over x is skipped
+    int nblk = pre_nblk > 0 ? pre_nblk : pde_bn_blocks(M, C);
     const int rpb = (M + nblk - 1) / nblk;
-    hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)x,
-                       M, C, rpb, part);
+    if (pre_nblk <= 0)
+      hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
+                         (const uint4*)x, M, C, rpb, part);
+    if (pre_nblk > kFoldThreshold) {
+      // too many partial rows for the finalize's per-channel fold: pre-fold into kFoldRows rows
+      // stored after them (the caller sizes part as (pre_nblk + kFoldRows) x 2C)
+      float* folded = part + (size_t)pre_nblk * 2 * C;
+      const int rows_per = (pre_nblk + kFoldRows - 1) / kFoldRows;
+      hipLaunchKernelGGL(k_fold_rows, dim3((2 * C + 255) / 256, kFoldRows), dim3(256), 0, st, part, pre_nblk,
+                         2 * C, rows_per, folded);
+      part = folded;
+      nblk = kFoldRows;
+    }
     hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                        (const bf16_t*)gamma, (const bf16_t*)beta, eps, momentum, run_mean, run_var, mean, rstd, scale,
                        shift);

@@ -34,18 +34,21 @@ class BN(tnn.Module):
         self.running_var.data = self.running_var.data.float()
         return self
 
-    def forward(self, x, residual=None, relu=True):
+    def forward(self, x, residual=None, relu=True, stats=None):
+        if isinstance(x, tuple):                 # (conv output, its fused BN partial sums)
+            x, stats = x
         if self.training and not getattr(self, "_counted_by_model", False):
             self.num_batches_tracked.add_(1)
         return batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                              self.momentum, self.eps, residual, relu)
+                              self.momentum, self.eps, residual, relu, stats)
 
 
 class Conv2d(tnn.Conv2d):
     """torch Conv2d (same parameter name / layout / init) whose forward runs the MFMA implicit GEMM."""
 
-    def forward(self, x):
-        return conv2d_nhwc(x, self.weight, self.stride[0], self.padding[0])
+    def forward(self, x, with_stats: bool = False):
+        """``with_stats`` (the conv feeds a training-mode BN): returns ``(y, stats)``."""
+        return conv2d_nhwc(x, self.weight, self.stride[0], self.padding[0], with_stats)
 
 
 def _conv(cin, cout, k, stride=1, pad=0):
@@ -68,12 +71,13 @@ class BasicBlock(tnn.Module):
             self.downsample = tnn.Sequential(_conv(cin, cout, 1, stride), BN(cout))
 
     def forward(self, x):
+        st = self.training and x.is_cuda
         if self.downsample is not None:
-            idt = self.downsample[1](self.downsample[0](x), relu=False)
+            idt = self.downsample[1](self.downsample[0](x, st), relu=False)
         else:
             idt = x
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), residual=idt, relu=True)
+        out = self.bn1(self.conv1(x, st))
+        return self.bn2(self.conv2(out, st), residual=idt, relu=True)
 
 
 class ResNet(tnn.Module):
@@ -112,7 +116,7 @@ class ResNet(tnn.Module):
     def forward(self, x):
         if self.training:
             self._bn_counters().add_(1)
-        x = self.bn1(self.conv1(x))
+        x = self.bn1(self.conv1(x, self.training and x.is_cuda))
         x = max_pool3s2(x)
         for i in range(1, 5):
             x = getattr(self, f"layer{i}")(x)

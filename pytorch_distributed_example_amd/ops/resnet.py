@@ -21,7 +21,7 @@ from ..parallel.flat import flat_grad_slot
 
 class BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, run_mean, run_var, momentum, eps, relu, training):
+    def forward(ctx, x, gamma, beta, res, run_mean, run_var, momentum, eps, relu, training, stats=None):
         K = kernels()
         C = x.shape[1]
         M = x.numel() // C
@@ -31,7 +31,10 @@ class BatchNormActFn(torch.autograd.Function):
         rstd = torch.empty(C, device=dev, dtype=torch.float32)
         scale = torch.empty(C, device=dev, dtype=torch.float32)
         shift = torch.empty(C, device=dev, dtype=torch.float32)
-        if training:
+        pre_nblk = 0
+        if training and stats is not None:
+            part, pre_nblk = stats                       # partial sums from the conv epilogue
+        elif training:
             part = torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev, dtype=torch.float32)
         else:
             part = torch.empty(0, device=dev, dtype=torch.float32)
@@ -42,7 +45,7 @@ class BatchNormActFn(torch.autograd.Function):
                 mean.copy_(run_mean)
                 rstd.copy_(r)
         K.bn_fwd(x, res, y, gamma, beta, eps, momentum, run_mean if training else None,
-                 run_var if training else None, part, mean, rstd, scale, shift, relu, training)
+                 run_var if training else None, part, mean, rstd, scale, shift, relu, training, pre_nblk)
         ctx.save_for_backward(x, y, gamma, beta, mean, rstd)
         ctx.relu, ctx.has_res = relu, res is not None
         return y
@@ -64,26 +67,36 @@ class BatchNormActFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
         K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, ctx.relu)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
 class Conv2dNHWCFn(torch.autograd.Function):
     """Bias-free conv2d over channels-last bf16 on the implicit-GEMM MFMA kernels."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad):
+    def forward(ctx, x, w, stride, pad, with_stats=False):
+        K = kernels()
         N, C, H, W = x.shape
         O, _, R, S = w.shape
         OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
         y = torch.empty(N, O, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
-        kernels().conv_fprop(x, w, y, None, stride, pad)
+        stats = None
+        if with_stats:
+            nblk = K.conv_stats_blocks(N * OH * OW, O)
+            stats = torch.empty(K.bn_part_rows(nblk) * 2 * O, device=x.device, dtype=torch.float32)
+            ctx.nblk = nblk
+            ctx.mark_non_differentiable(stats)
+            ctx.set_materialize_grads(False)
+        K.conv_fprop(x, w, y, stats, stride, pad)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
-        return y
+        return (y, stats) if with_stats else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dstats=None):
         x, w = ctx.saved_tensors
+        if dy is None:
+            return None, None, None, None, None
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
@@ -98,7 +111,7 @@ class Conv2dNHWCFn(torch.autograd.Function):
             if dw is None or not dw.is_contiguous(memory_format=torch.channels_last):
                 dw = torch.empty_like(w, memory_format=torch.channels_last)
             K.conv_wgrad(dy, x, w, part, splits, dw, ctx.stride, ctx.pad)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def igemm_eligible(x, w, stride: int, pad: int) -> bool:
@@ -108,23 +121,33 @@ def igemm_eligible(x, w, stride: int, pad: int) -> bool:
             and stride in (1, 2) and 0 <= pad < w.shape[2])
 
 
-def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0):
-    """conv2d (no bias) for channels-last bf16 activations: MFMA implicit GEMM where eligible."""
+def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0, with_stats: bool = False):
+    """conv2d (no bias) for channels-last bf16 activations: MFMA implicit GEMM where eligible.
+    ``with_stats``: return ``(y, stats)`` where ``stats`` is ``(partials, nblk)`` -- per-channel
+    (sum, sum of squares) partials of y for a following training-mode BatchNorm -- or None when
+    the library path ran."""
     if igemm_eligible(x, w, stride, pad):
-        return Conv2dNHWCFn.apply(x.contiguous(memory_format=torch.channels_last),
-                                  w.contiguous(memory_format=torch.channels_last), stride, pad)
-    return F.conv2d(x, w, None, stride, pad)
+        out = Conv2dNHWCFn.apply(x.contiguous(memory_format=torch.channels_last),
+                                 w.contiguous(memory_format=torch.channels_last), stride, pad, with_stats)
+        if with_stats:
+            y, part = out
+            return y, (part, kernels().conv_stats_blocks(y.shape[0] * y.shape[2] * y.shape[3], w.shape[0]))
+        return out
+    y = F.conv2d(x, w, None, stride, pad)
+    return (y, None) if with_stats else y
 
 
 def batch_norm_act(x, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,
-                   eps: float = 1e-5, residual=None, relu: bool = True):
+                   eps: float = 1e-5, residual=None, relu: bool = True, stats=None):
+    """``stats``: optional ``(partials, nblk)`` from ``conv2d_nhwc(..., with_stats=True)`` (the batch
+    statistics of ``x`` were summed by the convolution that produced it)."""
     if x.is_cuda:
         if x.dim() == 4 and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
         if residual is not None and residual.dim() == 4:
             residual = residual.contiguous(memory_format=torch.channels_last)
         return BatchNormActFn.apply(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu,
-                                    training)
+                                    training, stats if training else None)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
     if residual is not None:
         y = y + residual

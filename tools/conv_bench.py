@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--stages", type=int, nargs="+", default=[3, 2], help="LDS pipeline depths to time")
     args = ap.parse_args()
     K = kernels()
     dev = "cuda"
@@ -69,9 +70,13 @@ def main():
         wr = w.detach().requires_grad_()
         res = {}
         for rnd in range(2):
-            res["fprop"] = timeit(lambda: K.conv_fprop(x, w, y, None, s, p), args.iters)
-            res["dgrad"] = timeit(lambda: K.conv_dgrad(dy, w, wt, dx, s, p), args.iters)
-            res["wgrad"] = timeit(lambda: K.conv_wgrad(dy, x, w, part, splits, dw, s, p), args.iters)
+            for nst in args.stages:
+                K.conv_set_stages(nst)
+                sfx = "" if nst == args.stages[0] else f"_nst{nst}"
+                res["fprop" + sfx] = timeit(lambda: K.conv_fprop(x, w, y, None, s, p), args.iters)
+                res["dgrad" + sfx] = timeit(lambda: K.conv_dgrad(dy, w, wt, dx, s, p), args.iters)
+                res["wgrad" + sfx] = timeit(lambda: K.conv_wgrad(dy, x, w, part, splits, dw, s, p), args.iters)
+            K.conv_set_stages(args.stages[0])
             res["mi_fprop"] = timeit(lambda: F.conv2d(x, w, None, s, p), args.iters)
             res["mi_dgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
                 dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False]), args.iters)
