@@ -184,4 +184,11 @@ PYBIND11_MODULE(_runtime, m) {
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error);
+  py::class_<CommWatchdog, std::shared_ptr<CommWatchdog>>(m, "CommWatchdog")
+      .def(py::init<std::shared_ptr<RcclComm>, int64_t, int>(), py::arg("comm"), py::arg("timeout_ms"),
+           py::arg("poll_ms") = 20)
+      .def("watch", &CommWatchdog::watch, py::arg("stream"), py::arg("what") = "collective")
+      .def("error", &CommWatchdog::error)
+      .def("pending", &CommWatchdog::pending)
+      .def("stop", &CommWatchdog::stop, py::call_guard<py::gil_scoped_release>());
 }

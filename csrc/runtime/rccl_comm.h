@@ -8,9 +8,15 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 
 namespace pde {
 
@@ -42,9 +48,42 @@ class RcclComm {
 
  private:
   explicit RcclComm(ncclComm_t c, int device);
-  void check_open() const;
-  ncclComm_t comm_ = nullptr;
+  ncclComm_t get() const;
+  std::atomic<ncclComm_t> comm_{nullptr};   // nulled by abort() (possibly from the watchdog thread)
   int rank_ = 0, world_ = 1, device_ = 0;
+};
+
+// Failure detection for GPU collectives ("failure detection"): every collective the
+// Python layer enqueues is followed by `watch(stream)`, which records a private HIP event behind
+// it.  A background thread polls the events; one that is still pending after `timeout_ms` (a peer
+// died or hangs, so the RCCL kernel can never finish) -- or an asynchronous RCCL error -- aborts
+// the communicator (ncclCommAbort unblocks the hung kernels) and latches an error message that the
+// next wait / collective on the group raises.  No-op while the stream is being graph-captured.
+class CommWatchdog {
+ public:
+  CommWatchdog(std::shared_ptr<RcclComm> comm, int64_t timeout_ms, int poll_ms);
+  ~CommWatchdog();
+  void watch(uintptr_t stream, const std::string& what);
+  std::string error();
+  int64_t pending();
+  void stop();
+
+ private:
+  struct Item {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t0;
+    std::string what;
+  };
+  void loop();
+  std::shared_ptr<RcclComm> comm_;
+  int64_t timeout_ms_;
+  int poll_ms_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Item> items_;
+  std::string error_;
+  bool stop_ = false;
+  std::thread th_;
 };
 
 }  // namespace pde

@@ -101,14 +101,17 @@ class GroupMember:
 class Work:
     """Handle of an asynchronous collective (``async_op=True``)."""
 
-    def __init__(self, native=None, event=None, keep=(), post=None):
+    def __init__(self, native=None, event=None, keep=(), post=None, group=None):
         self._native = native
         self._event = event
         self._keep = keep
         self._post = post
+        self._group = group
         self._done = False
 
     def wait(self, timeout=None):
+        if self._group is not None:
+            self._group.check_health()
         if self._done:
             return True
         if self._native is not None:
@@ -133,7 +136,9 @@ class Work:
     def synchronize(self):
         self.wait()
         if self._event is not None:
-            self._event.synchronize()
+            self._event.synchronize()       # returns once the watchdog has aborted a hung collective
+        if self._group is not None:
+            self._group.check_health()
 
 
 class _Completed(Work):
@@ -157,6 +162,17 @@ class ProcessGroup:
         self.device = device
         self._stream = None
         self._lock = threading.Lock()
+        # failure detection: a collective still pending after the group timeout (dead / hung peer)
+        # or an async RCCL error aborts the communicator; the next wait or collective raises
+        self.watchdog = None
+        if rccl is not None and os.environ.get("PDE_RCCL_WATCHDOG", "1") != "0":
+            self.watchdog = runtime().CommWatchdog(rccl, timeout_ms)
+
+    def check_health(self):
+        if self.watchdog is not None:
+            err = self.watchdog.error()
+            if err:
+                raise RuntimeError(err)
 
     # torch-compatible accessors
     def rank(self) -> int:
@@ -188,6 +204,8 @@ class ProcessGroup:
             self.host.shutdown()
         except Exception:
             pass
+        if self.watchdog is not None:
+            self.watchdog.stop()
         if self.rccl is not None:
             try:
                 self.rccl.destroy()
@@ -399,19 +417,22 @@ def _check(t: torch.Tensor):
         raise TypeError(f"unsupported dtype {t.dtype}")
 
 
-def _gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool):
+def _gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool, what: str = "collective"):
     """Run fn(stream_handle) on the group's comm stream, ordered after the caller's stream."""
+    g.check_health()
     cur = torch.cuda.current_stream(g.device)
     cs = g.comm_stream
     cs.wait_stream(cur)
     with torch.cuda.stream(cs):
         fn(cs.cuda_stream)
+    if g.watchdog is not None:
+        g.watchdog.watch(cs.cuda_stream, what)
     for t in tensors:
         t.record_stream(cs)
     ev = torch.cuda.Event()
     ev.record(cs)
     if async_op:
-        return Work(event=ev, keep=tuple(tensors))
+        return Work(event=ev, keep=tuple(tensors), group=g)
     cur.wait_event(ev)
     return None
 
