@@ -58,41 +58,11 @@ __device__ __forceinline__ int toff(int row, int ch) {
 __device__ __forceinline__ bf16x8 row_frag(const char* img, int row, int ch) {
   return *reinterpret_cast<const bf16x8*>(img + toff(row, ch));
 }
-// transposed operand of a 16-row k-step: lane (r = l&31, h = l>>5) gets column col0 + r of rows
-// row0 + {4h..4h+3, 8+4h..8+4h+3}.  EXEC must be full.
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int row0, int col0) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
-  const int ch = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
-  const int r = row0 + 4 * h + q;
-  const s4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(img + toff(r, ch) + 8 * (p & 1)));
-  const s4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(img + toff(r + 8, ch) + 8 * (p & 1)));
-  bf16x8 out;
-  out[0] = v0[0]; out[1] = v0[1]; out[2] = v0[2]; out[3] = v0[3];
-  out[4] = v1[0]; out[5] = v1[1]; out[6] = v1[2]; out[7] = v1[3];
-  return out;
-}
-
-// The same transposed read as inline asm, for loops with LDS-DMA in flight: hipcc puts a blanket
-// `s_waitcnt vmcnt(0)` before every ds_read_b64_tr_b16 builtin there (no memory operand to prove
-// it does not alias the DMA), which drains the prefetched stages.  The asm form is not tracked:
-// the caller waits with `lgkm_fence()` before using the fragments.
+// Transposed reads (ds_read_b64_tr_b16) are issued as inline asm in loops with LDS-DMA in flight:
+// hipcc puts a blanket `s_waitcnt vmcnt(0)` before every ds_read_b64_tr_b16 BUILTIN there (no
+// memory operand to prove it does not alias the DMA), which drains the prefetched stages.  The asm
+// form is not tracked: the caller waits with `lgkm_fence()` before using the fragments.
 typedef __attribute__((address_space(3))) char lds_char;
-__device__ __forceinline__ s4v ds_tr_asm(const char* p) {
-  s4v r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)(lds_char*)p));
-  return r;
-}
-__device__ __forceinline__ bf16x8 tr_frag_asm(const char* img, int row0, int col0) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
-  const int ch = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
-  const int r = row0 + 4 * h + q;
-  const s4v v0 = ds_tr_asm(img + toff(r, ch) + 8 * (p & 1));
-  const s4v v1 = ds_tr_asm(img + toff(r + 8, ch) + 8 * (p & 1));
-  bf16x8 out;
-  out[0] = v0[0]; out[1] = v0[1]; out[2] = v0[2]; out[3] = v0[3];
-  out[4] = v1[0]; out[5] = v1[1]; out[6] = v1[2]; out[7] = v1[3];
-  return out;
-}
 // wait for this wave's outstanding LDS reads; the sched_barrier keeps the MFMAs that consume
 // asm-loaded fragments from being hoisted above the wait (cdna_hip_programming.md §5.4 rule 18)
 __device__ __forceinline__ void lgkm_fence() {
@@ -100,9 +70,52 @@ __device__ __forceinline__ void lgkm_fence() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// p / d for 0 <= p < 2^23 via a float reciprocal and one correction step (no integer division in
+// the K loop: its ~40-instruction expansion per row made wgrad VALU-bound)
+__device__ __forceinline__ int fdiv(int p, int d, float inv) {
+  int q = (int)((float)p * inv);
+  const int r = p - q * d;
+  q += r < 0 ? -1 : (r >= d ? 1 : 0);
+  return q;
+}
+
+// Transposed-read fragment pair at a compile-time offset from two per-wave base addresses (the rows
+// 4h+q and 8+4h+q of a k-step sit in differently swizzled slots, hence two bases): every
+// ds_read_b64_tr_b16 of a wgrad stage is base + immediate (k-step 2048*S, fragment column half 512),
+// so the K loop spends no VALU on LDS addresses.
+template <int OFF>
+__device__ __forceinline__ bf16x8 trpair(uint2 a) {
+  s4v v0, v1;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v0) : "v"(a.x), "n"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a.y), "n"(OFF));
+  bf16x8 out;
+  out[0] = v0[0]; out[1] = v0[1]; out[2] = v0[2]; out[3] = v0[3];
+  out[4] = v1[0]; out[5] = v1[1]; out[6] = v1[2]; out[7] = v1[3];
+  return out;
+}
+// byte offset of fragment column block x (32 columns each) inside a stage's 64-column images
+__host__ __device__ constexpr int colblk_off(int x) { return (x >> 1) * 8192 + (x & 1) * 512; }
+// lane part of the two transposed reads (column 0 of an image, rows 4h+q / 8+4h+q of k-step 0,
+// 8-B half p&1)
+__device__ __forceinline__ uint2 tr_lane_off() {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int ch = 2 * (g & 1) + (p >> 1);
+  return make_uint2(toff(4 * h + q, ch) + 8 * (p & 1), toff(8 + 4 * h + q, ch) + 8 * (p & 1));
+}
+__device__ __forceinline__ uint2 add2(uint2 a, uint32_t b) { return make_uint2(a.x + b, a.y + b); }
+template <int S, int TM, int TN>
+__device__ __forceinline__ void wg_frags(uint2 ab, uint2 bb, bf16x8* fa, bf16x8* fb) {
+  static_assert(TM <= 2 && TN <= 2, "wg_frags: at most 2 x 2 fragments");
+  fa[0] = trpair<2048 * S>(ab);
+  if constexpr (TM > 1) fa[1] = trpair<2048 * S + colblk_off(1)>(ab);
+  fb[0] = trpair<2048 * S>(bb);
+  if constexpr (TN > 1) fb[1] = trpair<2048 * S + colblk_off(1)>(bb);
+}
+
 // ============================================================================ fprop / dgrad
 struct Phase {
   int ph, pw, Hq, Wq, ntap;
+  float inv_hw, inv_w;           // 1 / (Hq * Wq), 1 / Wq for fdiv
   // per tap, packed into one dword so the wave-uniform lookup in the K loop is a scalar load
   // (byte-sized kernarg elements become VECTOR loads, whose vmcnt wait would drain the in-flight
   // LDS-DMA stages): bits 0-7 dh, 8-15 dw (signed), 16-23 weight tap index
@@ -175,20 +188,33 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
 
   // ---- per-thread gather rows: instruction i fills 8-row group 4i + w, this lane row glds_row ----
   const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
-  int pix[AI], hb[AI], wb[AI];
+  // Per row: element offset of its pixel (tap delta 0) + this lane's channel chunk, and a bit per tap
+  // telling whether that tap lies inside the image.  Per stage the tap's offset delta is
+  // wave-uniform (scalar), so a row's load costs one add, a bit test and a select (VALU per MFMA
+  // was the limiter of the first version: 22 vector instructions per MFMA at BM = 256).
+  int aoff[AI];
+  uint32_t vmask[AI];
+  int taps[9];
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) taps[tt] = P.tap[tt];     // wave-uniform, loaded once
 #pragma unroll
   for (int u = 0; u < AI; ++u) {
     const int m = m0 + 8 * (4 * u + w) + lrow;
+    aoff[u] = 0;
+    vmask[u] = 0;
     if (m < Mq) {
-      const int b = m / (P.Hq * P.Wq), r2 = m % (P.Hq * P.Wq);
-      const int hq = r2 / P.Wq, wq = r2 % P.Wq;
-      pix[u] = b * a.IH * a.IW;
-      hb[u] = hq * a.sA;
-      wb[u] = wq * a.sA;
-    } else {
-      pix[u] = 0;
-      hb[u] = -(1 << 20);                             // always out of the image -> zeros
-      wb[u] = 0;
+      const int b = fdiv(m, P.Hq * P.Wq, P.inv_hw), r2 = m - b * (P.Hq * P.Wq);
+      const int hq = fdiv(r2, P.Wq, P.inv_w), wq = r2 - hq * P.Wq;
+      const int hb = hq * a.sA, wb = wq * a.sA;
+      aoff[u] = ((b * a.IH + hb) * a.IW + wb) * a.CA + ch * 8;
+      uint32_t mk = 0;
+#pragma unroll
+      for (int tt = 0; tt < 9; ++tt) {
+        const int tp = taps[tt];
+        const int ih = hb + (int)(signed char)(tp & 0xff), iw = wb + (int)(signed char)((tp >> 8) & 0xff);
+        mk |= (tt < P.ntap && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW) ? (1u << tt) : 0u;
+      }
+      vmask[u] = mk;
     }
   }
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), wr = make_rsrc(a.W, a.w_bytes);
@@ -200,14 +226,13 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
     const int tap = kt / CPT, c0 = (kt - tap * CPT) * 64;
     const int tp = P.tap[tap];
     const int dh = (int)(signed char)(tp & 0xff), dw = (int)(signed char)((tp >> 8) & 0xff), wi = tp >> 16;
+    const int td = (dh * a.IW + dw) * a.CA + c0;     // wave-uniform
     const char* Ai = smem + buf * STAGE;
     const char* Bi = Ai + ABYTES;
 #pragma unroll
     for (int u = 0; u < AI; ++u) {
-      const int ih = hb[u] + dh, iw = wb[u] + dw;
-      const bool ok = (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
-      const uint32_t off = ((uint32_t)((pix[u] + ih * a.IW + iw) * a.CA + c0 + ch * 8)) * 2u;
-      glds16(ar, Ai + (4 * u + w) * 1024, ok ? off : kOOB);
+      const bool ok = (vmask[u] >> tap) & 1u;
+      glds16(ar, Ai + (4 * u + w) * 1024, ok ? (uint32_t)(aoff[u] + td) * 2u : kOOB);
     }
 #pragma unroll
     for (int v = 0; v < BI; ++v) glds16(wr, Bi + (4 * v + w) * 1024, wrow[v] + (uint32_t)(wi * a.CA + c0) * 2u);
@@ -292,8 +317,9 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
     const int c = t + kThreads * u, row = c / CPR, cc = c % CPR;
     const int m = m0 + row;
     if (m < Mq) {
-      const int b = m / (P.Hq * P.Wq), r2 = m % (P.Hq * P.Wq);
-      const int oh = (r2 / P.Wq) * a.sO + P.ph, ow = (r2 % P.Wq) * a.sO + P.pw;
+      const int b = fdiv(m, P.Hq * P.Wq, P.inv_hw), r2 = m - b * (P.Hq * P.Wq);
+      const int hq = fdiv(r2, P.Wq, P.inv_w);
+      const int oh = hq * a.sO + P.ph, ow = (r2 - hq * P.Wq) * a.sO + P.pw;
       const uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
       *reinterpret_cast<uint4*>(a.Y + (((size_t)b * a.OH + oh) * a.OW + ow) * a.NC + n0 + cc * 8) = v;
     }
@@ -331,6 +357,7 @@ struct WgradArgs {
   uint32_t dy_bytes, x_bytes;
   int Bn, IH, IW, C, OH, OW, N, S, stride, pad, T;
   int P, stages_per_split, mtiles, ntiles;
+  float inv_hw, inv_w;
 };
 
 template <int BM, int BN, int NST>
@@ -383,8 +410,8 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
     for (int v = 0; v < BI; ++v) {
       const int q = 4 * v + w, p = p0 + 8 * (q & 7) + lrow;
       const int pp = min(p, a.P - 1);
-      const int b = pp / (a.OH * a.OW), r2 = pp - b * (a.OH * a.OW);
-      const int oh = r2 / a.OW, ow = r2 - oh * a.OW;
+      const int b = fdiv(pp, a.OH * a.OW, a.inv_hw), r2 = pp - b * (a.OH * a.OW);
+      const int oh = fdiv(r2, a.OW, a.inv_w), ow = r2 - oh * a.OW;
       const int ih = oh * a.stride + xr_[v], iw = ow * a.stride + xs_[v];
       const bool ok = p < pend && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
       const uint32_t off = (uint32_t)(((b * a.IH + ih) * a.IW + iw) * a.C + xc_[v]) * 2u;
@@ -393,6 +420,12 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
   };
 
   const int wm = w / WN, wn = w % WN, lr = l & 31;
+  // per-wave transposed-read bases (the fragment column offsets separate: BM/WM, BN/WN are 32 or 64)
+  static_assert((BM / WM) % 64 == 0 || TM == 1, "A column blocks");
+  static_assert((BN / WN) % 64 == 0 || TN == 1, "B column blocks");
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_char*)smem;
+  const uint2 a_lane = add2(tr_lane_off(), colblk_off(wm * (BM / WM) / 32));
+  const uint2 b_lane = add2(tr_lane_off(), colblk_off(wn * (BN / WN) / 32));
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -417,37 +450,25 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
         nb = nb >= NST ? nb - NST : nb;
         issue(kt + NST - 1, nb);
       }
-      const char* Ai = smem + buf * STAGE;
-      const char* Bi = Ai + ABYTES;
       // fragments of k-step s+1 are read while the MFMAs of k-step s run (two named register sets)
+      const uint32_t sb = lds_base + buf * STAGE;
+      const uint2 ab = add2(a_lane, sb), bb = add2(b_lane, sb + ABYTES);
       bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-      auto rd = [&](int s, bf16x8* fa, bf16x8* fb) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int col = wm * (BM / WM) + i * 32;
-          fa[i] = tr_frag_asm(Ai + (col >> 6) * 8192, 16 * s, col & 63);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wn * (BN / WN) + j * 32;
-          fb[j] = tr_frag_asm(Bi + (col >> 6) * 8192, 16 * s, col & 63);
-        }
-      };
       auto mm = [&](const bf16x8* fa, const bf16x8* fb) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
       };
-      rd(0, fa0, fb0);
+      wg_frags<0, TM, TN>(ab, bb, fa0, fb0);
       lgkm_fence();
-      rd(1, fa1, fb1);
+      wg_frags<1, TM, TN>(ab, bb, fa1, fb1);
       mm(fa0, fb0);
       lgkm_fence();
-      rd(2, fa0, fb0);
+      wg_frags<2, TM, TN>(ab, bb, fa0, fb0);
       mm(fa1, fb1);
       lgkm_fence();
-      rd(3, fa1, fb1);
+      wg_frags<3, TM, TN>(ab, bb, fa1, fb1);
       mm(fa0, fb0);
       lgkm_fence();
       mm(fa1, fb1);
@@ -527,6 +548,8 @@ hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, i
   a.sA = stride; a.sO = 1; a.nphase = 1;
   Phase& P = a.phase[0];
   P.ph = P.pw = 0; P.Hq = OH; P.Wq = OW; P.ntap = R * S;
+  P.inv_hw = 1.0f / (float)(OH * OW);
+  P.inv_w = 1.0f / (float)OW;
   for (int r = 0; r < R; ++r)
     for (int s = 0; s < S; ++s) {
       const int k = r * S + s;
@@ -560,6 +583,8 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int 
     P.ph = z / stride; P.pw = z % stride;
     P.Hq = (H - P.ph + stride - 1) / stride;
     P.Wq = (W - P.pw + stride - 1) / stride;
+    P.inv_hw = 1.0f / (float)(P.Hq * P.Wq);
+    P.inv_w = 1.0f / (float)P.Wq;
     P.ntap = 0;
     for (int r = 0; r < R; ++r) {
       const int nh = P.ph + pad - r;
@@ -601,6 +626,8 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   a.Bn = Bn; a.IH = H; a.IW = W; a.C = C; a.OH = OH; a.OW = OW; a.N = N; a.S = S;
   a.stride = stride; a.pad = pad; a.T = R * S;
   a.P = Bn * OH * OW;
+  a.inv_hw = 1.0f / (float)(OH * OW);
+  a.inv_w = 1.0f / (float)OW;
   const int stages = (a.P + 63) / 64;
   a.stages_per_split = (stages + splits - 1) / splits;
   const int TC = a.T * C;
