@@ -44,6 +44,16 @@ void ln_bwd(const at::Tensor& dY, const at::Tensor& X, const at::Tensor& mean, c
             "ln_bwd");
 }
 
+// out (bf16, contiguous) = sum of the S fp32 slabs of part ([S, *out.shape]) -- split-K reduction
+void sum_slabs_bf16(const at::Tensor& part, const at::Tensor& out) {
+  const int64_t n = out.numel();
+  check_cuda(out, "out", BF16);
+  check_cuda(part, "part", F32);
+  TORCH_CHECK(n % 4 == 0 && part.numel() % n == 0, "sum_slabs_bf16: part must hold S x out.numel() floats");
+  hip_check(pde_sum_slabs_bf16(ptr<float>(part), (int)(part.numel() / n), n, out.data_ptr(), cur_stream()),
+            "sum_slabs_bf16");
+}
+
 void gelu_fwd(const at::Tensor& X, const at::Tensor& Y) {
   check_cuda(X, "X", BF16);
   check_cuda(Y, "Y", BF16, X.numel());
@@ -199,6 +209,7 @@ void register_transformer(pybind11::module& m) {
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd_blocks", &ln_bwd_blocks);
   m.def("ln_bwd", &ln_bwd);
+  m.def("sum_slabs_bf16", &sum_slabs_bf16);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_bf16", &xent_bf16);

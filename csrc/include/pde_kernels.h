@@ -99,6 +99,7 @@ hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStre
 hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int H, int W, int C, int N, int R, int S,
                           int stride, int pad, int OH, int OW, hipStream_t st);
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C);
+hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hipStream_t st);
 hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,
                           int C, int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
 

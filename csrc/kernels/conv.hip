@@ -613,6 +613,14 @@ int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C) {
   return max(1, splits);
 }
 
+// out (bf16) = sum over S fp32 slabs [S][n] (split-K partial products), n % 4 == 0
+hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hipStream_t st) {
+  if (n % 4 || S < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n,
+                     (bf16_t*)out);
+  return hipGetLastError();
+}
+
 // part: fp32 [splits][N][T*C] scratch; dw: bf16 [N][T*C]
 hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,
                           int C, int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st) {

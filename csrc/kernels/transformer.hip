@@ -490,18 +490,25 @@ __global__ __launch_bounds__(256) void k_colsum_bf16_part(const uint4* __restric
   }
 }
 
+// 64 columns per block; the 4 waves stride over the RS partial rows with 4 independent
+// accumulators each (a single thread walking all RS rows was a 64-deep dependent-load chain).
 __global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__ part, int RS, int C,
                                                        bf16_t* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s0 = 0.f, s1 = 0.f;
-  int k = 0;
-  for (; k + 1 < RS; k += 2) {
+  __shared__ float sh[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = min(blockIdx.x * 64 + lane, C - 1);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = w;
+  for (; k + 12 < RS; k += 16) {
     s0 += part[(size_t)k * C + c];
-    s1 += part[(size_t)(k + 1) * C + c];
+    s1 += part[(size_t)(k + 4) * C + c];
+    s2 += part[(size_t)(k + 8) * C + c];
+    s3 += part[(size_t)(k + 12) * C + c];
   }
-  if (k < RS) s0 += part[(size_t)k * C + c];
-  out[c] = f2bf(s0 + s1);
+  for (; k < RS; k += 4) s0 += part[(size_t)k * C + c];
+  sh[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && blockIdx.x * 64 + lane < C) out[c] = f2bf(sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]);
 }
 
 // out[0] = sum(x[0..n)) (one 1024-thread block; n up to a few 1e5 -- loss rows)
@@ -637,7 +644,7 @@ hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, 
   if (C % 8) return hipErrorInvalidValue;
   const int rs = pde_colsum_bf16_splits(C);
   hipLaunchKernelGGL(k_colsum_bf16_part, dim3((C + 255) / 256, rs), dim3(256), 0, st, (const uint4*)x, N, C, part);
-  hipLaunchKernelGGL(k_colsum_finish, dim3((C + 255) / 256), dim3(256), 0, st, part, rs, C, (bf16_t*)out);
+  hipLaunchKernelGGL(k_colsum_finish, dim3((C + 63) / 64), dim3(256), 0, st, part, rs, C, (bf16_t*)out);
   return hipGetLastError();
 }
 

@@ -83,8 +83,11 @@ class Block(tnn.Module):
         self.mlp = _MLP(cfg)
 
     def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        return x + self.mlp(self.ln_2(x))
+        # (residual, LN(x)) from one op: the residual-gradient add is fused into the LN backward
+        x, h = T.layer_norm_residual(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+        x = x + self.attn(h)
+        x, h = T.layer_norm_residual(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
+        return x + self.mlp(h)
 
 
 class _Transformer(tnn.Module):

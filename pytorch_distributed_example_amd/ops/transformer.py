@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .._ext import kernels
+from ..parallel.flat import flat_grad_slot
 
 _BF16 = torch.bfloat16
 
@@ -51,7 +52,8 @@ class LayerNormFn(torch.autograd.Function):
         K = kernels()
         dx = torch.empty_like(x)
         part = torch.empty(K.ln_bwd_blocks(N) * 2 * C, device=x.device, dtype=torch.float32)
-        dw = torch.empty(C, device=x.device, dtype=w.dtype)
+        dw = flat_grad_slot(w)
+        dw = torch.empty(C, device=x.device, dtype=w.dtype) if dw is None else dw
         db = torch.empty(C, device=x.device, dtype=w.dtype)
         K.ln_bwd(_c(dy), x, mean, rstd, w, None, dx, part, dw, db, False)
         return dx, dw, db, None
@@ -61,6 +63,48 @@ def layer_norm(x, weight, bias, eps: float = 1e-5):
     if _gpu(x):
         return LayerNormFn.apply(x, weight, bias, eps)
     return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+
+
+class LayerNormResFn(torch.autograd.Function):
+    """(x, LayerNorm(x)) for a pre-LN residual block ``x + f(LN(x))``: x goes on as the residual, so
+    its gradient is dres + LN_bwd(dy) -- computed by ONE backward kernel (dRes fused) instead of the
+    LN backward plus autograd's separate accumulation add of the two gradient paths."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xc = _c(x)
+        C = xc.shape[-1]
+        N = xc.numel() // C
+        y = torch.empty_like(xc)
+        mean = torch.empty(N, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(N, device=x.device, dtype=torch.float32)
+        kernels().ln_fwd(xc, w, b, y, mean, rstd, eps)
+        ctx.save_for_backward(xc, w, b, mean, rstd)
+        return xc.view_as(xc), y
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        x, w, b, mean, rstd = ctx.saved_tensors
+        C = x.shape[-1]
+        N = x.numel() // C
+        K = kernels()
+        dx = torch.empty_like(x)
+        part = torch.empty(K.ln_bwd_blocks(N) * 2 * C, device=x.device, dtype=torch.float32)
+        dw = flat_grad_slot(w)
+        dw = torch.empty(C, device=x.device, dtype=w.dtype) if dw is None else dw
+        db = flat_grad_slot(b)
+        db = torch.empty(C, device=x.device, dtype=w.dtype) if db is None else db
+        if dy is None:
+            dy = torch.zeros_like(x)
+        K.ln_bwd(_c(dy), x, mean, rstd, w, None if dres is None else _c(dres), dx, part, dw, db, False)
+        return dx, dw, db, None
+
+
+def layer_norm_residual(x, weight, bias, eps: float = 1e-5):
+    """Returns ``(x, layer_norm(x))``; use the first output as the residual stream."""
+    if _gpu(x):
+        return LayerNormResFn.apply(x, weight, bias, eps)
+    return x, F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
 
 
 # --------------------------------------------------------------------------------------- GELU
@@ -233,14 +277,20 @@ def _splitk(N: int, out: int, fin: int) -> int:
     return S
 
 
-def _wgrad(dy2, x2):
+def _wgrad(dy2, x2, dst=None):
+    """dW = dy2^T x2 (into ``dst`` -- the weight's flat gradient slot -- when given).  Split-K
+    partials are fp32 (``bmm(..., out_dtype=float32)``) and summed by one HIP pass straight into the
+    bf16 result (no bf16 rounding of partial sums, no extra reduction kernel)."""
     N, out = dy2.shape
     fin = x2.shape[1]
     S = _splitk(N, out, fin)
+    if dst is None:
+        dst = torch.empty(out, fin, device=dy2.device, dtype=dy2.dtype)
     if S == 1:
-        return torch.matmul(dy2.t(), x2)
-    part = torch.bmm(dy2.view(S, N // S, out).transpose(1, 2), x2.view(S, N // S, fin))
-    return part.sum(0)
+        return torch.matmul(dy2.t(), x2, out=dst)
+    part = torch.bmm(dy2.view(S, N // S, out).transpose(1, 2), x2.view(S, N // S, fin), out_dtype=torch.float32)
+    kernels().sum_slabs_bf16(part, dst)
+    return dst
 
 
 class LinearFn(torch.autograd.Function):
@@ -251,6 +301,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.bias = b
         return F.linear(x, w, b)
 
     @staticmethod
@@ -263,11 +314,13 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(dy2, w).view(x.shape)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy2, x2)
+            slot = flat_grad_slot(w)
+            dw = _wgrad(dy2, x2, slot if slot is not None and slot.is_contiguous() else None)
         if ctx.has_b and ctx.needs_input_grad[2]:
             K = kernels()
             part = torch.empty(K.colsum_bf16_splits(out) * out, device=dy.device, dtype=torch.float32)
-            db = torch.empty(out, device=dy.device, dtype=dy.dtype)
+            db = flat_grad_slot(ctx.bias)
+            db = torch.empty(out, device=dy.device, dtype=dy.dtype) if db is None else db
             K.colsum_bf16(dy2, part, db)
         return dx, dw, db
 

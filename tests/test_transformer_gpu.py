@@ -213,3 +213,22 @@ def test_linear_splitk_and_bias_grad(N, fin, fout):
     assert rel_err(x.grad, xr.grad) < 2e-2
     assert rel_err(w.grad, wr.grad) < 2e-2
     assert rel_err(b.grad, br.grad) < 2e-2
+
+
+def test_layer_norm_residual_fused_grad():
+    """(x, LN(x)) with the residual gradient folded into the LN backward kernel vs fp32 autograd."""
+    from pytorch_distributed_example_amd.ops.transformer import layer_norm_residual
+    torch.manual_seed(21)
+    x = torch.randn(96, 384).to("cuda", torch.bfloat16).requires_grad_()
+    w = (1 + 0.1 * torch.randn(384)).to("cuda", torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(384)).to("cuda", torch.bfloat16).requires_grad_()
+    g1 = torch.randn(96, 384, device="cuda")
+    g2 = torch.randn(96, 384, device="cuda")
+    xr, y = layer_norm_residual(x, w, b)
+    ((xr.float() * g1).sum() + (y.float() * g2).sum()).backward()
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yf = torch.nn.functional.layer_norm(xf, (384,), wf, bf, 1e-5)
+    ((xf * g1).sum() + (yf * g2).sum()).backward()
+    for a, r in ((x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
+        err = ((a.float() - r).abs().max() / r.abs().max()).item()
+        assert err < 2e-2, err
