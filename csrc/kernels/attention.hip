@@ -19,28 +19,34 @@
 // row-major, XOR-swizzled image (cdna_hip_programming.md T10 layout (a), 8 KB): the row-operand
 // fragments are ds_read_b128 row reads and the transposed operands (V^T, K^T, dO^T, Q^T) are
 // ds_read_b64_tr_b16 hardware-transposed reads of the same image -- conflict-free for both (checked
-// with the bank model of §2).  Tiles are double-buffered: global loads of tile t+1 are issued before
-// the MFMA work on tile t and written to the other buffer after it; one barrier per tile.
+// with the bank model of §2).  Tiles are staged by LDS-DMA (buffer_load ... lds, pde_lds.h) into a
+// ring of NST stage buffers, NST-1 tiles in flight ahead of the MFMAs: per tile a counted vmcnt
+// wait, one raw s_barrier, the next issue, then compute.  (The first version staged through
+// registers; hipcc placed the staging registers in scratch and waited vmcnt(0) after every load,
+// leaving the waves parked 65% of their cycles.)  Transposed reads are inline asm with immediate
+// offsets (the builtin makes hipcc drain the DMA queue before each one).  exp2 is the bare
+// v_exp_f32 (inputs <= 0; no denormal fix-up), and the O rescale is skipped when no query's
+// running max grew (cdna_hip_programming.md T13 with threshold 0: exact).
 #include "pde_hip.h"
 #include "pde_bf16.h"
 #include "pde_kernels.h"
+#include "pde_lds.h"
 
 namespace {
 
+using namespace pde_lds;
+
 constexpr int HD = 64;        // head dim
 constexpr int TILE = 8192;    // bytes of one 64 x 64 bf16 tile image
+constexpr int NST = 4;        // LDS stage ring depth
 
-typedef short s4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s4v lds_s4v;
-
-__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
-
-// byte offset of 16-byte chunk `ch` (0..7) of row `row` (0..63) in a tile image
-__device__ __forceinline__ int toff(int row, int ch) {
-  return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// max of three with no NaN canonicalisation (fmaxf on MFMA results costs a v_max x,x per operand)
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
 // accumulator regs 8s..8s+7 -> bf16 fragment
@@ -51,41 +57,28 @@ __device__ __forceinline__ bf16x8 frag_of(const f32x16& a) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
-// row operand: row `row` of the tile, dims 8*ch .. 8*ch+7
-__device__ __forceinline__ bf16x8 row_frag(const char* tile, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(tile + toff(row, ch));
-}
-
-// transposed operand: lane (r, h) gets column col0 + r of rows row0 + {4h..4h+3, 8+4h..8+4h+3}
-// (= the permuted K order of a 32x32x16 k-step), via two ds_read_b64_tr_b16.  EXEC must be full.
-__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int row0, int col0) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
-  const int ch = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
-  const int r = row0 + 4 * h + q;
-  const char* a0 = tile + toff(r, ch) + 8 * (p & 1);
-  const char* a1 = tile + toff(r + 8, ch) + 8 * (p & 1);
-  const s4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)a0);
-  const s4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)a1);
-  bf16x8 out;
-  out[0] = v0[0]; out[1] = v0[1]; out[2] = v0[2]; out[3] = v0[3];
-  out[4] = v1[0]; out[5] = v1[1]; out[6] = v1[2]; out[7] = v1[3];
-  return out;
-}
-
-// 64 rows x 64 dims starting at `row0` of a [*, ld] matrix: 512 16-byte chunks, two per thread
-__device__ __forceinline__ void tile_load(const bf16_t* src, size_t ld, int row0, uint4* reg) {
+// LDS-DMA of the 64-row tile starting at row0 of a [T][ld] bf16 matrix (resource r) into img:
+// wave w fills the 8-row groups w and w + 4 (two wave-instructions).
+__device__ __forceinline__ void issue_tile(rsrc_t r, int ld, int row0, const char* img, int w, int lrow, int lch) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = threadIdx.x + 256 * u;
-    reg[u] = *reinterpret_cast<const uint4*>(src + (size_t)(row0 + (c >> 3)) * ld + (c & 7) * 8);
+  for (int gg = 0; gg < 2; ++gg) {
+    const int g = w + 4 * gg;
+    glds16(r, img + g * 1024, (uint32_t)(((row0 + 8 * g + lrow) * ld + lch * 8) * 2));
   }
 }
-__device__ __forceinline__ void tile_store(char* tile, const uint4* reg) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = threadIdx.x + 256 * u;
-    *reinterpret_cast<uint4*>(tile + toff(c >> 3, c & 7)) = reg[u];
-  }
+
+// wait until at most `ahead` younger stages (of PER glds per wave) are in flight
+template <int PER>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  if (ahead >= 2) wait_vm<2 * PER>();
+  else if (ahead == 1) wait_vm<PER>();
+  else wait_vm<0>();
+}
+
+// V^T / K^T / dO^T / Q^T fragment of k-step S, dims half C (0/1) from a transposed-read base
+template <int S, int C>
+__device__ __forceinline__ bf16x8 tfrag(uint2 base) {
+  return trpair<2048 * S + colblk_off(C)>(base);
 }
 
 // write a [dim x query] accumulator pair (dims 0..31 / 32..63) of one lane's query as 8-byte rows
@@ -105,36 +98,40 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
                                                      const bf16_t* __restrict__ V, int ldq, bf16_t* __restrict__ O,
                                                      int ldo, float* __restrict__ LSE, int T, int H, float sl2,
                                                      float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[4 * TILE];  // K[2] | V[2]
+  __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const int qt = gridDim.x - 1 - blockIdx.x;  // longest (most keys) tiles first
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
-  const bf16_t* Kb = K + boff;
-  const bf16_t* Vb = V + boff;
+  const uint32_t tbytes = (uint32_t)T * ldq * 2;
+  const rsrc_t kr = make_rsrc(K + boff, tbytes), vr = make_rsrc(V + boff, tbytes);
+  const int lrow = glds_row(lane), lch = glds_chunk(lane, w & 1);
   const int q0 = qt * 128 + w * 32, myq = q0 + r;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = ld16(Q + boff + (size_t)myq * ldq + 16 * s + 8 * h);
-  f32x16 o0 = {}, o1 = {};
-  float m = -INFINITY, l = 0.f;
   const int nkt = (qt * 128 + 127) / 64 + 1;
   const int last_kt = (q0 + 31) / 64;
-  uint4 kr[2], vr[2];
-  tile_load(Kb, ldq, 0, kr);
-  tile_load(Vb, ldq, 0, vr);
-  tile_store(lds, kr);
-  tile_store(lds + 2 * TILE, vr);
-  __syncthreads();
+  auto issue = [&](int kt) {
+    const char* st = lds + (kt % NST) * 2 * TILE;
+    issue_tile(kr, ldq, kt * 64, st, w, lrow, lch);
+    issue_tile(vr, ldq, kt * 64, st + TILE, w, lrow, lch);
+  };
+  bf16x8 qf[4];                        // issued before the DMA prologue: waiting for them later
+#pragma unroll                          // does not drain the prefetched stages (in-order vmcnt)
+  for (int s = 0; s < 4; ++s) qf[s] = ld16(Q + boff + (size_t)myq * ldq + 16 * s + 8 * h);
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nkt) issue(s);
+  const uint2 tl = tr_lane_off();
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
+  f32x16 o0 = {}, o1 = {};
+  float m = -INFINITY, l = 0.f;
   for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + 1 < nkt;
-    if (more) {
-      tile_load(Kb, ldq, (kt + 1) * 64, kr);
-      tile_load(Vb, ldq, (kt + 1) * 64, vr);
-    }
+    wait_stages<4>(min(NST - 2, nkt - 1 - kt));
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nkt) issue(kt + NST - 1);
     if (kt <= last_kt) {
-      const char* Ks = lds + (kt & 1) * TILE;
-      const char* Vs = lds + 2 * TILE + (kt & 1) * TILE;
+      const int sb = kt % NST;
+      const char* Ks = lds + sb * 2 * TILE;
+      const uint2 vb = add2(tl, lds0 + sb * 2 * TILE + TILE);
       const int k0 = kt * 64;
       f32x16 s0 = {}, s1 = {};
 #pragma unroll
@@ -142,6 +139,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
         s0 = mfma_bf16(row_frag(Ks, r, 2 * s + h), qf[s], s0);
         s1 = mfma_bf16(row_frag(Ks, 32 + r, 2 * s + h), qf[s], s1);
       }
+      // V^T fragments in flight while the softmax runs
+      const bf16x8 v00 = tfrag<0, 0>(vb), v01 = tfrag<0, 1>(vb), v10 = tfrag<1, 0>(vb), v11 = tfrag<1, 1>(vb);
+      const bf16x8 v20 = tfrag<2, 0>(vb), v21 = tfrag<2, 1>(vb), v30 = tfrag<3, 0>(vb), v31 = tfrag<3, 1>(vb);
       if (k0 + 63 > q0) {  // tile crosses the diagonal of this wave
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -152,40 +152,39 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+      for (int i = 0; i < 16; ++i) mx = max3(mx, s0[i], s1[i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
-      const float alpha = exp2f((m - mn) * sl2);
-      const float mb = mn * sl2;
+      if (__any(mn > m)) {                 // some query's running max grew: rescale O and l
+        const float alpha = fexp2((m - mn) * sl2);
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o0[i] *= alpha;
+          o1[i] *= alpha;
+        }
+        m = mn;
+      }
+      const float mb = m * sl2;
       float ls = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        s0[i] = exp2f(s0[i] * sl2 - mb);
-        s1[i] = exp2f(s1[i] * sl2 - mb);
+        s0[i] = fexp2(s0[i] * sl2 - mb);
+        s1[i] = fexp2(s1[i] * sl2 - mb);
         ls += s0[i] + s1[i];
       }
-      l = l * alpha + ls;
-      m = mn;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o0[i] *= alpha;
-        o1[i] *= alpha;
-      }
+      l += ls;
       const bf16x8 p0 = frag_of<0>(s0), p1 = frag_of<1>(s0), p2 = frag_of<0>(s1), p3 = frag_of<1>(s1);
-      o0 = mfma_bf16(tr_frag(Vs, 0, 0), p0, o0);
-      o1 = mfma_bf16(tr_frag(Vs, 0, 32), p0, o1);
-      o0 = mfma_bf16(tr_frag(Vs, 16, 0), p1, o0);
-      o1 = mfma_bf16(tr_frag(Vs, 16, 32), p1, o1);
-      o0 = mfma_bf16(tr_frag(Vs, 32, 0), p2, o0);
-      o1 = mfma_bf16(tr_frag(Vs, 32, 32), p2, o1);
-      o0 = mfma_bf16(tr_frag(Vs, 48, 0), p3, o0);
-      o1 = mfma_bf16(tr_frag(Vs, 48, 32), p3, o1);
+      lgkm_fence();
+      o0 = mfma_bf16(v00, p0, o0);
+      o1 = mfma_bf16(v01, p0, o1);
+      o0 = mfma_bf16(v10, p1, o0);
+      o1 = mfma_bf16(v11, p1, o1);
+      o0 = mfma_bf16(v20, p2, o0);
+      o1 = mfma_bf16(v21, p2, o1);
+      o0 = mfma_bf16(v30, p3, o0);
+      o1 = mfma_bf16(v31, p3, o1);
     }
-    if (more) {
-      tile_store(lds + ((kt + 1) & 1) * TILE, kr);
-      tile_store(lds + 2 * TILE + ((kt + 1) & 1) * TILE, vr);
-    }
-    __syncthreads();
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   store_dimrows(O + (size_t)b * T * ldo + (size_t)myq * ldo + hh * HD, o0, o1, 1.f / lt, h);
@@ -222,15 +221,23 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
                                                         const float* __restrict__ LSE, const float* __restrict__ Dd,
                                                         bf16_t* __restrict__ dQ, int T, int H, float sl2,
                                                         float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[4 * TILE];  // K[2] | V[2]
+  __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const int qt = gridDim.x - 1 - blockIdx.x;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
-  const bf16_t* Kb = K + boff;
-  const bf16_t* Vb = V + boff;
+  const uint32_t tbytes = (uint32_t)T * ldq * 2;
+  const rsrc_t kr = make_rsrc(K + boff, tbytes), vr = make_rsrc(V + boff, tbytes);
+  const int lrow = glds_row(lane), lch = glds_chunk(lane, w & 1);
   const bf16_t* dOb = dO + (size_t)b * T * ldo + hh * HD;
   const int q0 = qt * 128 + w * 32, myq = q0 + r;
+  const int nkt = (qt * 128 + 127) / 64 + 1;
+  const int last_kt = (q0 + 31) / 64;
+  auto issue = [&](int kt) {
+    const char* st = lds + (kt % NST) * 2 * TILE;
+    issue_tile(kr, ldq, kt * 64, st, w, lrow, lch);
+    issue_tile(vr, ldq, kt * 64, st + TILE, w, lrow, lch);
+  };
   bf16x8 qf[4], gf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -239,24 +246,21 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
   }
   const float lse2 = LSE[(size_t)bh * T + myq] * 1.4426950408889634f;
   const float dq_d = Dd[(size_t)bh * T + myq];
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nkt) issue(s);
+  const uint2 tl = tr_lane_off();
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
   f32x16 a0 = {}, a1 = {};
-  const int nkt = (qt * 128 + 127) / 64 + 1;
-  const int last_kt = (q0 + 31) / 64;
-  uint4 kr[2], vr[2];
-  tile_load(Kb, ldq, 0, kr);
-  tile_load(Vb, ldq, 0, vr);
-  tile_store(lds, kr);
-  tile_store(lds + 2 * TILE, vr);
-  __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + 1 < nkt;
-    if (more) {
-      tile_load(Kb, ldq, (kt + 1) * 64, kr);
-      tile_load(Vb, ldq, (kt + 1) * 64, vr);
-    }
+    wait_stages<4>(min(NST - 2, nkt - 1 - kt));
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nkt) issue(kt + NST - 1);
     if (kt <= last_kt) {
-      const char* Ks = lds + (kt & 1) * TILE;
-      const char* Vs = lds + 2 * TILE + (kt & 1) * TILE;
+      const int sb = kt % NST;
+      const char* Ks = lds + sb * 2 * TILE;
+      const char* Vs = Ks + TILE;
+      const uint2 kb = add2(tl, lds0 + sb * 2 * TILE);
       const int k0 = kt * 64;
       f32x16 s0 = {}, s1 = {}, d0 = {}, d1 = {};
 #pragma unroll
@@ -266,35 +270,39 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
         d0 = mfma_bf16(row_frag(Vs, r, 2 * s + h), gf[s], d0);
         d1 = mfma_bf16(row_frag(Vs, 32 + r, 2 * s + h), gf[s], d1);
       }
+      const bf16x8 k00 = tfrag<0, 0>(kb), k01 = tfrag<0, 1>(kb), k10 = tfrag<1, 0>(kb), k11 = tfrag<1, 1>(kb);
+      const bf16x8 k20 = tfrag<2, 0>(kb), k21 = tfrag<2, 1>(kb), k30 = tfrag<3, 0>(kb), k31 = tfrag<3, 1>(kb);
+      const bool diag = k0 + 63 > q0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float p0 = key > myq ? 0.f : exp2f(s0[i] * sl2 - lse2);
-        const float p1 = key + 32 > myq ? 0.f : exp2f(s1[i] * sl2 - lse2);
+        float p0 = fexp2(s0[i] * sl2 - lse2);
+        float p1 = fexp2(s1[i] * sl2 - lse2);
+        if (diag) {
+          p0 = key > myq ? 0.f : p0;
+          p1 = key + 32 > myq ? 0.f : p1;
+        }
         s0[i] = p0 * (d0[i] - dq_d);
         s1[i] = p1 * (d1[i] - dq_d);
       }
       const bf16x8 p0 = frag_of<0>(s0), p1 = frag_of<1>(s0), p2 = frag_of<0>(s1), p3 = frag_of<1>(s1);
-      a0 = mfma_bf16(tr_frag(Ks, 0, 0), p0, a0);
-      a1 = mfma_bf16(tr_frag(Ks, 0, 32), p0, a1);
-      a0 = mfma_bf16(tr_frag(Ks, 16, 0), p1, a0);
-      a1 = mfma_bf16(tr_frag(Ks, 16, 32), p1, a1);
-      a0 = mfma_bf16(tr_frag(Ks, 32, 0), p2, a0);
-      a1 = mfma_bf16(tr_frag(Ks, 32, 32), p2, a1);
-      a0 = mfma_bf16(tr_frag(Ks, 48, 0), p3, a0);
-      a1 = mfma_bf16(tr_frag(Ks, 48, 32), p3, a1);
+      lgkm_fence();
+      a0 = mfma_bf16(k00, p0, a0);
+      a1 = mfma_bf16(k01, p0, a1);
+      a0 = mfma_bf16(k10, p1, a0);
+      a1 = mfma_bf16(k11, p1, a1);
+      a0 = mfma_bf16(k20, p2, a0);
+      a1 = mfma_bf16(k21, p2, a1);
+      a0 = mfma_bf16(k30, p3, a0);
+      a1 = mfma_bf16(k31, p3, a1);
     }
-    if (more) {
-      tile_store(lds + ((kt + 1) & 1) * TILE, kr);
-      tile_store(lds + 2 * TILE + ((kt + 1) & 1) * TILE, vr);
-    }
-    __syncthreads();
   }
   store_dimrows(dQ + boff + (size_t)myq * ldq, a0, a1, scale, h);
 }
 
 // dK, dV: grid (T/128, B*H); wave w owns keys kb*128 + 32w + (0..31); loops over 64-query tiles
-// with Q / dO (+ lse, D) staged in LDS (rows for S / dP, transposed reads for dK / dV).
+// with Q / dO / LSE / D staged in LDS (rows for S / dP, transposed reads for dK / dV).
+constexpr int kDkdvStage = 2 * TILE + 512;           // Q | dO | LSE[64] | D[64]
 __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, int ldq,
                                                           const bf16_t* __restrict__ dO, int ldo,
@@ -302,48 +310,50 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
                                                           const float* __restrict__ Dd, bf16_t* __restrict__ dK,
                                                           bf16_t* __restrict__ dV, int T, int H, float sl2,
                                                           float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[4 * TILE];  // Q[2] | dO[2]
-  __shared__ __attribute__((aligned(16))) float Ls[2][64], Ds[2][64];
+  __shared__ __attribute__((aligned(16))) char lds[NST * kDkdvStage];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const int kb = blockIdx.x;  // tile 0 has the most queries: natural order is heavy-first
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
-  const bf16_t* Qb = Q + boff;
-  const bf16_t* dOb = dO + (size_t)b * T * ldo + hh * HD;
-  const float* Lb = LSE + (size_t)bh * T;
-  const float* Db = Dd + (size_t)bh * T;
+  const rsrc_t qr = make_rsrc(Q + boff, (uint32_t)T * ldq * 2);
+  const rsrc_t gr = make_rsrc(dO + (size_t)b * T * ldo + hh * HD, (uint32_t)T * ldo * 2);
+  // wave w & 1 == 0 stages LSE, == 1 stages D (two waves write each: identical bytes)
+  const rsrc_t vecr = make_rsrc((w & 1) ? Dd + (size_t)bh * T : LSE + (size_t)bh * T, (uint32_t)T * 4);
+  const int lrow = glds_row(lane), lch = glds_chunk(lane, w & 1);
   const int k0 = kb * 128 + w * 32, myk = k0 + r;
+  const int qt0 = (kb * 128) / 64, nqt = T / 64;
+  auto issue = [&](int qt) {
+    const char* st = lds + ((qt - qt0) % NST) * kDkdvStage;
+    issue_tile(qr, ldq, qt * 64, st, w, lrow, lch);
+    issue_tile(gr, ldo, qt * 64, st + TILE, w, lrow, lch);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vecr, (__attribute__((address_space(3))) void*)(st + 2 * TILE +
+                                                                                              256 * (w & 1)),
+                                             4, (uint32_t)(qt * 64 + lane) * 4, 0, 0, 0);
+  };
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     kf[s] = ld16(K + boff + (size_t)myk * ldq + 16 * s + 8 * h);
     vf[s] = ld16(V + boff + (size_t)myk * ldq + 16 * s + 8 * h);
   }
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (qt0 + s < nqt) issue(qt0 + s);
+  const uint2 tl = tr_lane_off();
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
   f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
-  const int qt0 = (kb * 128) / 64, nqt = T / 64;
-  const int tid = threadIdx.x;
-  uint4 qr[2], gr[2];
-  float lsv = 0.f;
-  tile_load(Qb, ldq, qt0 * 64, qr);
-  tile_load(dOb, ldo, qt0 * 64, gr);
-  lsv = tid < 64 ? Lb[qt0 * 64 + tid] : (tid < 128 ? Db[qt0 * 64 + tid - 64] : 0.f);
-  tile_store(lds, qr);
-  tile_store(lds + 2 * TILE, gr);
-  if (tid < 64) Ls[0][tid] = lsv * 1.4426950408889634f;
-  else if (tid < 128) Ds[0][tid - 64] = lsv;
-  __syncthreads();
   for (int qt = qt0; qt < nqt; ++qt) {
-    const int buf = (qt - qt0) & 1;
-    const bool more = qt + 1 < nqt;
-    if (more) {
-      tile_load(Qb, ldq, (qt + 1) * 64, qr);
-      tile_load(dOb, ldo, (qt + 1) * 64, gr);
-      lsv = tid < 64 ? Lb[(qt + 1) * 64 + tid] : (tid < 128 ? Db[(qt + 1) * 64 + tid - 64] : 0.f);
-    }
+    wait_stages<5>(min(NST - 2, nqt - 1 - qt));
+    __builtin_amdgcn_s_barrier();
+    if (qt + NST - 1 < nqt) issue(qt + NST - 1);
     const int qbase = qt * 64;
     if (k0 <= qbase + 63) {  // some query of this tile sees some key of this wave
-      const char* Qs = lds + buf * TILE;
-      const char* Gs = lds + 2 * TILE + buf * TILE;
+      const int sb = (qt - qt0) % NST;
+      const char* Qs = lds + sb * kDkdvStage;
+      const char* Gs = Qs + TILE;
+      const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
+      const float* Ds = Ls + 64;
+      const uint2 qbv = add2(tl, lds0 + sb * kDkdvStage), gbv = add2(tl, lds0 + sb * kDkdvStage + TILE);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 S = {}, dP = {};
@@ -352,40 +362,43 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
           S = mfma_bf16(row_frag(Qs, 32 * u + r, 2 * s + h), kf[s], S);
           dP = mfma_bf16(row_frag(Gs, 32 * u + r, 2 * s + h), vf[s], dP);
         }
+        bf16x8 g00, g01, g10, g11, q00, q01, q10, q11;
+        if (u == 0) {
+          g00 = tfrag<0, 0>(gbv); g01 = tfrag<0, 1>(gbv); g10 = tfrag<1, 0>(gbv); g11 = tfrag<1, 1>(gbv);
+          q00 = tfrag<0, 0>(qbv); q01 = tfrag<0, 1>(qbv); q10 = tfrag<1, 0>(qbv); q11 = tfrag<1, 1>(qbv);
+        } else {
+          g00 = tfrag<2, 0>(gbv); g01 = tfrag<2, 1>(gbv); g10 = tfrag<3, 0>(gbv); g11 = tfrag<3, 1>(gbv);
+          q00 = tfrag<2, 0>(qbv); q01 = tfrag<2, 1>(qbv); q10 = tfrag<3, 0>(qbv); q11 = tfrag<3, 1>(qbv);
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][32 * u + 8 * g + 4 * h]);
-          const float4 d4 = *reinterpret_cast<const float4*>(&Ds[buf][32 * u + 8 * g + 4 * h]);
-          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+          const float4 l4 = *reinterpret_cast<const float4*>(&Ls[32 * u + 8 * g + 4 * h]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&Ds[32 * u + 8 * g + 4 * h]);
+          const float lv[4] = {l4.x * 1.4426950408889634f, l4.y * 1.4426950408889634f,
+                               l4.z * 1.4426950408889634f, l4.w * 1.4426950408889634f};
           const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g + e;
             const int q = qbase + 32 * u + 8 * g + 4 * h + e;
-            const float p = myk > q ? 0.f : exp2f(S[i] * sl2 - lv[e]);
+            const float p = myk > q ? 0.f : fexp2(S[i] * sl2 - lv[e]);
             S[i] = p;
             dP[i] = p * (dP[i] - dv[e]);
           }
         }
         const bf16x8 p0 = frag_of<0>(S), p1 = frag_of<1>(S);
-        const bf16x8 g0 = frag_of<0>(dP), g1 = frag_of<1>(dP);
-        dv0 = mfma_bf16(p0, tr_frag(Gs, 32 * u, 0), dv0);
-        dv1 = mfma_bf16(p0, tr_frag(Gs, 32 * u, 32), dv1);
-        dv0 = mfma_bf16(p1, tr_frag(Gs, 32 * u + 16, 0), dv0);
-        dv1 = mfma_bf16(p1, tr_frag(Gs, 32 * u + 16, 32), dv1);
-        dk0 = mfma_bf16(g0, tr_frag(Qs, 32 * u, 0), dk0);
-        dk1 = mfma_bf16(g0, tr_frag(Qs, 32 * u, 32), dk1);
-        dk0 = mfma_bf16(g1, tr_frag(Qs, 32 * u + 16, 0), dk0);
-        dk1 = mfma_bf16(g1, tr_frag(Qs, 32 * u + 16, 32), dk1);
+        const bf16x8 d0 = frag_of<0>(dP), d1 = frag_of<1>(dP);
+        lgkm_fence();
+        dv0 = mfma_bf16(p0, g00, dv0);
+        dv1 = mfma_bf16(p0, g01, dv1);
+        dv0 = mfma_bf16(p1, g10, dv0);
+        dv1 = mfma_bf16(p1, g11, dv1);
+        dk0 = mfma_bf16(d0, q00, dk0);
+        dk1 = mfma_bf16(d0, q01, dk1);
+        dk0 = mfma_bf16(d1, q10, dk0);
+        dk1 = mfma_bf16(d1, q11, dk1);
       }
     }
-    if (more) {
-      tile_store(lds + (buf ^ 1) * TILE, qr);
-      tile_store(lds + 2 * TILE + (buf ^ 1) * TILE, gr);
-      if (tid < 64) Ls[buf ^ 1][tid] = lsv * 1.4426950408889634f;
-      else if (tid < 128) Ds[buf ^ 1][tid - 64] = lsv;
-    }
-    __syncthreads();
   }
   // acc rows = keys (regs), cols = dims (lanes): 2-byte stores, coalesced across the 32 lanes of a half
   bf16_t* dKb = dK + boff;
