@@ -6,7 +6,8 @@ main.py:130-147) on synthetic MNIST, DDP at 1/2/4/8 GPUs (weak scaling: 128 imag
 step, the reference's default ``--batch-size``), fp32 (the reference's dtype), Adam(lr=1e-3).
 
 One timed "step" is the full reference step (main.py:84-99): forward, cross-entropy, backward,
-gradient all-reduce + average over ranks (RCCL, bucketed, overlapped with the conv backward),
+gradient all-reduce + average over ranks (bucketed, overlapped with the conv backward; each bucket
+takes the faster of RCCL and the xGMI peer all-reduce, timed on this node at start-up),
 Adam update, loss/accuracy meters.  Each rank trains on its DistributedSampler shard of a
 60,000-sample synthetic set (random-init weights, synthetic data: no network on the box).
 
@@ -73,6 +74,12 @@ def main():
     if comm is not None:
         dist.broadcast_parameters(net)            # DDP semantics: replicas start identical
     eng = LeNetTrainStep(net, batch_size=args.batch_size, lr=1e-3, comm=comm, overlap=not args.no_overlap)
+    routes = {}
+    if comm is not None and eng.comm_on:
+        routes = {"routes": {str(k): v for k, v in comm.routes.items()},
+                  "route_us_per_call": {str(k): v for k, v in comm.timings.items()}}
+        if comm.peer is None and os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0":
+            print("note: xGMI peer all-reduce unavailable, RCCL only", file=sys.stderr)
     train = synthetic_mnist(args.train_size, seed=args.seed, device=dev, kind="fashion")
     eng.bind_dataset(train.images, train.labels)
     sampler = DistributedSampler(train, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
@@ -112,6 +119,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    health = comm.health() if comm is not None else ""
+    if health:
+        print(f"error: communication failure during the timed steps: {health}", file=sys.stderr)
     loss_sum, correct, _ = eng.read_meters()
     n_img = args.steps * args.batch_size * world
     ips = n_img / elapsed
@@ -138,7 +148,9 @@ def main():
                 "optimizer": "Adam(lr=1e-3)",
                 "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
                 "grad_allreduce": "none" if world == 1 else ("bucketed-overlap" if not args.no_overlap else "flat"),
+                **routes,
             },
+            "comm_errors": health or None,
             "stock_torch_same_hw_w1_images_per_s": STOCK_TORCH_W1,
             "speedup_vs_stock_torch_per_gpu": round(ips / world / STOCK_TORCH_W1, 2),
             "train_loss_mean_timed_rank0": round(loss_sum / max(1, args.steps * args.batch_size), 5),

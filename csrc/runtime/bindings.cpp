@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "hostcomm.h"
+#include "peer_allreduce.h"
 #include "rccl_comm.h"
 #include "store.h"
 
@@ -191,4 +192,30 @@ PYBIND11_MODULE(_runtime, m) {
       .def("error", &CommWatchdog::error)
       .def("pending", &CommWatchdog::pending)
       .def("stop", &CommWatchdog::stop, py::call_guard<py::gil_scoped_release>());
+  py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce")
+      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("capacity_bytes"), py::call_guard<py::gil_scoped_release>())
+      .def("handle", [](PeerAllReduce& p) { return py::bytes(p.handle()); })
+      .def("open",
+           [](PeerAllReduce& p, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             py::gil_scoped_release nogil;
+             p.open(v);
+           })
+      .def("all_reduce_f32", &PeerAllReduce::all_reduce_f32, py::arg("inp"), py::arg("out"), py::arg("count"),
+           py::arg("scale"), py::arg("algo"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_bf16", &PeerAllReduce::all_reduce_bf16, py::arg("inp"), py::arg("out"), py::arg("count"),
+           py::arg("scale"), py::arg("algo"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("capacity_bytes", &PeerAllReduce::capacity_bytes)
+      .def_property_readonly("rank", &PeerAllReduce::rank)
+      .def_property_readonly("world", &PeerAllReduce::world)
+      .def_property_readonly("device", &PeerAllReduce::device)
+      .def_property_readonly("is_open", &PeerAllReduce::is_open)
+      .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
+      .def("reset_error", &PeerAllReduce::reset_error)
+      .def("set_timeout_ms", &PeerAllReduce::set_timeout_ms)
+      .def("set_one_shot_max_bytes", &PeerAllReduce::set_one_shot_max_bytes)
+      .def("set_max_blocks", &PeerAllReduce::set_max_blocks)
+      .def("close", &PeerAllReduce::close, py::call_guard<py::gil_scoped_release>());
 }

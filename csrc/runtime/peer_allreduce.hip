@@ -1,0 +1,361 @@
+// Peer all-reduce over xGMI-mapped peer memory (design notes in peer_allreduce.h).
+#include "peer_allreduce.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace pde {
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
+}
+
+constexpr int kThreads = 512;                 // 8 waves per block
+constexpr int64_t kFlagBytes = 64 * 1024;     // flags[2 phases][kPeerMaxBlocks][kPeerMaxRanks] u32 (8 KB used)
+
+struct Args {
+  uint8_t* base[kPeerMaxRanks];   // every rank's shared region (base[rank] = own)
+  const uint4* in;
+  uint4* out;
+  uint32_t* ctrl;                 // [0] completed calls, [1] blocks done in this call, [2] timeouts
+  int64_t n4;                     // 16-byte vectors
+  int64_t tail;                   // trailing elements (< elements per vector)
+  int64_t chunk4;                 // two-shot chunk (vectors); == n4 for one-shot
+  int64_t cap;                    // bytes per stage / res buffer
+  int64_t timeout;                // s_memrealtime ticks
+  float scale;
+  int rank;
+};
+
+__device__ __forceinline__ uint32_t* flag_ptr(uint8_t* region, int phase, int block, int src) {
+  return reinterpret_cast<uint32_t*>(region) + (phase * kPeerMaxBlocks + block) * kPeerMaxRanks + src;
+}
+__device__ __forceinline__ uint8_t* stage_ptr(uint8_t* region, int64_t cap, uint32_t par) {
+  return region + kFlagBytes + par * cap;
+}
+__device__ __forceinline__ uint8_t* res_ptr(uint8_t* region, int64_t cap, uint32_t par) {
+  return region + kFlagBytes + (2 + par) * cap;
+}
+
+// Block-level barrier between block b of every rank: publish `target` into every peer's flag slot
+// for this rank, wait until every peer published it into ours.  Every thread first drains its own
+// stores (vmcnt(0)); the signalling store is a system-scope release after the block barrier.
+template <int W>
+__device__ __forceinline__ void peer_barrier(const Args& a, int phase, uint32_t target, bool failed) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): this wave's stores have landed
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < W) {
+    __hip_atomic_store(flag_ptr(a.base[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = flag_ptr(a.base[a.rank], phase, blockIdx.x, t);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int spins = 0;
+    // after a time-out the communicator is poisoned: signal, never wait again (fail fast, no hang)
+    while (!failed && __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == 256) {
+        spins = 0;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {   // dead / hung peer
+          __hip_atomic_fetch_add(a.ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+struct F32Op {
+  static __device__ __forceinline__ void zero(float* acc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = 0.f;
+  }
+  static __device__ __forceinline__ void add(float* acc, uint4 v) {
+    acc[0] += __uint_as_float(v.x); acc[1] += __uint_as_float(v.y);
+    acc[2] += __uint_as_float(v.z); acc[3] += __uint_as_float(v.w);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* acc, float s) {
+    return make_uint4(__float_as_uint(acc[0] * s), __float_as_uint(acc[1] * s), __float_as_uint(acc[2] * s),
+                      __float_as_uint(acc[3] * s));
+  }
+  static constexpr int kAcc = 4;
+  static constexpr int kPerVec = 4;
+  static __device__ __forceinline__ void tail_add(float& acc, const uint8_t* p, int64_t i) {
+    acc += reinterpret_cast<const float*>(p)[i];
+  }
+  static __device__ __forceinline__ void tail_store(uint8_t* p, int64_t i, float v) {
+    reinterpret_cast<float*>(p)[i] = v;
+  }
+  static __device__ __forceinline__ void tail_copy(uint8_t* d, const uint8_t* s, int64_t i) {
+    reinterpret_cast<float*>(d)[i] = reinterpret_cast<const float*>(s)[i];
+  }
+};
+
+struct BF16Op {
+  static __device__ __forceinline__ void zero(float* acc) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  }
+  static __device__ __forceinline__ void add(float* acc, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[2 * i] += __uint_as_float(w[i] << 16);
+      acc[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ uint32_t pk(float a, float b) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    bf2 v;
+    v[0] = (__bf16)a;
+    v[1] = (__bf16)b;
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* acc, float s) {
+    return make_uint4(pk(acc[0] * s, acc[1] * s), pk(acc[2] * s, acc[3] * s), pk(acc[4] * s, acc[5] * s),
+                      pk(acc[6] * s, acc[7] * s));
+  }
+  static constexpr int kAcc = 8;
+  static constexpr int kPerVec = 8;
+  static __device__ __forceinline__ void tail_add(float& acc, const uint8_t* p, int64_t i) {
+    acc += __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(p)[i]) << 16);
+  }
+  static __device__ __forceinline__ void tail_store(uint8_t* p, int64_t i, float v) {
+    reinterpret_cast<uint16_t*>(p)[i] = uint16_t(pk(v, 0.f) & 0xffffu);
+  }
+  static __device__ __forceinline__ void tail_copy(uint8_t* d, const uint8_t* s, int64_t i) {
+    reinterpret_cast<uint16_t*>(d)[i] = reinterpret_cast<const uint16_t*>(s)[i];
+  }
+};
+
+// Sum slice element i (vector index) over every rank's buffer at byte offset `off` of region + buf.
+template <int W, typename Op>
+__device__ __forceinline__ uint4 reduce_vec(const Args& a, uint32_t par, int64_t i, bool res) {
+  uint4 v[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {   // all W loads in flight before the first add
+    const uint8_t* src = res ? res_ptr(a.base[p], a.cap, par) : stage_ptr(a.base[p], a.cap, par);
+    v[p] = reinterpret_cast<const uint4*>(src)[i];
+  }
+  float acc[Op::kAcc];
+  Op::zero(acc);
+#pragma unroll
+  for (int p = 0; p < W; ++p) Op::add(acc, v[p]);   // fixed rank order: bit-identical on every rank
+  return Op::pack(acc, a.scale);
+}
+
+template <int W, bool TWO, typename Op>
+__global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
+  __shared__ uint32_t s_call, s_failed;
+  if (threadIdx.x == 0) {
+    s_call = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_failed = __hip_atomic_load(a.ctrl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t call = s_call;
+  const bool failed = s_failed != 0;
+  const uint32_t par = call & 1u, target = call + 1u;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int nchunks = TWO ? W : 1;
+  uint8_t* my_stage = stage_ptr(a.base[a.rank], a.cap, par);
+
+  // 1. stage this rank's input (chunk-relative slices: block b owns the same slices on every rank)
+  for (int c = 0; c < nchunks; ++c) {
+    const int64_t lo = (int64_t)c * a.chunk4;
+    const int64_t len = (lo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
+    for (int64_t i = t0; i < len; i += stride)
+      reinterpret_cast<uint4*>(my_stage)[lo + i] = a.in[lo + i];
+  }
+  const int64_t tail_off = a.n4 * Op::kPerVec;
+  if (blockIdx.x == 0 && threadIdx.x < a.tail)
+    Op::tail_copy(my_stage, reinterpret_cast<const uint8_t*>(a.in), tail_off + threadIdx.x);
+  peer_barrier<W>(a, 0, target, failed);
+
+  if (blockIdx.x == 0 && threadIdx.x < a.tail) {   // tail: every rank reduces it itself, same order
+    float acc = 0.f;
+    for (int p = 0; p < W; ++p) Op::tail_add(acc, stage_ptr(a.base[p], a.cap, par), tail_off + threadIdx.x);
+    Op::tail_store(reinterpret_cast<uint8_t*>(a.out), tail_off + threadIdx.x, acc * a.scale);
+  }
+  if (!TWO) {
+    for (int64_t i = t0; i < a.n4; i += stride) a.out[i] = reduce_vec<W, Op>(a, par, i, false);
+  } else {
+    // 2. reduce this rank's chunk from every peer's stage into own res[par] (+ own output)
+    const int64_t lo = (int64_t)a.rank * a.chunk4;
+    const int64_t len = (lo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
+    uint4* my_res = reinterpret_cast<uint4*>(res_ptr(a.base[a.rank], a.cap, par));
+    for (int64_t i = t0; i < len; i += stride) {
+      const uint4 r = reduce_vec<W, Op>(a, par, lo + i, false);
+      my_res[lo + i] = r;
+      a.out[lo + i] = r;
+    }
+    peer_barrier<W>(a, 1, target, failed);
+    // 3. gather every other chunk from its owner's res[par]
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q == a.rank) continue;
+      const int64_t qlo = (int64_t)q * a.chunk4;
+      const int64_t qlen = (qlo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > qlo ? a.n4 - qlo : 0);
+      const uint4* src = reinterpret_cast<const uint4*>(res_ptr(a.base[q], a.cap, par));
+      for (int64_t i = t0; i < qlen; i += stride) a.out[qlo + i] = src[qlo + i];
+    }
+  }
+  // call bookkeeping: the last block of this call advances the call number
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(a.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(a.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int W, typename Op>
+void launch_w(const Args& a, bool two, int nb, hipStream_t s) {
+  if (two)
+    hipLaunchKernelGGL((peer_allreduce_kernel<W, true, Op>), dim3(nb), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((peer_allreduce_kernel<W, false, Op>), dim3(nb), dim3(kThreads), 0, s, a);
+}
+
+template <typename Op>
+void launch_any(int world, const Args& a, bool two, int nb, hipStream_t s) {
+  switch (world) {
+    case 1: launch_w<1, Op>(a, two, nb, s); break;
+    case 2: launch_w<2, Op>(a, two, nb, s); break;
+    case 3: launch_w<3, Op>(a, two, nb, s); break;
+    case 4: launch_w<4, Op>(a, two, nb, s); break;
+    case 5: launch_w<5, Op>(a, two, nb, s); break;
+    case 6: launch_w<6, Op>(a, two, nb, s); break;
+    case 7: launch_w<7, Op>(a, two, nb, s); break;
+    case 8: launch_w<8, Op>(a, two, nb, s); break;
+    default: throw std::invalid_argument("peer all-reduce supports 1..8 ranks");
+  }
+}
+
+}  // namespace
+
+PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_bytes)
+    : rank_(rank), world_(world), device_(device) {
+  if (world < 1 || world > kPeerMaxRanks) throw std::invalid_argument("peer all-reduce supports 1..8 ranks");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("bad rank");
+  cap_ = (capacity_bytes + 65535) / 65536 * 65536;
+  region_bytes_ = kFlagBytes + 4 * cap_;
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  void* p = nullptr;
+  hip_check(hipExtMallocWithFlags(&p, region_bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  region_ = static_cast<uint8_t*>(p);
+  hip_check(hipMemset(region_, 0, region_bytes_), "hipMemset");
+  void* c = nullptr;
+  hip_check(hipExtMallocWithFlags(&c, 256, hipDeviceMallocUncached), "hipExtMallocWithFlags(ctrl)");
+  ctrl_ = static_cast<uint32_t*>(c);
+  hip_check(hipMemset(ctrl_, 0, 256), "hipMemset");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  peers_[rank_] = region_;
+}
+
+PeerAllReduce::~PeerAllReduce() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+void PeerAllReduce::close() {
+  if (region_ == nullptr) return;
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
+  for (int p = 0; p < world_; ++p)
+    if (p != rank_ && peers_[p] != nullptr) (void)hipIpcCloseMemHandle(peers_[p]);
+  for (auto& q : peers_) q = nullptr;
+  (void)hipFree(region_);
+  (void)hipFree(ctrl_);
+  region_ = nullptr;
+  ctrl_ = nullptr;
+  opened_ = false;
+}
+
+std::string PeerAllReduce::handle() const {
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void PeerAllReduce::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::invalid_argument("need one IPC handle per rank");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    if (handles[p].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[p].data(), sizeof(h));
+    void* ptr = nullptr;
+    hip_check(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    peers_[p] = static_cast<uint8_t*>(ptr);
+  }
+  opened_ = true;
+}
+
+void PeerAllReduce::launch(uintptr_t in, uintptr_t out, int64_t count, float scale, int algo, uintptr_t stream,
+                           bool bf16) {
+  if (!opened_) throw std::runtime_error("peer all-reduce used before open()");
+  const int esize = bf16 ? 2 : 4;
+  const int per_vec = 16 / esize;
+  if (count <= 0) return;
+  if (count * esize > cap_) throw std::invalid_argument("peer all-reduce buffer exceeds the registered capacity");
+  if ((in | out) & 15) throw std::invalid_argument("peer all-reduce needs 16-byte aligned buffers");
+  Args a;
+  for (int p = 0; p < kPeerMaxRanks; ++p) a.base[p] = p < world_ ? peers_[p] : nullptr;
+  a.in = reinterpret_cast<const uint4*>(in);
+  a.out = reinterpret_cast<uint4*>(out);
+  a.ctrl = ctrl_;
+  a.n4 = count / per_vec;
+  a.tail = count - a.n4 * per_vec;
+  a.cap = cap_;
+  a.timeout = timeout_ticks_;
+  a.scale = scale;
+  a.rank = rank_;
+  const bool two = algo == 2 || (algo == 0 && world_ > 2 && count * esize > one_shot_max_);
+  a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
+  int64_t work = two ? a.chunk4 : a.n4;
+  int64_t nb = (work + kThreads - 1) / kThreads;
+  if (nb < 1) nb = 1;
+  if (nb > max_blocks_) nb = max_blocks_;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (bf16)
+    launch_any<BF16Op>(world_, a, two, (int)nb, s);
+  else
+    launch_any<F32Op>(world_, a, two, (int)nb, s);
+  hip_check(hipGetLastError(), "peer all-reduce launch");
+}
+
+void PeerAllReduce::all_reduce_f32(uintptr_t in, uintptr_t out, int64_t count, float scale, int algo,
+                                   uintptr_t stream) {
+  launch(in, out, count, scale, algo, stream, false);
+}
+
+void PeerAllReduce::all_reduce_bf16(uintptr_t in, uintptr_t out, int64_t count, float scale, int algo,
+                                    uintptr_t stream) {
+  launch(in, out, count, scale, algo, stream, true);
+}
+
+int64_t PeerAllReduce::error() {
+  uint32_t v = 0;
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemcpy(&v, ctrl_ + 2, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+  return v;
+}
+
+void PeerAllReduce::reset_error() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipMemset(ctrl_ + 2, 0, 4), "hipMemset");
+}
+
+}  // namespace pde

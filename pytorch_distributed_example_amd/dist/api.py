@@ -730,23 +730,73 @@ def barrier(group=None, async_op: bool = False, device_ids=None):
 # framework helpers
 # ------------------------------------------------------------------------------------------------
 class EngineComm:
-    """Minimal comm handle for the fused training engines: SUM all-reduce of a flat buffer enqueued on
-    the CURRENT stream (the engine puts it on its comm stream and captures it in hipGraphs)."""
+    """Comm handle for the fused training engines: SUM all-reduce of a flat buffer enqueued on the
+    CURRENT stream (the engine puts it on its comm stream and captures it in hipGraphs).
 
-    def __init__(self, group: ProcessGroup):
-        if group.rccl is None:
+    ``enable_peer(sizes)`` adds the xGMI peer all-reduce (``dist/peer.py``) for small buffers and
+    times it against RCCL at exactly those sizes; each size then takes the faster route.  A group
+    without RCCL (gloo, e.g. several ranks sharing one GPU in tests) routes everything to the peer
+    kernel."""
+
+    def __init__(self, group: ProcessGroup, allow_host_only: bool = False):
+        if group.rccl is None and not allow_host_only:
             raise RuntimeError("engine comm needs an RCCL (backend='nccl') process group")
         self.group = group
         self.world_size = group.size()
         self.rank = group.rank()
+        self.peer = None
+        self.routes = {}
+        self.timings = {}
 
-    def all_reduce_(self, t: torch.Tensor, op=ReduceOp.SUM):
+    def _rccl(self, t: torch.Tensor, op=ReduceOp.SUM):
         self.group.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPES[t.dtype], _op_code(op),
                                    torch.cuda.current_stream(t.device).cuda_stream)
 
+    def enable_peer(self, sizes, device, dtype=torch.float32, capacity_bytes: Optional[int] = None, tune=True):
+        """Collective.  Returns the chosen route per size ({numel: 'rccl'|'peer1'|'peer2'})."""
+        from .peer import PeerAllReduce, tune_routes
+        sizes = sorted({int(n) for n in sizes})
+        esize = torch.tensor([], dtype=dtype).element_size()
+        cap = capacity_bytes or max(sizes) * esize
+        if os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0":
+            self.peer = PeerAllReduce(self.group, torch.device(device), cap)
+            if not self.peer.ok:
+                self.peer = None
+        rccl_fn = self._rccl if self.group.rccl is not None else None
+        if tune:
+            self.routes, self.timings = tune_routes(self.group, self.peer, rccl_fn, sizes, device, dtype)
+        else:
+            self.routes = {n: ("peer2" if self.peer is not None else "rccl") for n in sizes}
+        return self.routes
 
-def engine_comm(group=None) -> EngineComm:
-    return EngineComm(_group(group))
+    def route(self, t: torch.Tensor) -> str:
+        r = self.routes.get(t.numel())
+        if r is None:
+            r = "rccl" if self.group.rccl is not None or self.peer is None else "peer2"
+        if r != "rccl" and not (self.peer is not None and self.peer.supports(t)):
+            r = "rccl"
+        if r == "rccl" and self.group.rccl is None:
+            raise RuntimeError("no RCCL communicator and the peer all-reduce cannot take this buffer")
+        return r
+
+    def all_reduce_(self, t: torch.Tensor, op=ReduceOp.SUM):
+        r = self.route(t) if _op_code(op) in (0, 4) else "rccl"
+        if r == "rccl":
+            self._rccl(t, op)
+        else:
+            self.peer.all_reduce_(t, r, scale=(1.0 / self.world_size) if _op_code(op) == 4 else 1.0)
+
+    def health(self) -> str:
+        """'' if healthy, else a description of the failure (peer barrier time-outs, RCCL errors)."""
+        if self.peer is not None and self.peer.error():
+            return f"peer all-reduce: {self.peer.error()} barrier time-out(s)"
+        if self.group.watchdog is not None:
+            return self.group.watchdog.error()
+        return ""
+
+
+def engine_comm(group=None, allow_host_only: bool = False) -> EngineComm:
+    return EngineComm(_group(group), allow_host_only)
 
 
 @torch.no_grad()

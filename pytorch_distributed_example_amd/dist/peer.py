@@ -1,0 +1,191 @@
+"""xGMI peer all-reduce for small, latency-bound buffers (``csrc/runtime/peer_allreduce.hip``).
+
+The reference averages gradients with one blocking all-reduce per parameter
+(/root/reference/mnist/main.py:122-127); the framework packs them into two flat buckets
+(1.62 MB + 0.10 MB for the toy CNN).  At that size a ring all-reduce over 8 GPUs is dominated by
+its 2·(W-1) dependent hops, so for small buckets every rank instead reads its peers' staged data
+directly over the 7 point-to-point xGMI links (one-shot: one barrier; two-shot: reduce-scatter +
+all-gather through peer memory, two barriers).  Large buckets (ResNet-18 / GPT-2) stay on RCCL.
+
+``PeerAllReduce(group)`` is collective over a process group: every rank allocates an uncached
+shared region, exchanges its IPC handle through the group's TCP store, maps every peer's region,
+and then runs a self-test of both algorithms (f32 and bf16, ragged sizes) against the exact
+answer.  Any failure on any rank (IPC unsupported, wrong sums, a barrier time-out) disables the
+path on every rank and the caller keeps using RCCL.
+
+``tune_routes`` times RCCL against the one-/two-shot peer kernels at the sizes an engine will use
+(max over ranks, so every rank takes the same decision) and returns the fastest per size.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Iterable, Optional
+
+import torch
+
+from .._ext import runtime
+
+ONE_SHOT, TWO_SHOT, RCCL = "peer1", "peer2", "rccl"
+_ALGO = {ONE_SHOT: 1, TWO_SHOT: 2}
+_SEQ = [0]
+
+
+def _host_allreduce_min(group, value: int) -> int:
+    t = torch.tensor([int(value)], dtype=torch.int64)
+    group.host.allreduce(t.data_ptr(), 1, 3, 2)     # int64, MIN
+    return int(t.item())
+
+
+def _host_allreduce_max_f64(group, vals) -> list:
+    t = torch.tensor(list(vals), dtype=torch.float64)
+    group.host.allreduce(t.data_ptr(), t.numel(), 1, 3)   # float64, MAX
+    return t.tolist()
+
+
+class PeerAllReduce:
+    """Collective constructor; see the module docstring.  ``ok`` says whether the path is usable."""
+
+    def __init__(self, group, device: torch.device, capacity_bytes: int, timeout_ms: int = 10000,
+                 self_test: bool = True):
+        self.group = group
+        self.device = torch.device(device)
+        self.rank, self.world = group.rank(), group.size()
+        self.native = None
+        self.ok = False
+        self.reason = ""
+        _SEQ[0] += 1
+        key = f"{group.prefix}/peer_ar/{_SEQ[0]}"
+        err = ""
+        try:
+            self.native = runtime().PeerAllReduce(self.rank, self.world, self.device.index, int(capacity_bytes))
+            self.native.set_timeout_ms(int(timeout_ms))
+            group.store.set(f"{key}/h{self.rank}", self.native.handle())
+            group.store.set(f"{key}/dev{self.rank}", str(self.device.index).encode())
+        except Exception as e:   # noqa: BLE001 - any failure means "no peer path"
+            err = f"setup: {e}"
+            group.store.set(f"{key}/h{self.rank}", b"")
+            group.store.set(f"{key}/dev{self.rank}", b"-1")
+        handles = [group.store.get(f"{key}/h{r}") for r in range(self.world)]
+        devs = [int(group.store.get(f"{key}/dev{r}")) for r in range(self.world)]
+        if not err:
+            try:
+                if any(len(h) == 0 for h in handles):
+                    raise RuntimeError("a peer failed to create its region")
+                me = self.device.index
+                for d in set(devs):
+                    if d != me and not torch.cuda.can_device_access_peer(me, d):
+                        raise RuntimeError(f"cuda:{me} cannot access peer cuda:{d}")
+                self.native.open(handles)
+            except Exception as e:   # noqa: BLE001
+                err = f"open: {e}"
+        ok = _host_allreduce_min(group, 0 if err else 1)
+        group.host.barrier()
+        if ok and self_test:
+            try:
+                self._self_test()
+            except Exception as e:   # noqa: BLE001
+                err = f"self-test: {e}"
+            ok = _host_allreduce_min(group, 0 if err else 1)
+        self.ok = bool(ok)
+        self.reason = err or ("" if ok else "disabled by a peer rank")
+        if not self.ok and self.native is not None:
+            try:
+                self.native.close()
+            except Exception:   # noqa: BLE001
+                pass
+            self.native = None
+
+    @property
+    def capacity_bytes(self) -> int:
+        return self.native.capacity_bytes if self.native is not None else 0
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return (self.ok and t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+                and t.numel() * t.element_size() <= self.capacity_bytes and t.data_ptr() % 16 == 0)
+
+    def all_reduce_(self, t: torch.Tensor, algo: str = "auto", scale: float = 1.0, stream=None):
+        """In-place SUM (times ``scale``) on ``stream`` (default: the current stream)."""
+        s = stream if stream is not None else torch.cuda.current_stream(t.device)
+        a = _ALGO.get(algo, 0)
+        fn = self.native.all_reduce_f32 if t.dtype == torch.float32 else self.native.all_reduce_bf16
+        fn(t.data_ptr(), t.data_ptr(), t.numel(), float(scale), a, s.cuda_stream)
+
+    def error(self) -> int:
+        return int(self.native.error()) if self.native is not None else 0
+
+    def _self_test(self):
+        W, r = self.world, self.rank
+        cap_el = self.capacity_bytes // 4
+        sizes = sorted({1, 3, 5, 1000, 4099, min(cap_el, 70001), cap_el - 3})
+        for dtype in (torch.float32, torch.bfloat16):
+            for n in sizes:
+                if n <= 0 or n * (4 if dtype == torch.float32 else 2) > self.capacity_bytes:
+                    continue
+                base = (torch.arange(n, device=self.device, dtype=torch.float32) % 13) - 6
+                for algo in (ONE_SHOT, TWO_SHOT):
+                    x = (base * (r + 1)).to(dtype)
+                    self.all_reduce_(x, algo)
+                    torch.cuda.synchronize(self.device)
+                    if self.error():
+                        raise RuntimeError(f"barrier time-out during self-test ({algo} {dtype} n={n})")
+                    want = (base * (W * (W + 1) // 2)).to(dtype)
+                    if not torch.equal(x, want):
+                        bad = int((x != want).sum())
+                        raise RuntimeError(f"{algo} {dtype} n={n}: {bad} wrong elements")
+        if self.error():
+            raise RuntimeError("barrier time-out during self-test")
+
+    def close(self):
+        if self.native is not None:
+            self.native.close()
+            self.native = None
+            self.ok = False
+
+
+def _time_calls(fn, iters: int, device) -> float:
+    torch.cuda.synchronize(device)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize(device)
+    return s.elapsed_time(e) * 1e3 / iters   # us per call
+
+
+def tune_routes(group, peer: Optional[PeerAllReduce], rccl_fn, sizes: Iterable[int], device,
+                dtype=torch.float32, iters: int = 30):
+    """Fastest all-reduce route per element count: ({numel: 'rccl' | 'peer1' | 'peer2'},
+    {numel: {candidate: us per call (max over ranks)}}).
+
+    ``rccl_fn(tensor)`` enqueues the RCCL all-reduce on the current stream (None: RCCL unavailable).
+    Every candidate is timed on every rank; the per-candidate MAX over ranks decides, so all ranks
+    agree.  Forced with PDE_ALLREDUCE_ROUTE=rccl|peer1|peer2."""
+    forced = os.environ.get("PDE_ALLREDUCE_ROUTE")
+    out: Dict[int, str] = {}
+    timings: Dict[int, dict] = {}
+    for n in sizes:
+        cands = []
+        if rccl_fn is not None:
+            cands.append(RCCL)
+        buf = torch.zeros(n, device=device, dtype=dtype)
+        if peer is not None and peer.ok and peer.supports(buf):
+            cands += [ONE_SHOT, TWO_SHOT]
+        if forced in cands:
+            out[n] = forced
+            continue
+        if not cands:
+            raise RuntimeError("no all-reduce route available")
+        if len(cands) == 1:
+            out[n] = cands[0]
+            continue
+        times = []
+        for c in cands:
+            fn = (lambda: rccl_fn(buf)) if c == RCCL else (lambda c=c: peer.all_reduce_(buf, c))
+            fn()
+            group.host.barrier()
+            times.append(_time_calls(fn, iters, device))
+        times = _host_allreduce_max_f64(group, times)
+        out[n] = cands[min(range(len(cands)), key=lambda i: times[i])]
+        timings[n] = dict(zip(cands, [round(t, 2) for t in times]))
+    return out, timings

@@ -96,6 +96,9 @@ class LeNetTrainStep:
         self._ev = {k: torch.cuda.Event() for k in ("fc", "conv", "fc_done")}
         self.bucket_ranges = [tuple(r) for r in self.layout.bucket_ranges]
         assert self.bucket_ranges[0][0] == 0 and self.bucket_ranges[1][0] >= self.bucket_ranges[0][1]
+        if self.comm_on and hasattr(comm, "enable_peer") and not comm.routes:
+            # small buckets: time the xGMI peer all-reduce against RCCL at exactly these sizes
+            comm.enable_peer([b.numel() for b in self.bucket_grads] + [self.grads.numel()], dev)
         self.X = self.Y = self.idx = None
         self.nbatches = 0
         self.graphs = {}

@@ -7,7 +7,8 @@ objects travel with the repo snapshot to the GPU box (see ``_ext.py`` for loadin
 Two extension modules are produced:
 
 * ``_runtime``  - C++ distributed runtime (TCP rendezvous store, host TCP collectives, RCCL
-                  communicator).  pybind11 only, no torch headers, links torch's bundled
+                  communicator, xGMI peer all-reduce kernel ``runtime/peer_allreduce.hip``).
+                  pybind11 only, no torch headers, links torch's bundled
                   ``librccl.so.1`` / ``libamdhip64.so.7`` (same sonames as /opt/rocm).
 * ``_kernels``  - CDNA4 HIP kernels (``csrc/kernels/*.hip``, device code, no torch headers)
                   plus a thin torch C++ binding layer (``csrc/ops_bindings.cpp``).
@@ -77,9 +78,10 @@ def _targets():
     rpath = ["-Wl,-rpath," + tlib, "-Wl,-rpath," + os.path.join(ROCM, "lib")]
     return {
         "_runtime": dict(
-            sources=[(s, host_cpp) for s in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))],
-            link=["g++", "-shared", "-fPIC", "-L" + tlib, "-l:librccl.so", "-l:libamdhip64.so",
-                  "-lpthread"] + rpath,
+            sources=[(s, host_cpp) for s in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))]
+            + [(s, hip_dev) for s in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.hip")))],
+            link=["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-L" + tlib, "-l:librccl.so",
+                  "-l:libamdhip64.so", "-lpthread"] + rpath,
         ),
         "_kernels": dict(
             sources=[(s, hip_dev) for s in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))]

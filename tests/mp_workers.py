@@ -273,6 +273,98 @@ def case_engine_comm(steps="3", mode="eager"):
     dist.destroy_process_group()
 
 
+def _shared_gpu_init():
+    """Ranks that share cuda:0 (1-GPU box): gloo group for control, peer kernel for data."""
+    _init("gloo")
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+def case_peer_allreduce(graph="1"):
+    """xGMI peer all-reduce (one-/two-shot, f32/bf16, ragged sizes) vs an fp64 reference; results must
+    be bit-identical on every rank.  Also replays it from a captured hipGraph."""
+    from pytorch_distributed_example_amd.dist.peer import PeerAllReduce
+
+    dev = _shared_gpu_init()
+    g = dist.get_default_group()
+    cap = 4 << 20
+    p = PeerAllReduce(g, dev, cap)
+    assert p.ok, p.reason
+    sums = []
+    for dt in (torch.float32, torch.bfloat16):
+        for n in (1, 7, 8, 1000, 4097, 65536 + 5, 431080, (cap // (4 if dt == torch.float32 else 2)) - 1):
+            for algo in ("peer1", "peer2", "auto"):
+                gens = [torch.Generator().manual_seed(1000 * r + n) for r in range(W)]
+                xs = [torch.randn(n, generator=gg).to(dt) for gg in gens]
+                ref = sum(x.double() for x in xs)
+                x = xs[R].to(dev)
+                p.all_reduce_(x, algo)
+                torch.cuda.synchronize()
+                err = (x.double().cpu() - ref).abs().max().item()
+                tol = 1e-5 * W if dt == torch.float32 else 0.02 * W
+                assert err <= tol * max(1.0, ref.abs().max().item()), (dt, n, algo, err)
+                sums.append(float(x.double().sum().item()))
+    # AVG through the scale argument
+    x = torch.full((1000,), float(R + 1), device=dev)
+    p.all_reduce_(x, "peer2", scale=1.0 / W)
+    torch.cuda.synchronize()
+    assert torch.allclose(x, torch.full_like(x, (W + 1) / 2)), x[:4]
+    if graph == "1":
+        xs = [torch.full((300_001,), float(R + 1 + k), device=dev) for k in range(3)]
+        src = [t.clone() for t in xs]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            for k, t in enumerate(xs):
+                p.all_reduce_(t, "peer1" if k == 1 else "peer2")
+        for rep in range(2):
+            for t, s0 in zip(xs, src):
+                t.copy_(s0)
+            torch.cuda.synchronize()
+            dist.barrier()
+            gr.replay()
+            torch.cuda.synchronize()
+            for k, t in enumerate(xs):
+                want = float(sum(r + 1 + k for r in range(W)))
+                assert torch.all(t == want), (rep, k, t[:3])
+    assert p.error() == 0
+    emit({"rank": R, "sums": sums})
+    p.close()
+    dist.destroy_process_group()
+
+
+def case_peer_engine(steps="6", mode="eager", overlap="1"):
+    """Fused LeNet engine, W ranks sharing one GPU, gradients averaged by the peer all-reduce only."""
+    from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
+    from pytorch_distributed_example_amd.engine import LeNetTrainStep
+    from pytorch_distributed_example_amd.models import build_net
+
+    dev = _shared_gpu_init()
+    net = build_net(seed=3 + R, device=dev)
+    dist.broadcast_parameters(net)
+    ds = synthetic_mnist(512 * W, seed=0, device=dev)
+    comm = dist.engine_comm(allow_host_only=True)
+    eng = LeNetTrainStep(net, batch_size=64, comm=comm, force_comm=True, overlap=overlap == "1")
+    assert comm.peer is not None and all(r != "rccl" for r in comm.routes.values()), comm.routes
+    eng.bind_dataset(ds.images, ds.labels)
+    s = DistributedSampler(ds, num_replicas=W, rank=R, shuffle=False)
+    eng.set_epoch_indices(s.indices_tensor())
+    if mode == "graph":
+        eng.capture(steps=2)
+        for _ in range(int(steps) // 2):
+            eng.replay(steps=2)
+    else:
+        for _ in range(int(steps)):
+            eng.step()
+    torch.cuda.synchronize()
+    assert comm.health() == "", comm.health()
+    emit({"rank": R, "routes": {str(k): v for k, v in comm.routes.items()},
+          "params": [p.detach().double().sum().item() for p in net.parameters()],
+          "grads": [float(eng.grads.double().abs().sum().item())]})
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     name = sys.argv[1]
     globals()["case_" + name](*sys.argv[2:])
