@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph (graph mode)")
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0, gloo control group, peer all-reduce for the data")
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--model", choices=["lenet", "gpt2", "resnet18"], default="lenet",
@@ -63,12 +65,15 @@ def main():
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
     from pytorch_distributed_example_amd.models import build_net
 
+    if args.shared_gpu:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     comm = None
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
-        comm = dist.engine_comm()
+        dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method="env://", rank=rank,
+                                world_size=world)
+        comm = dist.engine_comm(allow_host_only=args.shared_gpu)
 
     net = build_net(seed=args.seed, device=dev)
     if comm is not None:
