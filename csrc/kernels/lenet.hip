@@ -86,18 +86,19 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
                                                   float* __restrict__ P2, uint8_t* __restrict__ A2,
                                                   int* __restrict__ cur_row, long long* __restrict__ cur_lbl,
                                                   float* __restrict__ zero_ptr, int zero_n, int dbg) {
-  // dbg (ablation only): 1 skip conv1 compute, 2 skip conv2 MFMA, 4 skip weight-slice staging
+  // dbg (ablation only): 1 skip conv1 compute, 2 skip conv2 MFMA, 4 skip weight-slice staging,
+  // 8 row = b (no counter -> idx -> image load chain), 16 no P1/A1 stores, 32 no bucket zeroing
   __shared__ __attribute__((aligned(16))) float smem[kFwdLds];
   float* ws = smem;                        // [500 k'][32 co]
   float* xs = smem + kFwdWs;               // conv1 output [20][144]
   float* xin = xs + kP1;                   // input image [784]
   float* w1s = xin + kImg;                 // conv1 weight [500] + bias [20] (+pad)
   const int b = blockIdx.x, ct = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
-  if (zero_ptr) {
+  if (zero_ptr && !(dbg & 32)) {
     const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
     for (int i = bid * 256 + t; i < zero_n; i += nb * 256) zero_ptr[i] = 0.f;
   }
-  const int row = sample_row(src, b);
+  const int row = (dbg & 8) ? b : sample_row(src, b);
   // ---- phase 0: issue every global load (image + conv1 weights first, then the weight slice) ----
   const float4 xv = reinterpret_cast<const float4*>(X + (size_t)row * kImg)[min(t, kImg / 4 - 1)];
   const float4 wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
             if (v > best) { best = v; code = q; }
           }
           xs[ch * 144 + pq] = best;
-          if (ct == 0) {
+          if (ct == 0 && !(dbg & 16)) {
             const size_t o = (size_t)b * kP1 + ch * 144 + pq;
             P1[o] = best;
             A1[o] = (uint8_t)code;

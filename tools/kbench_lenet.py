@@ -52,6 +52,10 @@ def main():
         "conv_fwd -conv2mfma": conv_fwd(2),
         "conv_fwd -wstage": conv_fwd(4),
         "conv_fwd -all": conv_fwd(7),
+        "conv_fwd -chain": conv_fwd(8),
+        "conv_fwd -p1store": conv_fwd(16),
+        "conv_fwd -zero": conv_fwd(32),
+        "conv_fwd -all-chain-p1-zero": conv_fwd(7 | 8 | 16 | 32),
         "fc1_fwd": lambda: K.lenet_fc1_fwd(e.P2, B, p["fc1.weight"], p["fc1.bias"], e.H1, None),
         "head": lambda: K.lenet_head(e.H1, B, p["fc2.weight"], p["fc2.bias"], e.cur_lbl, 1.0 / B, None, e.dZ2, e.dZ1,
                                      e.row_loss, e.row_hit, None, None),
@@ -77,9 +81,9 @@ def main():
     # whole-step variants: the real producer -> consumer chain (caches / XCD state as in training),
     # with one kernel's roles ablated, to attribute in-step time (isolated launches of the same kernel
     # back-to-back re-read hot inputs and can under-state it by ~2x).
-    def step(fc_dbg=0, cv_dbg=0, adam=True, fc_split=False):
+    def step(fc_dbg=0, cv_dbg=0, adam=True, fc_split=False, cf_dbg=0):
         def run():
-            conv_fwd(0)()
+            conv_fwd(cf_dbg)()
             K.lenet_fc1_fwd(e.P2, B, p["fc1.weight"], p["fc1.bias"], e.H1, None)
             K.lenet_head(e.H1, B, p["fc2.weight"], p["fc2.bias"], e.cur_lbl, 1.0 / B, None, e.dZ2, e.dZ1,
                          e.row_loss, e.row_hit, None, None)
@@ -106,6 +110,11 @@ def main():
         "STEP cv onlyD": step(cv_dbg=1),
         "STEP cv none": step(cv_dbg=3),
         "STEP -adam": step(adam=False),
+        "STEP cf -chain": step(cf_dbg=8),
+        "STEP cf -p1store": step(cf_dbg=16),
+        "STEP cf -zero": step(cf_dbg=32),
+        "STEP cf -conv1": step(cf_dbg=1),
+        "STEP cf -conv2": step(cf_dbg=2),
     })
     # graph mode: G launches of a variant captured in one hipGraph -> GPU-side cost per launch
     # (kernel + boundary), free of the ~4 us host launch overhead of eager Python launches
