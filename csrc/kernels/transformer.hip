@@ -382,9 +382,12 @@ __global__ __launch_bounds__(256) void k_embed_tok_merge(float* __restrict__ acc
 }
 
 // ---------------------------------------------------------------------------------- optimizer
-// sum of squares of a bf16 buffer (times scale^2) accumulated into *out (one atomic per block)
-__global__ __launch_bounds__(256) void k_sumsq_bf16(const uint2* __restrict__ g, int64_t n4, float scale,
-                                                    float* __restrict__ out) {
+// sum of squares of a bf16 buffer (times scale^2) -> out[0].  Deterministic (bit-identical run to
+// run and across data-parallel ranks holding identical gradients, so clipped replicas never drift):
+// block b writes its partial to out[1 + b], one block then sums the partials in a fixed order.
+constexpr int kSumsqMaxBlocks = 1024;
+
+__global__ __launch_bounds__(256) void k_sumsq_bf16(const uint2* __restrict__ g, int64_t n4, float* __restrict__ out) {
   __shared__ float sh[4];
   float s = 0.f;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -395,7 +398,17 @@ __global__ __launch_bounds__(256) void k_sumsq_bf16(const uint2* __restrict__ g,
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, (sh[0] + sh[1] + sh[2] + sh[3]) * scale * scale);
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__global__ __launch_bounds__(256) void k_sumsq_finish(float* __restrict__ out, int nparts, float scale) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += out[1 + i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) * scale * scale;
 }
 
 // AdamW (torch semantics, decoupled decay) on fp32 master weights; writes the bf16 model copy.
@@ -619,8 +632,9 @@ hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* d
 
 hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st) {
   const int64_t n4 = n / 4;
-  hipLaunchKernelGGL(k_sumsq_bf16, dim3(grid_for(n4, 256, 1024)), dim3(256), 0, st, (const uint2*)g, n4, scale,
-                     out);
+  const int grid = grid_for(n4, 256, kSumsqMaxBlocks);
+  hipLaunchKernelGGL(k_sumsq_bf16, dim3(grid), dim3(256), 0, st, (const uint2*)g, n4, out);
+  hipLaunchKernelGGL(k_sumsq_finish, dim3(1), dim3(256), 0, st, out, grid, scale);
   return hipGetLastError();
 }
 

@@ -802,12 +802,19 @@ def engine_comm(group=None, allow_host_only: bool = False) -> EngineComm:
 @torch.no_grad()
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None, buffers: bool = True):
     """Make every rank's replica identical (DDP semantics; the reference never does this, survey Q2)."""
-    g = _group(group)
-    if g is None or g.size() == 1:
-        return
     tensors = [p.data for p in module.parameters()]
     if buffers:
         tensors += [b for b in module.buffers()]
+    broadcast_coalesced(tensors, src, group)
+
+
+@torch.no_grad()
+def broadcast_coalesced(tensors, src: int = 0, group=None):
+    """Broadcast a list of tensors with ONE collective per (device, dtype): flatten, broadcast, scatter
+    back (torch DDP's ``_broadcast_coalesced``)."""
+    g = _group(group)
+    if g is None or g.size() == 1:
+        return
     by_dev = {}
     for t in tensors:
         by_dev.setdefault((t.device, t.dtype), []).append(t)

@@ -68,7 +68,7 @@ class _MasterBase(torch.optim.Optimizer):
         for k in self._state_keys:
             bufs[k] = torch.zeros(n, device=dev, dtype=torch.float32)
         self._flat = dict(layout=layout, p=fp, g=fg, bufs=bufs, decay=decay.to(dev),
-                          sumsq=torch.zeros(1, device=dev, dtype=torch.float32))
+                          sumsq=torch.zeros(1025, device=dev, dtype=torch.float32))   # [0] + partials
         for p in params:
             st = self.state[p]
             name = p._pde_flat[3]
@@ -147,9 +147,8 @@ class AdamWMaster(_MasterBase):
         f, K = self._flat, kernels()
         clip = None
         if self.max_grad_norm is not None:
-            f["sumsq"].zero_()
-            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"])
-            clip = f["sumsq"]
+            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"])    # deterministic: replicas never drift
+            clip = f["sumsq"][:1]
         g0 = self.param_groups[0]
         b1, b2 = g0["betas"]
         K.adamw_master(f["bufs"]["master"], f["p"], f["g"], f["bufs"]["exp_avg"], f["bufs"]["exp_avg_sq"], g0["lr"],
@@ -158,7 +157,7 @@ class AdamWMaster(_MasterBase):
 
     def grad_norm(self) -> float:
         """Global grad norm of the last clipped step (host sync; for logging only)."""
-        return float(self._flat["sumsq"].sqrt()) if self._flat is not None else 0.0
+        return float(self._flat["sumsq"][0].sqrt()) if self._flat is not None else 0.0
 
 
 class SGDMaster(_MasterBase):

@@ -5,7 +5,8 @@ parameter (``Trainer.average_gradients``, /root/reference/mnist/main.py:122-127)
 synchronises the initial replicas (survey Q2).  This wrapper provides torch-DDP semantics, built
 for MI355X:
 
-* construction broadcasts parameters and buffers from rank 0 (replicas start identical);
+* construction broadcasts parameters and buffers from rank 0 (replicas start identical); every
+  forward re-broadcasts the buffers (BatchNorm running stats) coalesced, one collective per dtype;
 * gradients live in flat per-bucket buffers (``p.grad`` are zero-copy views, shared with the fused
   optimizer), buckets are filled in REVERSE registration order (the order backward produces them)
   and capped at ``bucket_cap_mb``;
@@ -88,9 +89,8 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *inputs, **kwargs):
         if self.broadcast_buffers and self.world_size > 1:
             bufs = list(self.module.buffers())
-            if bufs:
-                for b in bufs:
-                    dist.broadcast(b, self.process_group.ranks[0], group=self.process_group)
+            if bufs:      # e.g. BatchNorm running stats: one coalesced broadcast per dtype, not one per buffer
+                dist.broadcast_coalesced(bufs, self.process_group.ranks[0], group=self.process_group)
         return self.module(*inputs, **kwargs)
 
     @contextlib.contextmanager

@@ -23,3 +23,13 @@ def test_peer_engine_ranks_stay_identical(mode, overlap):
     assert rc == 0, "\n".join(logs)
     assert res[0]["params"] == res[1]["params"], "replicas diverged"
     assert res[0]["grads"][0] > 0
+
+
+@pytest.mark.parametrize("model", ["gpt2", "resnet"])
+def test_ddp_model_replicas_identical(model):
+    """DDP of the driver-added configs over 2 ranks (sharing one GPU, gloo transport)."""
+    rc, res, logs = run_ranks("ddp_model", 2, model, "3")
+    assert rc == 0, "\n".join(logs)
+    assert res[0]["n_buckets"] > 1
+    assert res[0]["params"] == res[1]["params"], "replicas diverged"
+    assert res[0]["buffers"] == res[1]["buffers"], "buffers not broadcast"
