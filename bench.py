@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo control group, peer all-reduce for the data")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the W>1 communication path (buckets, routes, split optimizer) even at W=1")
+    ap.add_argument("--no-autotune", action="store_true", help="W>1: skip the whole-step schedule autotuning")
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--model", choices=["lenet", "gpt2", "resnet18"], default="lenet",
@@ -64,21 +67,24 @@ def main():
     from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_mnist
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
     from pytorch_distributed_example_amd.models import build_net
+    from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
     if args.shared_gpu:
         local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     comm = None
-    if world > 1:
-        dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method="env://", rank=rank,
-                                world_size=world)
-        comm = dist.engine_comm(allow_host_only=args.shared_gpu)
-
-    net = build_net(seed=args.seed, device=dev)
-    if comm is not None:
-        dist.broadcast_parameters(net)            # DDP semantics: replicas start identical
-    eng = LeNetTrainStep(net, batch_size=args.batch_size, lr=1e-3, comm=comm, overlap=not args.no_overlap)
+    with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
+        if world > 1 or args.force_comm:
+            init = "env://" if "MASTER_PORT" in os.environ else "tcp://127.0.0.1:29533"
+            dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method=init, rank=rank,
+                                    world_size=world)
+            comm = dist.engine_comm(allow_host_only=args.shared_gpu)
+        net = build_net(seed=args.seed, device=dev)
+        if comm is not None:
+            dist.broadcast_parameters(net)            # DDP semantics: replicas start identical
+        eng = LeNetTrainStep(net, batch_size=args.batch_size, lr=1e-3, comm=comm, overlap=not args.no_overlap,
+                             force_comm=args.force_comm)
     routes = {}
     if comm is not None and eng.comm_on:
         routes = {"routes": {str(k): v for k, v in comm.routes.items()},
@@ -104,6 +110,10 @@ def main():
             for _ in range(n):
                 eng.step()
 
+    if eng.comm_on and not args.no_autotune:
+        # time every communication schedule (bucket routes x overlap) on whole steps, keep the fastest
+        routes["schedule_us_per_step"] = eng.autotune_schedule(graph_steps=S)
+        routes["schedule"] = eng.schedule
     if args.mode == "graph":
         eng.capture(steps=S)
         eng.capture(steps=1)
@@ -152,7 +162,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "optimizer": "Adam(lr=1e-3)",
                 "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
-                "grad_allreduce": "none" if world == 1 else ("bucketed-overlap" if not args.no_overlap else "flat"),
+                "grad_allreduce": "none" if not eng.comm_on else eng.mode,
                 **routes,
             },
             "comm_errors": health or None,

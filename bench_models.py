@@ -27,9 +27,13 @@ def _setup():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
+
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
+        with stdout_to_stderr():                  # RCCL's init banner must not precede the JSON line
+            dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
+            dist.barrier()
     return torch, dist, rank, world, torch.device("cuda", local_rank)
 
 

@@ -193,8 +193,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("pending", &CommWatchdog::pending)
       .def("stop", &CommWatchdog::stop, py::call_guard<py::gil_scoped_release>());
   py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce")
-      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("capacity_bytes"), py::call_guard<py::gil_scoped_release>())
+      .def(py::init<int, int, int, int64_t, bool>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("capacity_bytes"), py::arg("uncached_data") = false, py::call_guard<py::gil_scoped_release>())
       .def("handle", [](PeerAllReduce& p) { return py::bytes(p.handle()); })
       .def("open",
            [](PeerAllReduce& p, const std::vector<py::bytes>& hs) {

@@ -15,9 +15,13 @@
 // rewrites stage[par] two calls later, and it can only get there after every peer has passed the
 // next call's first barrier, i.e. finished this call.  Barriers are per block index (block b of
 // every rank owns the same slices), flags hold the monotonically increasing global call number.
-// All IPC memory is allocated uncached (hipDeviceMallocUncached) so loads of peer data and flags
-// never hit a stale L2 line (each of the 8 XCDs has its own L2).  Spins are bounded by a wall-clock
-// timeout (s_memrealtime): a dead peer latches an error word instead of hanging the GPU.
+// Flags live in uncached memory (hipDeviceMallocUncached: a spinning load always sees the peer's
+// store).  stage/res are ordinary device memory by default: the signalling store is a system-scope
+// release (L2 write-back of this XCD after every wave drained its stores) and the waiter does a
+// system-scope acquire (L2 invalidate) before touching peer data, so no stale line is read on any
+// of the 8 per-XCD L2s; ``uncached_data`` allocates them uncached instead (slower local traffic).
+// Spins are bounded by a wall-clock timeout (s_memrealtime): a dead peer latches an error word
+// instead of hanging the GPU.
 //
 // Calls on one PeerAllReduce must be ordered on a single stream (the engine's comm stream) and be
 // issued by every rank in the same order with the same sizes (collective semantics); launches are
@@ -32,13 +36,13 @@
 namespace pde {
 
 constexpr int kPeerMaxRanks = 8;
-constexpr int kPeerMaxBlocks = 128;
+constexpr int kPeerMaxBlocks = 256;
 
 class PeerAllReduce {
  public:
-  PeerAllReduce(int rank, int world, int device, int64_t capacity_bytes);
+  PeerAllReduce(int rank, int world, int device, int64_t capacity_bytes, bool uncached_data = false);
   ~PeerAllReduce();
-  // IPC handle (bytes) of this rank's shared region; exchanged through the store by the caller.
+  // IPC handles (bytes: flags | data) of this rank's shared regions; exchanged through the store.
   std::string handle() const;
   // Map every peer's region (handles indexed by rank; this rank's own entry is ignored).
   void open(const std::vector<std::string>& handles);
@@ -64,9 +68,12 @@ class PeerAllReduce {
   int rank_, world_, device_;
   int64_t cap_;                 // bytes per stage / res buffer
   int64_t region_bytes_ = 0;
-  uint8_t* region_ = nullptr;   // own shared region: flags | stage0 | stage1 | res0 | res1
+  bool uncached_data_ = false;
+  uint8_t* flags_ = nullptr;    // own flag region (uncached)
+  uint8_t* region_ = nullptr;   // own data region: stage0 | stage1 | res0 | res1
   uint32_t* ctrl_ = nullptr;    // local (not shared): [0] call counter, [1] done counter, [2] error count
   uint8_t* peers_[kPeerMaxRanks] = {};
+  uint8_t* peer_flags_[kPeerMaxRanks] = {};
   bool opened_ = false;
   int64_t timeout_ticks_ = 10LL * 100000000;   // 10 s
   int64_t one_shot_max_ = 256 * 1024;

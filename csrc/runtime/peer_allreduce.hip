@@ -16,12 +16,20 @@ void hip_check(hipError_t e, const char* what) {
 }
 
 constexpr int kThreads = 512;                 // 8 waves per block
-constexpr int64_t kFlagBytes = 64 * 1024;     // flags[2 phases][kPeerMaxBlocks][kPeerMaxRanks] u32 (8 KB used)
+constexpr int64_t kFlagBytes = 64 * 1024;     // flags[2 phases][kPeerMaxBlocks][kPeerMaxRanks] u32 (16 KB used)
+constexpr int kHandle = sizeof(hipIpcMemHandle_t);
+// 16-byte vector as a clang vector type: arrays of HIP's struct vec_t defeat SROA and land in scratch
+typedef unsigned int vec_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ vec_t mkvec(unsigned a, unsigned b, unsigned c, unsigned d) {
+  vec_t v = {a, b, c, d};
+  return v;
+}
 
 struct Args {
-  uint8_t* base[kPeerMaxRanks];   // every rank's shared region (base[rank] = own)
-  const uint4* in;
-  uint4* out;
+  uint8_t* flags[kPeerMaxRanks];  // every rank's flag region (uncached; [rank] = own)
+  uint8_t* data[kPeerMaxRanks];   // every rank's stage0 | stage1 | res0 | res1 region
+  const vec_t* in;
+  vec_t* out;
   uint32_t* ctrl;                 // [0] completed calls, [1] blocks done in this call, [2] timeouts
   int64_t n4;                     // 16-byte vectors
   int64_t tail;                   // trailing elements (< elements per vector)
@@ -36,10 +44,10 @@ __device__ __forceinline__ uint32_t* flag_ptr(uint8_t* region, int phase, int bl
   return reinterpret_cast<uint32_t*>(region) + (phase * kPeerMaxBlocks + block) * kPeerMaxRanks + src;
 }
 __device__ __forceinline__ uint8_t* stage_ptr(uint8_t* region, int64_t cap, uint32_t par) {
-  return region + kFlagBytes + par * cap;
+  return region + par * cap;
 }
 __device__ __forceinline__ uint8_t* res_ptr(uint8_t* region, int64_t cap, uint32_t par) {
-  return region + kFlagBytes + (2 + par) * cap;
+  return region + (2 + par) * cap;
 }
 
 // Block-level barrier between block b of every rank: publish `target` into every peer's flag slot
@@ -51,9 +59,10 @@ __device__ __forceinline__ void peer_barrier(const Args& a, int phase, uint32_t 
   __syncthreads();
   const int t = threadIdx.x;
   if (t < W) {
-    __hip_atomic_store(flag_ptr(a.base[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELEASE,
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: write back this XCD's L2
+    __hip_atomic_store(flag_ptr(a.flags[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t* mine = flag_ptr(a.base[a.rank], phase, blockIdx.x, t);
+    uint32_t* mine = flag_ptr(a.flags[a.rank], phase, blockIdx.x, t);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int spins = 0;
     // after a time-out the communicator is poisoned: signal, never wait again (fail fast, no hang)
@@ -77,12 +86,12 @@ struct F32Op {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = 0.f;
   }
-  static __device__ __forceinline__ void add(float* acc, uint4 v) {
+  static __device__ __forceinline__ void add(float* acc, vec_t v) {
     acc[0] += __uint_as_float(v.x); acc[1] += __uint_as_float(v.y);
     acc[2] += __uint_as_float(v.z); acc[3] += __uint_as_float(v.w);
   }
-  static __device__ __forceinline__ uint4 pack(const float* acc, float s) {
-    return make_uint4(__float_as_uint(acc[0] * s), __float_as_uint(acc[1] * s), __float_as_uint(acc[2] * s),
+  static __device__ __forceinline__ vec_t pack(const float* acc, float s) {
+    return mkvec(__float_as_uint(acc[0] * s), __float_as_uint(acc[1] * s), __float_as_uint(acc[2] * s),
                       __float_as_uint(acc[3] * s));
   }
   static constexpr int kAcc = 4;
@@ -103,7 +112,7 @@ struct BF16Op {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
   }
-  static __device__ __forceinline__ void add(float* acc, uint4 v) {
+  static __device__ __forceinline__ void add(float* acc, vec_t v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -118,8 +127,8 @@ struct BF16Op {
     v[1] = (__bf16)b;
     return __builtin_bit_cast(uint32_t, v);
   }
-  static __device__ __forceinline__ uint4 pack(const float* acc, float s) {
-    return make_uint4(pk(acc[0] * s, acc[1] * s), pk(acc[2] * s, acc[3] * s), pk(acc[4] * s, acc[5] * s),
+  static __device__ __forceinline__ vec_t pack(const float* acc, float s) {
+    return mkvec(pk(acc[0] * s, acc[1] * s), pk(acc[2] * s, acc[3] * s), pk(acc[4] * s, acc[5] * s),
                       pk(acc[6] * s, acc[7] * s));
   }
   static constexpr int kAcc = 8;
@@ -135,20 +144,42 @@ struct BF16Op {
   }
 };
 
-// Sum slice element i (vector index) over every rank's buffer at byte offset `off` of region + buf.
+// Sum vector i over every rank's stage[par] in fixed rank order (bit-identical on every rank).
 template <int W, typename Op>
-__device__ __forceinline__ uint4 reduce_vec(const Args& a, uint32_t par, int64_t i, bool res) {
-  uint4 v[W];
-#pragma unroll
-  for (int p = 0; p < W; ++p) {   // all W loads in flight before the first add
-    const uint8_t* src = res ? res_ptr(a.base[p], a.cap, par) : stage_ptr(a.base[p], a.cap, par);
-    v[p] = reinterpret_cast<const uint4*>(src)[i];
-  }
+__device__ __forceinline__ vec_t sum_ranks(const vec_t (&v)[W], float scale) {
   float acc[Op::kAcc];
   Op::zero(acc);
 #pragma unroll
-  for (int p = 0; p < W; ++p) Op::add(acc, v[p]);   // fixed rank order: bit-identical on every rank
-  return Op::pack(acc, a.scale);
+  for (int p = 0; p < W; ++p) Op::add(acc, v[p]);
+  return Op::pack(acc, scale);
+}
+
+// out[i] (and res[i] when given) = sum over ranks of stage_p[i] for i in [lo, lo + len), this
+// thread's grid-stride share, two vectors per iteration: 2W independent loads in flight.
+template <int W, typename Op>
+__device__ __forceinline__ void reduce_range(const Args& a, uint32_t par, int64_t lo, int64_t len, int64_t t0,
+                                             int64_t stride, vec_t* res) {
+  const vec_t* st[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) st[p] = reinterpret_cast<const vec_t*>(stage_ptr(a.data[p], a.cap, par)) + lo;
+  for (int64_t i = t0; i < len; i += 2 * stride) {
+    const int64_t j = i + stride;
+    const int64_t jj = j < len ? j : i;
+    vec_t v0[W], v1[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      v0[p] = st[p][i];
+      v1[p] = st[p][jj];
+    }
+    const vec_t r0 = sum_ranks<W, Op>(v0, a.scale);
+    const vec_t r1 = sum_ranks<W, Op>(v1, a.scale);
+    a.out[lo + i] = r0;
+    if (res) res[lo + i] = r0;
+    if (j < len) {
+      a.out[lo + j] = r1;
+      if (res) res[lo + j] = r1;
+    }
+  }
 }
 
 template <int W, bool TWO, typename Op>
@@ -164,47 +195,60 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
   const uint32_t par = call & 1u, target = call + 1u;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int nchunks = TWO ? W : 1;
-  uint8_t* my_stage = stage_ptr(a.base[a.rank], a.cap, par);
+  constexpr int NC = TWO ? W : 1;                    // chunks
+  constexpr int U = NC >= 8 ? 1 : 8 / NC;            // vectors per chunk per iteration: ~8 loads in flight
+  vec_t* my_stage = reinterpret_cast<vec_t*>(stage_ptr(a.data[a.rank], a.cap, par));
+  const int64_t last = a.n4 - 1;
 
-  // 1. stage this rank's input (chunk-relative slices: block b owns the same slices on every rank)
-  for (int c = 0; c < nchunks; ++c) {
-    const int64_t lo = (int64_t)c * a.chunk4;
-    const int64_t len = (lo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
-    for (int64_t i = t0; i < len; i += stride)
-      reinterpret_cast<uint4*>(my_stage)[lo + i] = a.in[lo + i];
+  // 1. stage this rank's input.  Slices are chunk-relative (vector i of every chunk belongs to block
+  //    (i / kThreads) % gridDim.x on every rank), so a block-level barrier suffices below.
+  for (int64_t i = t0; i < a.chunk4; i += U * stride) {
+    vec_t v[NC * U];
+#pragma unroll
+    for (int k = 0; k < NC * U; ++k) {
+      const int64_t g = (int64_t)(k / U) * a.chunk4 + i + (k % U) * stride;
+      v[k] = a.in[g < last ? g : last];             // clamped: every load unconditional
+    }
+    // unconditional stores to the same clamped addresses: an out-of-slice index rewrites an element
+    // with the identical input value (benign), and no branch keeps v[] out of registers
+#pragma unroll
+    for (int k = 0; k < NC * U; ++k) {
+      const int64_t g = (int64_t)(k / U) * a.chunk4 + i + (k % U) * stride;
+      my_stage[g < last ? g : last] = v[k];
+    }
   }
   const int64_t tail_off = a.n4 * Op::kPerVec;
   if (blockIdx.x == 0 && threadIdx.x < a.tail)
-    Op::tail_copy(my_stage, reinterpret_cast<const uint8_t*>(a.in), tail_off + threadIdx.x);
+    Op::tail_copy(reinterpret_cast<uint8_t*>(my_stage), reinterpret_cast<const uint8_t*>(a.in),
+                  tail_off + threadIdx.x);
   peer_barrier<W>(a, 0, target, failed);
 
   if (blockIdx.x == 0 && threadIdx.x < a.tail) {   // tail: every rank reduces it itself, same order
     float acc = 0.f;
-    for (int p = 0; p < W; ++p) Op::tail_add(acc, stage_ptr(a.base[p], a.cap, par), tail_off + threadIdx.x);
+    for (int p = 0; p < W; ++p) Op::tail_add(acc, stage_ptr(a.data[p], a.cap, par), tail_off + threadIdx.x);
     Op::tail_store(reinterpret_cast<uint8_t*>(a.out), tail_off + threadIdx.x, acc * a.scale);
   }
   if (!TWO) {
-    for (int64_t i = t0; i < a.n4; i += stride) a.out[i] = reduce_vec<W, Op>(a, par, i, false);
+    reduce_range<W, Op>(a, par, 0, a.n4, t0, stride, nullptr);
   } else {
     // 2. reduce this rank's chunk from every peer's stage into own res[par] (+ own output)
     const int64_t lo = (int64_t)a.rank * a.chunk4;
     const int64_t len = (lo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
-    uint4* my_res = reinterpret_cast<uint4*>(res_ptr(a.base[a.rank], a.cap, par));
-    for (int64_t i = t0; i < len; i += stride) {
-      const uint4 r = reduce_vec<W, Op>(a, par, lo + i, false);
-      my_res[lo + i] = r;
-      a.out[lo + i] = r;
-    }
+    reduce_range<W, Op>(a, par, lo, len, t0, stride, reinterpret_cast<vec_t*>(res_ptr(a.data[a.rank], a.cap, par)));
     peer_barrier<W>(a, 1, target, failed);
-    // 3. gather every other chunk from its owner's res[par]
+    // 3. gather every chunk from its owner's res[par] (W loads in flight; own chunk already in out)
+    for (int64_t i = t0; i < a.chunk4; i += stride) {
+      vec_t v[W];
 #pragma unroll
-    for (int q = 0; q < W; ++q) {
-      if (q == a.rank) continue;
-      const int64_t qlo = (int64_t)q * a.chunk4;
-      const int64_t qlen = (qlo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > qlo ? a.n4 - qlo : 0);
-      const uint4* src = reinterpret_cast<const uint4*>(res_ptr(a.base[q], a.cap, par));
-      for (int64_t i = t0; i < qlen; i += stride) a.out[qlo + i] = src[qlo + i];
+      for (int q = 0; q < W; ++q) {
+        const int64_t g = (int64_t)q * a.chunk4 + i;
+        v[q] = reinterpret_cast<const vec_t*>(res_ptr(a.data[q], a.cap, par))[g < last ? g : last];
+      }
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const int64_t g = (int64_t)q * a.chunk4 + i;
+        if (q != a.rank && g <= last) a.out[g] = v[q];
+      }
     }
   }
   // call bookkeeping: the last block of this call advances the call number
@@ -242,15 +286,22 @@ void launch_any(int world, const Args& a, bool two, int nb, hipStream_t s) {
 
 }  // namespace
 
-PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_bytes)
-    : rank_(rank), world_(world), device_(device) {
+PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_bytes, bool uncached_data)
+    : rank_(rank), world_(world), device_(device), uncached_data_(uncached_data) {
   if (world < 1 || world > kPeerMaxRanks) throw std::invalid_argument("peer all-reduce supports 1..8 ranks");
   if (rank < 0 || rank >= world) throw std::invalid_argument("bad rank");
   cap_ = (capacity_bytes + 65535) / 65536 * 65536;
-  region_bytes_ = kFlagBytes + 4 * cap_;
+  region_bytes_ = 4 * cap_;
   hip_check(hipSetDevice(device), "hipSetDevice");
+  void* f = nullptr;
+  hip_check(hipExtMallocWithFlags(&f, kFlagBytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(flags)");
+  flags_ = static_cast<uint8_t*>(f);
+  hip_check(hipMemset(flags_, 0, kFlagBytes), "hipMemset");
   void* p = nullptr;
-  hip_check(hipExtMallocWithFlags(&p, region_bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  if (uncached_data)
+    hip_check(hipExtMallocWithFlags(&p, region_bytes_, hipDeviceMallocUncached), "hipExtMallocWithFlags(data)");
+  else
+    hip_check(hipMalloc(&p, region_bytes_), "hipMalloc(data)");
   region_ = static_cast<uint8_t*>(p);
   hip_check(hipMemset(region_, 0, region_bytes_), "hipMemset");
   void* c = nullptr;
@@ -259,6 +310,7 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_b
   hip_check(hipMemset(ctrl_, 0, 256), "hipMemset");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_[rank_] = region_;
+  peer_flags_[rank_] = flags_;
 }
 
 PeerAllReduce::~PeerAllReduce() {
@@ -272,20 +324,27 @@ void PeerAllReduce::close() {
   if (region_ == nullptr) return;
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
-  for (int p = 0; p < world_; ++p)
-    if (p != rank_ && peers_[p] != nullptr) (void)hipIpcCloseMemHandle(peers_[p]);
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    if (peers_[p] != nullptr) (void)hipIpcCloseMemHandle(peers_[p]);
+    if (peer_flags_[p] != nullptr) (void)hipIpcCloseMemHandle(peer_flags_[p]);
+  }
   for (auto& q : peers_) q = nullptr;
+  for (auto& q : peer_flags_) q = nullptr;
   (void)hipFree(region_);
+  (void)hipFree(flags_);
   (void)hipFree(ctrl_);
   region_ = nullptr;
+  flags_ = nullptr;
   ctrl_ = nullptr;
   opened_ = false;
 }
 
 std::string PeerAllReduce::handle() const {
-  hipIpcMemHandle_t h;
-  hip_check(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
-  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+  hipIpcMemHandle_t h[2];
+  hip_check(hipIpcGetMemHandle(&h[0], flags_), "hipIpcGetMemHandle(flags)");
+  hip_check(hipIpcGetMemHandle(&h[1], region_), "hipIpcGetMemHandle(data)");
+  return std::string(reinterpret_cast<const char*>(h), sizeof(h));
 }
 
 void PeerAllReduce::open(const std::vector<std::string>& handles) {
@@ -293,12 +352,15 @@ void PeerAllReduce::open(const std::vector<std::string>& handles) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
-    if (handles[p].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
-    hipIpcMemHandle_t h;
-    std::memcpy(&h, handles[p].data(), sizeof(h));
-    void* ptr = nullptr;
-    hip_check(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    peers_[p] = static_cast<uint8_t*>(ptr);
+    if (handles[p].size() != 2 * kHandle) throw std::invalid_argument("bad IPC handle size");
+    hipIpcMemHandle_t h[2];
+    std::memcpy(h, handles[p].data(), sizeof(h));
+    void* fp = nullptr;
+    void* dp = nullptr;
+    hip_check(hipIpcOpenMemHandle(&fp, h[0], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(flags)");
+    peer_flags_[p] = static_cast<uint8_t*>(fp);
+    hip_check(hipIpcOpenMemHandle(&dp, h[1], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(data)");
+    peers_[p] = static_cast<uint8_t*>(dp);
   }
   opened_ = true;
 }
@@ -312,9 +374,12 @@ void PeerAllReduce::launch(uintptr_t in, uintptr_t out, int64_t count, float sca
   if (count * esize > cap_) throw std::invalid_argument("peer all-reduce buffer exceeds the registered capacity");
   if ((in | out) & 15) throw std::invalid_argument("peer all-reduce needs 16-byte aligned buffers");
   Args a;
-  for (int p = 0; p < kPeerMaxRanks; ++p) a.base[p] = p < world_ ? peers_[p] : nullptr;
-  a.in = reinterpret_cast<const uint4*>(in);
-  a.out = reinterpret_cast<uint4*>(out);
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    a.data[p] = p < world_ ? peers_[p] : nullptr;
+    a.flags[p] = p < world_ ? peer_flags_[p] : nullptr;
+  }
+  a.in = reinterpret_cast<const vec_t*>(in);
+  a.out = reinterpret_cast<vec_t*>(out);
   a.ctrl = ctrl_;
   a.n4 = count / per_vec;
   a.tail = count - a.n4 * per_vec;

@@ -7,8 +7,8 @@ its 2·(W-1) dependent hops, so for small buckets every rank instead reads its p
 directly over the 7 point-to-point xGMI links (one-shot: one barrier; two-shot: reduce-scatter +
 all-gather through peer memory, two barriers).  Large buckets (ResNet-18 / GPT-2) stay on RCCL.
 
-``PeerAllReduce(group)`` is collective over a process group: every rank allocates an uncached
-shared region, exchanges its IPC handle through the group's TCP store, maps every peer's region,
+``PeerAllReduce(group)`` is collective over a process group: every rank allocates a flag region
+(uncached) and a data region (PDE_PEER_UNCACHED=1: uncached too), exchanges their IPC handles through the group's TCP store, maps every peer's region,
 and then runs a self-test of both algorithms (f32 and bf16, ragged sizes) against the exact
 answer.  Any failure on any rank (IPC unsupported, wrong sums, a barrier time-out) disables the
 path on every rank and the caller keeps using RCCL.
@@ -57,7 +57,8 @@ class PeerAllReduce:
         key = f"{group.prefix}/peer_ar/{_SEQ[0]}"
         err = ""
         try:
-            self.native = runtime().PeerAllReduce(self.rank, self.world, self.device.index, int(capacity_bytes))
+            self.native = runtime().PeerAllReduce(self.rank, self.world, self.device.index, int(capacity_bytes),
+                                                  os.environ.get("PDE_PEER_UNCACHED", "0") == "1")
             self.native.set_timeout_ms(int(timeout_ms))
             group.store.set(f"{key}/h{self.rank}", self.native.handle())
             group.store.set(f"{key}/dev{self.rank}", str(self.device.index).encode())

@@ -7,6 +7,9 @@ zero_grad, backward, average_gradients, Adam step, meters) this issues:
                    -> B1 fc backward --(event)--> B2 conv backward --(event)--> [wait comm] -> fused Adam
   comm stream    :                    all_reduce(bucket 0: fc grads, 1.62 MB) | all_reduce(bucket 1: conv grads)
 
+(the "overlap" schedule; W > 1 picks overlap / flat / serial and a route per bucket -- RCCL or the
+xGMI peer kernel -- by timing whole steps on the node: ``autotune_schedule``)
+
 * Gradients live in one flat buffer laid out in bucket order (``parallel.flat``); bucket 0 (fc1/fc2,
   94 % of the bytes) is complete after B1, so its all-reduce overlaps the conv backward (B2).
 * The 1/world_size average of ``average_gradients`` (main.py:122-127) is folded into Adam's
@@ -49,7 +52,11 @@ class LeNetTrainStep:
         self.momentum = float(momentum)
         self.comm = comm
         self.world = comm.world_size if comm is not None else 1
-        self.overlap = overlap
+        # communication schedule (W > 1): "overlap" = fc bucket all-reduced on the comm stream beside
+        # the conv backward; "flat" = one all-reduce on the comm stream after backward; "serial" = one
+        # all-reduce on the compute stream (no cross-stream edges: in a hipGraph each edge between
+        # kernels on different streams measured 5-9 us, see autotune_schedule)
+        self.mode = "overlap" if overlap else "flat"
         # force_comm: run the comm-stream/event path even at world size 1 (1-GPU testing of the W>1 path)
         self.comm_on = comm is not None and (self.world > 1 or force_comm)
         self.K = kernels()
@@ -167,7 +174,7 @@ class LeNetTrainStep:
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)
-        if self.comm_on and self.overlap:
+        if self.comm_on and self.mode == "overlap":
             ev["fc"].record(cur)
             cs.wait_event(ev["fc"])
             with torch.cuda.stream(cs):
@@ -176,9 +183,13 @@ class LeNetTrainStep:
         if not self.comm_on:
             self._opt(0, self.params.numel(), True)
             return
+        if self.mode == "serial":
+            self.comm.all_reduce_(self.grads)
+            self._opt(0, self.params.numel(), True)
+            return
         ev["conv"].record(cur)
         cs.wait_event(ev["conv"])
-        if not self.overlap:
+        if self.mode == "flat":
             with torch.cuda.stream(cs):
                 self.comm.all_reduce_(self.grads)
             cur.wait_stream(cs)
@@ -193,6 +204,10 @@ class LeNetTrainStep:
         self._opt(a0, a1, False)
         cur.wait_stream(cs)
         self._opt(b0, b1, True)
+
+    @property
+    def overlap(self) -> bool:
+        return self.mode == "overlap"
 
     def _batch_size_at(self, b: int) -> int:
         return self.B if b < self.nfull else self.tail
@@ -310,3 +325,70 @@ class LeNetTrainStep:
     def sync_params(self):
         """Re-derive kernel-side weight copies after parameters were changed externally."""
         pack_conv2_weight(self.p["conv2.weight"], self.Wt2)
+
+    # ------------------------------------------------------------------ schedule autotuning (W > 1)
+    def schedule_candidates(self):
+        """(mode, {bucket numel: route}) pairs the comm path can run: bucketed + overlapped with the
+        conv backward (one route per bucket), or one all-reduce after backward on the comm stream
+        ("flat") or on the compute stream ("serial"), one route each."""
+        routes = ["rccl"] if self.comm.group.rccl is not None else []
+        if getattr(self.comm, "peer", None) is not None:
+            routes += ["peer1", "peer2"]
+        n0, n1, nall = (self.bucket_grads[0].numel(), self.bucket_grads[1].numel(), self.grads.numel())
+        out = [("overlap", {n0: a, n1: b}) for a in routes for b in routes]
+        out += [(m, {nall: a}) for m in ("flat", "serial") for a in routes]
+        return out
+
+    def autotune_schedule(self, steps: int = 40, graph_steps: int = 10, candidates=None):
+        """Pick the fastest communication schedule by timing WHOLE training steps on this node.
+
+        Isolated all-reduce timings (``dist.peer.tune_routes``) miss the interaction with the kernels
+        a collective overlaps (a peer kernel co-running with the conv backward competes for CUs, an
+        RCCL kernel may not get a CU until it finishes), so every candidate schedule runs ``steps``
+        real steps (hipGraph replays, as in training); the per-candidate MAX over ranks decides, so
+        every rank picks the same one.  Model / optimizer / data-position state is snapshotted and
+        restored: autotuning does not change training.  Returns {candidate label: us per step}."""
+        if not self.comm_on:
+            return {}
+        cands = candidates or self.schedule_candidates()
+        state = [self.params, self.m, self.counters] + ([self.v] if self.v is not self.m else [])
+        snap = [t.clone() for t in state]
+        saved_idx = None if self.idx is None else (self.idx, self.nfull, self.tail, self.nbatches)
+        if self.idx is None or self.nfull < 1:
+            raise RuntimeError("bind a dataset and set epoch indices before autotune_schedule")
+        g = self.comm.group
+        times = []
+        for mode, routes in cands:
+            self.mode = mode
+            self.comm.routes = dict(routes)
+            self.graphs.clear()
+            self.capture(steps=graph_steps)
+            reps = max(1, steps // graph_steps)
+            self.replay(steps=graph_steps)               # warm
+            torch.cuda.synchronize(self.device)
+            g.host.barrier()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                self.replay(steps=graph_steps)
+            e.record()
+            torch.cuda.synchronize(self.device)
+            times.append(s.elapsed_time(e) * 1e3 / (reps * graph_steps))
+        t = torch.tensor(times, dtype=torch.float64)
+        g.host.allreduce(t.data_ptr(), t.numel(), 1, 3)     # float64 MAX over ranks
+        times = t.tolist()
+        best = min(range(len(cands)), key=lambda i: times[i])
+        self.mode, self.comm.routes = cands[best][0], dict(cands[best][1])
+        self.graphs.clear()
+        # restore the training state the trial steps advanced
+        for t, s0 in zip(state, snap):
+            t.copy_(s0)
+        self.sync_params()
+        self.idx, self.nfull, self.tail, self.nbatches = saved_idx
+        self.loss_sum.zero_()
+        self.correct.zero_()
+        torch.cuda.synchronize(self.device)
+        label = lambda c: c[0] + " " + ",".join(f"{n}:{r}" for n, r in sorted(c[1].items()))
+        self.schedule_times = {label(c): round(x, 2) for c, x in zip(cands, times)}
+        self.schedule = label(cands[best])
+        return self.schedule_times

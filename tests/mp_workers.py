@@ -334,7 +334,7 @@ def case_peer_allreduce(graph="1"):
     dist.destroy_process_group()
 
 
-def case_peer_engine(steps="6", mode="eager", overlap="1"):
+def case_peer_engine(steps="6", mode="eager", overlap="1", autotune="0"):
     """Fused LeNet engine, W ranks sharing one GPU, gradients averaged by the peer all-reduce only."""
     from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
@@ -350,6 +350,10 @@ def case_peer_engine(steps="6", mode="eager", overlap="1"):
     eng.bind_dataset(ds.images, ds.labels)
     s = DistributedSampler(ds, num_replicas=W, rank=R, shuffle=False)
     eng.set_epoch_indices(s.indices_tensor())
+    sched = None
+    if autotune == "1":
+        sched = eng.autotune_schedule(steps=8, graph_steps=2)
+        assert len(sched) == len(eng.schedule_candidates()) and eng.schedule in sched, sched
     if mode == "graph":
         eng.capture(steps=2)
         for _ in range(int(steps) // 2):
@@ -359,7 +363,7 @@ def case_peer_engine(steps="6", mode="eager", overlap="1"):
             eng.step()
     torch.cuda.synchronize()
     assert comm.health() == "", comm.health()
-    emit({"rank": R, "routes": {str(k): v for k, v in comm.routes.items()},
+    emit({"rank": R, "routes": {str(k): v for k, v in comm.routes.items()}, "schedule": sched,
           "params": [p.detach().double().sum().item() for p in net.parameters()],
           "grads": [float(eng.grads.double().abs().sum().item())]})
     dist.destroy_process_group()

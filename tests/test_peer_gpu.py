@@ -33,3 +33,15 @@ def test_ddp_model_replicas_identical(model):
     assert res[0]["n_buckets"] > 1
     assert res[0]["params"] == res[1]["params"], "replicas diverged"
     assert res[0]["buffers"] == res[1]["buffers"], "buffers not broadcast"
+
+
+def test_engine_autotune_restores_training_state():
+    """Whole-step schedule autotuning runs real (graph-replayed) steps for every candidate, then
+    restores params / Adam state / data position: training afterwards matches a run without it."""
+    rc0, res0, logs0 = run_ranks("peer_engine", 2, "6", "eager", "1", "0")
+    rc1, res1, logs1 = run_ranks("peer_engine", 2, "6", "eager", "1", "1")
+    assert rc0 == 0 and rc1 == 0, "\n".join(logs0 + logs1)
+    assert res1[0]["params"] == res1[1]["params"]
+    assert res1[0]["schedule"] == res1[1]["schedule"]
+    for a, b in zip(res0[0]["params"], res1[0]["params"]):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (a, b)
