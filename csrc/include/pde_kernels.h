@@ -28,7 +28,8 @@ hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, 
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,
                               float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride,
                               const float* row_loss, const int* row_hit, double* loss_sum,
-                              unsigned long long* correct, int dbg, hipStream_t st);
+                              unsigned long long* correct, int dbg, const void* peer_dev, float* ar_buf, int64_t ar_n, int ar_two,
+                              hipStream_t st);
 
 // ---- optimizers: csrc/kernels/optim.hip ----
 // fold_*: gradient replicas folded before the update: for e in [fold_off, fold_off + fold_len),

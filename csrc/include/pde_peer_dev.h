@@ -1,0 +1,152 @@
+// Device side of the xGMI peer all-reduce for use inside another kernel ("side blocks").
+//
+// peer_ar_f32_vblock(d, in, out, count, scale, vb, nvb, two_shot) runs virtual block vb of nvb of
+// one all-reduce call (fp32 SUM * scale, in == out allowed) with exactly the protocol of the
+// standalone kernel in csrc/runtime/peer_allreduce.hip (same flag slots, call counter and parity
+// double-buffering), so fused and standalone calls interleave freely on one stream.  All threads of
+// the block must call it; the host kernel must run the SAME nvb virtual blocks on every rank.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pde_peer.h"
+
+namespace pde {
+
+typedef unsigned int peer_vec_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t* peer_flag(uint8_t* region, int phase, int vb, int src) {
+  return reinterpret_cast<uint32_t*>(region) + (phase * kPeerMaxBlocks + vb) * kPeerMaxRanks + src;
+}
+
+// Block barrier with virtual block vb of every rank (see peer_allreduce.hip: peer_barrier).
+__device__ __forceinline__ void peer_vbarrier(const PeerDev& d, int phase, int vb, uint32_t target, bool failed) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): this wave's stores have landed
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < d.world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: write back this XCD's L2
+    __hip_atomic_store(peer_flag(d.flags[t], phase, vb, d.rank), target, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = peer_flag(d.flags[d.rank], phase, vb, t);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int spins = 0;
+    while (!failed && __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == 256) {
+        spins = 0;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > d.timeout) {
+          __hip_atomic_fetch_add(d.ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ peer_vec_t peer_sum(const peer_vec_t (&v)[kPeerMaxRanks], int W, float s) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    if (p < W) {                                  // fixed rank order: bit-identical on every rank
+      a0 += __uint_as_float(v[p].x);
+      a1 += __uint_as_float(v[p].y);
+      a2 += __uint_as_float(v[p].z);
+      a3 += __uint_as_float(v[p].w);
+    }
+  }
+  peer_vec_t r = {__float_as_uint(a0 * s), __float_as_uint(a1 * s), __float_as_uint(a2 * s), __float_as_uint(a3 * s)};
+  return r;
+}
+
+// lds2: two words of the caller's LDS (no __shared__ object of our own: a second LDS object next to a
+// kernel's single staging array can change how hipcc schedules that kernel).
+__device__ void peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* out_f, int64_t count, float scale,
+                                   int vb, int nvb, bool two_shot, uint32_t* lds2) {
+  const int T = blockDim.x;
+  __syncthreads();                                // lds2 may alias LDS the caller just used
+  if (threadIdx.x == 0) {
+    lds2[0] = __hip_atomic_load(d.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lds2[1] = __hip_atomic_load(d.ctrl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t call = lds2[0], par = call & 1u, target = call + 1u;
+  const bool failed = lds2[1] != 0;
+  const int W = d.world;
+  const peer_vec_t* in = reinterpret_cast<const peer_vec_t*>(in_f);
+  peer_vec_t* out = reinterpret_cast<peer_vec_t*>(out_f);
+  const int64_t n4 = count / 4, tail = count - n4 * 4, last = n4 - 1;
+  const int NC = two_shot ? W : 1;
+  const int64_t chunk4 = two_shot ? (n4 + W - 1) / W : n4;
+  const int64_t stride = (int64_t)nvb * T, t0 = (int64_t)vb * T + threadIdx.x;
+  peer_vec_t* stage[kPeerMaxRanks];
+  peer_vec_t* res[kPeerMaxRanks];
+#pragma unroll
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    const int q = p < W ? p : 0;
+    stage[p] = reinterpret_cast<peer_vec_t*>(d.data[q] + par * d.cap);
+    res[p] = reinterpret_cast<peer_vec_t*>(d.data[q] + (2 + par) * d.cap);
+  }
+  peer_vec_t* my_stage = reinterpret_cast<peer_vec_t*>(d.data[d.rank] + par * d.cap);
+  // 1. stage the input: vector i of every chunk (chunk-relative) belongs to virtual block (i / T) % nvb
+  for (int64_t i = t0; i < chunk4; i += stride) {
+    peer_vec_t v[kPeerMaxRanks];
+#pragma unroll
+    for (int c = 0; c < kPeerMaxRanks; ++c) {      // c < NC is wave-uniform: scalar branches
+      const int64_t g = (int64_t)c * chunk4 + i;
+      if (c < NC) v[c] = in[g < last ? g : last];
+    }
+#pragma unroll
+    for (int c = 0; c < kPeerMaxRanks; ++c) {
+      const int64_t g = (int64_t)c * chunk4 + i;
+      if (c < NC) my_stage[g < last ? g : last] = v[c];   // clamped duplicates rewrite identical values
+    }
+  }
+  if (vb == 0 && threadIdx.x < tail) reinterpret_cast<float*>(my_stage)[n4 * 4 + threadIdx.x] = in_f[n4 * 4 + threadIdx.x];
+  peer_vbarrier(d, 0, vb, target, failed);
+  if (vb == 0 && threadIdx.x < tail) {
+    float acc = 0.f;
+    for (int p = 0; p < W; ++p) acc += reinterpret_cast<const float*>(stage[p])[n4 * 4 + threadIdx.x];
+    out_f[n4 * 4 + threadIdx.x] = acc * scale;
+  }
+  const int64_t lo = two_shot ? (int64_t)d.rank * chunk4 : 0;
+  const int64_t len = two_shot ? ((lo + chunk4 <= n4) ? chunk4 : (n4 > lo ? n4 - lo : 0)) : n4;
+  // 2. reduce [lo, lo + len) over every rank's stage (own chunk when two-shot)
+  for (int64_t i = t0; i < len; i += stride) {
+    peer_vec_t v[kPeerMaxRanks];
+#pragma unroll
+    for (int p = 0; p < kPeerMaxRanks; ++p)
+      if (p < W) v[p] = stage[p][lo + i];
+    const peer_vec_t r = peer_sum(v, W, scale);
+    out[lo + i] = r;
+    if (two_shot) reinterpret_cast<peer_vec_t*>(d.data[d.rank] + (2 + par) * d.cap)[lo + i] = r;
+  }
+  if (two_shot) {
+    peer_vbarrier(d, 1, vb, target, failed);
+    // 3. gather every other chunk from its owner's res[par]
+    for (int64_t i = t0; i < chunk4; i += stride) {
+      peer_vec_t v[kPeerMaxRanks];
+#pragma unroll
+      for (int q = 0; q < kPeerMaxRanks; ++q) {
+        const int64_t g = (int64_t)q * chunk4 + i;
+        if (q < W) v[q] = res[q][g < last ? g : last];
+      }
+#pragma unroll
+      for (int q = 0; q < kPeerMaxRanks; ++q) {
+        const int64_t g = (int64_t)q * chunk4 + i;
+        if (q < W && q != d.rank && g <= last) out[g] = v[q];
+      }
+    }
+  }
+  // call bookkeeping: the last virtual block of this call advances the call number
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(d.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nvb - 1) {
+      __hip_atomic_store(d.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace pde

@@ -25,6 +25,10 @@
 //   Wt2  [500][64] conv2 weight repacked: row k' = (kh*5+kw)*20+ci, column co (zero for co >= 50)
 #include "pde_hip.h"
 #include "pde_kernels.h"
+#include "pde_peer_dev.h"
+
+#include <algorithm>
+#include <cstring>
 
 namespace {
 
@@ -620,7 +624,13 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
                                                   float* __restrict__ gW2c, float* __restrict__ gb2c,
                                                   int c1_nrep, int c1_rep_stride, const float* __restrict__ row_loss,
                                                   const int* __restrict__ row_hit, double* __restrict__ loss_sum,
-                                                  unsigned long long* __restrict__ correct, int dbg) {
+                                                  unsigned long long* __restrict__ correct, int dbg,
+                                                  pde::PeerDev pd, float* __restrict__ ar_buf, int64_t ar_n,
+                                                  int ar_nvb, int ar_two) {
+  // Side blocks (ar_nvb > 0, the W > 1 "fused" schedule): the first ar_nvb blocks after the meters
+  // block all-reduce the fc-gradient bucket (complete since fc_bwd) across ranks with the xGMI peer
+  // protocol while the other blocks compute the conv gradients -- comm/compute overlap with no
+  // extra launch and no cross-stream edge in the graph.
   // conv1 grads go to replica (b % c1_nrep) at a stride of c1_rep_stride floats (the consumer folds
   // the replicas): 128 images adding into 520 addresses was the single largest cost (17 us).
   // dbg (ablation only; 0 in production): 1 skip role W, 2 skip role D, 4 no global atomics,
@@ -661,6 +671,14 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
       return;
     }
     bid -= 1;
+  }
+  if (ar_nvb > 0) {
+    if (bid < ar_nvb) {
+      pde::peer_ar_f32_vblock(pd, ar_buf, ar_buf, ar_n, 1.f, bid, ar_nvb, ar_two != 0,
+                              reinterpret_cast<uint32_t*>(smem));
+      return;
+    }
+    bid -= ar_nvb;
   }
   if (bid < nW) {
     if (dbg & 1) return;
@@ -918,12 +936,21 @@ hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, 
                               const float* dP2m, const uint8_t* A2, const float* W2c, int B, float* gW1c,
                               float* gb1c, float* gW2c, float* gb2c, int c1_nrep, int c1_rep_stride,
                               const float* row_loss, const int* row_hit, double* loss_sum,
-                              unsigned long long* correct, int dbg, hipStream_t st) {
+                              unsigned long long* correct, int dbg, const void* peer_dev, float* ar_buf,
+                              int64_t ar_n, int ar_two, hipStream_t st) {
   const int meters = (loss_sum && correct && row_loss && row_hit) ? 1 : 0;
-  const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B + meters;
+  pde::PeerDev pd{};
+  int ar_nvb = 0;
+  if (peer_dev != nullptr && ar_buf != nullptr && ar_n > 0) {
+    std::memcpy(&pd, peer_dev, sizeof(pd));
+    const int64_t n4 = ar_n / 4, work = ar_two ? (n4 + pd.world - 1) / pd.world : n4;
+    ar_nvb = (int)std::min<int64_t>(64, std::max<int64_t>(1, (work + 511) / 512));
+  }
+  const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B + meters + ar_nvb;
   hipLaunchKernelGGL(k_conv_bwd, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
                      gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, meters ? row_loss : nullptr,
-                     meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg);
+                     meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg, pd,
+                     ar_buf, ar_n, ar_nvb, ar_two);
   return hipGetLastError();
 }
 

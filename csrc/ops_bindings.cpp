@@ -12,6 +12,7 @@
 
 #include "pde_kernels.h"
 #include "pde_bind.h"
+#include "pde_peer.h"
 
 namespace {
 
@@ -150,9 +151,27 @@ void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tenso
                     const at::Tensor& dP2m, const at::Tensor& A2, const at::Tensor& W2c, int64_t B,
                     const at::Tensor& gW1c, const at::Tensor& gb1c, const at::Tensor& gW2c, const at::Tensor& gb2c,
                     int64_t c1_nrep, int64_t c1_rep_stride, const OptT& row_loss, const OptT& row_hit,
-                    const OptT& loss_sum, const OptT& correct, int64_t dbg) {
+                    const OptT& loss_sum, const OptT& correct, int64_t dbg, const OptT& peer_dev,
+                    const OptT& ar_buf, int64_t ar_two) {
   check_cuda(X, "X", F32);
   check_cuda(rows, "rows", I32, B);
+  // fused all-reduce side blocks: peer_dev = CPU uint8 bytes of a pde::PeerDev, ar_buf = fc bucket
+  const void* pdev = nullptr;
+  float* arp = nullptr;
+  int64_t arn = 0;
+  if (peer_dev.has_value() && peer_dev->defined()) {
+    TORCH_CHECK(!peer_dev->is_cuda() && peer_dev->scalar_type() == at::kByte &&
+                    peer_dev->numel() == (int64_t)sizeof(pde::PeerDev) && peer_dev->is_contiguous(),
+                "peer_dev must be the CPU uint8 bytes of PeerAllReduce.device_args()");
+    TORCH_CHECK(ar_buf.has_value() && ar_buf->defined(), "ar_buf required with peer_dev");
+    check_cuda(*ar_buf, "ar_buf", F32, 1);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(ar_buf->data_ptr()) % 16 == 0, "ar_buf must be 16-byte aligned");
+    pdev = peer_dev->data_ptr();
+    arp = ar_buf->data_ptr<float>();
+    arn = ar_buf->numel();
+    const auto* pd = static_cast<const pde::PeerDev*>(pdev);
+    TORCH_CHECK(arn * 4 <= pd->cap, "ar_buf exceeds the peer all-reduce capacity");
+  }
   check_cuda(P1, "P1", F32, B * 2880);
   check_cuda(A1, "A1", U8, B * 2880);
   check_cuda(dP2m, "dP2m", F32, B * 800);
@@ -171,7 +190,8 @@ void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tenso
                                ptr<float>(gW2c), ptr<float>(gb2c), (int)c1_nrep, (int)c1_rep_stride,
                                optr<float>(row_loss, "row_loss", F32, B), optr<int>(row_hit, "row_hit", I32, B),
                                optr<double>(loss_sum, "loss_sum", F64, 1),
-                               optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, cur_stream()),
+                               optr<unsigned long long>(correct, "correct", I64, 1), (int)dbg, pdev, arp, arn,
+                               (int)ar_two, cur_stream()),
             "lenet_conv_bwd");
 }
 
@@ -393,7 +413,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("gW2c"), py::arg("gb2c"),
         py::arg("c1_nrep") = 1, py::arg("c1_rep_stride") = 0, py::arg("row_loss") = py::none(),
         py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(), py::arg("correct") = py::none(),
-        py::arg("dbg") = 0);
+        py::arg("dbg") = 0, py::arg("peer_dev") = py::none(), py::arg("ar_buf") = py::none(), py::arg("ar_two") = 1);
   m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("decoupled"), py::arg("grad_scale"), py::arg("step"),
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),

@@ -212,6 +212,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("world", &PeerAllReduce::world)
       .def_property_readonly("device", &PeerAllReduce::device)
       .def_property_readonly("is_open", &PeerAllReduce::is_open)
+      .def("device_args", [](PeerAllReduce& p) { return py::bytes(p.device_args()); })
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
       .def("reset_error", &PeerAllReduce::reset_error)
       .def("set_timeout_ms", &PeerAllReduce::set_timeout_ms)

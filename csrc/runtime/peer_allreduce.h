@@ -33,10 +33,9 @@
 #include <string>
 #include <vector>
 
-namespace pde {
+#include "pde_peer.h"
 
-constexpr int kPeerMaxRanks = 8;
-constexpr int kPeerMaxBlocks = 256;
+namespace pde {
 
 class PeerAllReduce {
  public:
@@ -56,6 +55,9 @@ class PeerAllReduce {
   int device() const { return device_; }
   bool is_open() const { return opened_; }
   // 0 = healthy; otherwise the number of timed-out barrier waits since the last reset (synchronises).
+  // Device-side view (flags/data of every rank, ctrl) for kernels that run the algorithm in side
+  // blocks (pde_peer_dev.h); raw bytes of a PeerDev struct.
+  std::string device_args() const;
   int64_t error();
   void reset_error();
   void set_timeout_ms(int64_t ms) { timeout_ticks_ = ms * 100000; }   // s_memrealtime runs at 100 MHz

@@ -16,7 +16,7 @@ void hip_check(hipError_t e, const char* what) {
 }
 
 constexpr int kThreads = 512;                 // 8 waves per block
-constexpr int64_t kFlagBytes = 64 * 1024;     // flags[2 phases][kPeerMaxBlocks][kPeerMaxRanks] u32 (16 KB used)
+constexpr int64_t kFlagBytes = kPeerFlagBytes;   // flags[2 phases][kPeerMaxBlocks][kPeerMaxRanks] u32 (16 KB used)
 constexpr int kHandle = sizeof(hipIpcMemHandle_t);
 // 16-byte vector as a clang vector type: arrays of HIP's struct vec_t defeat SROA and land in scratch
 typedef unsigned int vec_t __attribute__((ext_vector_type(4)));
@@ -409,6 +409,21 @@ void PeerAllReduce::all_reduce_f32(uintptr_t in, uintptr_t out, int64_t count, f
 void PeerAllReduce::all_reduce_bf16(uintptr_t in, uintptr_t out, int64_t count, float scale, int algo,
                                     uintptr_t stream) {
   launch(in, out, count, scale, algo, stream, true);
+}
+
+std::string PeerAllReduce::device_args() const {
+  if (!opened_) throw std::runtime_error("peer all-reduce used before open()");
+  PeerDev d{};
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    d.flags[p] = p < world_ ? peer_flags_[p] : nullptr;
+    d.data[p] = p < world_ ? peers_[p] : nullptr;
+  }
+  d.ctrl = ctrl_;
+  d.cap = cap_;
+  d.timeout = timeout_ticks_;
+  d.rank = rank_;
+  d.world = world_;
+  return std::string(reinterpret_cast<const char*>(&d), sizeof(d));
 }
 
 int64_t PeerAllReduce::error() {

@@ -55,8 +55,11 @@ class LeNetTrainStep:
         # communication schedule (W > 1): "overlap" = fc bucket all-reduced on the comm stream beside
         # the conv backward; "flat" = one all-reduce on the comm stream after backward; "serial" = one
         # all-reduce on the compute stream (no cross-stream edges: in a hipGraph each edge between
-        # kernels on different streams measured 5-9 us, see autotune_schedule)
+        # kernels on different streams measured 5-9 us, see autotune_schedule); "fused" = the fc
+        # bucket is all-reduced by side blocks of the conv backward kernel (xGMI peer protocol), the
+        # conv bucket after it on the compute stream
         self.mode = "overlap" if overlap else "flat"
+        self._peer_dev = None
         # force_comm: run the comm-stream/event path even at world size 1 (1-GPU testing of the W>1 path)
         self.comm_on = comm is not None and (self.world > 1 or force_comm)
         self.K = kernels()
@@ -174,6 +177,12 @@ class LeNetTrainStep:
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)
+        if self.comm_on and self.mode == "fused":
+            fc_route = self.comm.routes.get(self.bucket_grads[0].numel(), "peer2")
+            K.lenet_conv_bwd(*conv_args, 0, self._peer_device_args(), self.bucket_grads[0], int(fc_route == "peer2"))
+            self.comm.all_reduce_(self.bucket_grads[1])
+            self._opt(0, self.params.numel(), True)
+            return
         if self.comm_on and self.mode == "overlap":
             ev["fc"].record(cur)
             cs.wait_event(ev["fc"])
@@ -204,6 +213,14 @@ class LeNetTrainStep:
         self._opt(a0, a1, False)
         cur.wait_stream(cs)
         self._opt(b0, b1, True)
+
+    def _peer_device_args(self):
+        if self._peer_dev is None:
+            peer = getattr(self.comm, "peer", None)
+            if peer is None or peer.native is None:
+                raise RuntimeError("the fused schedule needs the xGMI peer all-reduce")
+            self._peer_dev = torch.frombuffer(bytearray(peer.native.device_args()), dtype=torch.uint8)
+        return self._peer_dev
 
     @property
     def overlap(self) -> bool:
@@ -337,6 +354,8 @@ class LeNetTrainStep:
         n0, n1, nall = (self.bucket_grads[0].numel(), self.bucket_grads[1].numel(), self.grads.numel())
         out = [("overlap", {n0: a, n1: b}) for a in routes for b in routes]
         out += [(m, {nall: a}) for m in ("flat", "serial") for a in routes]
+        if getattr(self.comm, "peer", None) is not None:
+            out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in routes]
         return out
 
     def autotune_schedule(self, steps: int = 40, graph_steps: int = 10, candidates=None):
@@ -357,8 +376,21 @@ class LeNetTrainStep:
         if self.idx is None or self.nfull < 1:
             raise RuntimeError("bind a dataset and set epoch indices before autotune_schedule")
         g = self.comm.group
-        times = []
+        times, invalid = [], []
+        peer = getattr(self.comm, "peer", None)
+        wd = g.watchdog
         for mode, routes in cands:
+            uses_peer = mode == "fused" or any(r != "rccl" for r in routes.values())
+            perr0 = peer.error() if peer is not None else 0
+            anyerr = torch.tensor([perr0], dtype=torch.int64)
+            g.host.allreduce(anyerr.data_ptr(), 1, 3, 3)      # collective decision: every rank skips alike
+            if uses_peer and anyerr.item():      # a timed-out peer protocol is poisoned: never pick it
+                times.append(float("inf"))
+                invalid.append(1)
+                continue
+            for t, s0 in zip(state, snap):       # every candidate starts from the same (replicated) state
+                t.copy_(s0)
+            self.sync_params()
             self.mode = mode
             self.comm.routes = dict(routes)
             self.graphs.clear()
@@ -374,9 +406,21 @@ class LeNetTrainStep:
             e.record()
             torch.cuda.synchronize(self.device)
             times.append(s.elapsed_time(e) * 1e3 / (reps * graph_steps))
+            # safety net: a schedule must leave every replica bit-identical and report no comm error
+            bits = self.params.view(torch.int32).to(torch.int64).sum().item()
+            failed = (peer is not None and peer.error() > perr0) or (wd is not None and bool(wd.error()))
+            invalid.append(1 if failed else 0)
+            chk = torch.tensor([bits, -bits], dtype=torch.int64)
+            g.host.allreduce(chk.data_ptr(), 2, 3, 3)          # int64 MAX: max(bits) and -min(bits)
+            if chk[0].item() != -chk[1].item():
+                invalid[-1] = 1
         t = torch.tensor(times, dtype=torch.float64)
         g.host.allreduce(t.data_ptr(), t.numel(), 1, 3)     # float64 MAX over ranks
-        times = t.tolist()
+        bad = torch.tensor(invalid, dtype=torch.int64)
+        g.host.allreduce(bad.data_ptr(), bad.numel(), 3, 3)  # int64 MAX: invalid anywhere -> invalid
+        times = [float("inf") if b else x for x, b in zip(t.tolist(), bad.tolist())]
+        if all(x == float("inf") for x in times):
+            raise RuntimeError("no communication schedule kept the replicas identical (comm failure?)")
         best = min(range(len(cands)), key=lambda i: times[i])
         self.mode, self.comm.routes = cands[best][0], dict(cands[best][1])
         self.graphs.clear()
@@ -389,6 +433,6 @@ class LeNetTrainStep:
         self.correct.zero_()
         torch.cuda.synchronize(self.device)
         label = lambda c: c[0] + " " + ",".join(f"{n}:{r}" for n, r in sorted(c[1].items()))
-        self.schedule_times = {label(c): round(x, 2) for c, x in zip(cands, times)}
+        self.schedule_times = {label(c): (round(x, 2) if x != float("inf") else None) for c, x in zip(cands, times)}
         self.schedule = label(cands[best])
         return self.schedule_times

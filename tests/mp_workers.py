@@ -354,6 +354,13 @@ def case_peer_engine(steps="6", mode="eager", overlap="1", autotune="0"):
     if autotune == "1":
         sched = eng.autotune_schedule(steps=8, graph_steps=2)
         assert len(sched) == len(eng.schedule_candidates()) and eng.schedule in sched, sched
+        assert all(v is not None for v in sched.values()), sched      # every schedule kept replicas equal
+    elif autotune.startswith("mode="):
+        # force one schedule, e.g. mode=fused:peer2:peer1 (mode:fc-route:conv-route)
+        mode, r0, r1 = autotune[5:].split(":")
+        eng.mode = mode
+        comm.routes = {eng.bucket_grads[0].numel(): r0, eng.bucket_grads[1].numel(): r1,
+                       eng.grads.numel(): r1}
     if mode == "graph":
         eng.capture(steps=2)
         for _ in range(int(steps) // 2):

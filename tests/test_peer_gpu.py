@@ -45,3 +45,16 @@ def test_engine_autotune_restores_training_state():
     assert res1[0]["schedule"] == res1[1]["schedule"]
     for a, b in zip(res0[0]["params"], res1[0]["params"]):
         assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (a, b)
+
+
+@pytest.mark.parametrize("sched", ["mode=fused:peer2:peer1", "mode=fused:peer1:peer2", "mode=serial:peer2:peer2"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_engine_fused_schedules_match(sched, world):
+    """The fc bucket all-reduced by side blocks of the conv backward (fused) and the serial schedule
+    train exactly like the overlapped reference schedule (same parameters up to fp32 reassociation)."""
+    rc0, res0, logs0 = run_ranks("peer_engine", world, "6", "graph", "1", "0")
+    rc1, res1, logs1 = run_ranks("peer_engine", world, "6", "graph", "1", sched)
+    assert rc0 == 0 and rc1 == 0, "\n".join(logs0 + logs1)
+    assert all(r["params"] == res1[0]["params"] for r in res1), "replicas diverged"
+    for a, b in zip(res0[0]["params"], res1[0]["params"]):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (a, b)
