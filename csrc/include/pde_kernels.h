@@ -37,7 +37,8 @@ hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, 
 hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, float lr, float b1, float b2,
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
                          int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
-                         int fold_nrep, int fold_stride, hipStream_t st);
+                         int fold_nrep, int fold_stride, const void* peer_dev, long long ar_off,
+                         long long* ar_epoch, int ar_two, hipStream_t st);
 hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, float momentum, float dampening,
                         float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
                         long long pack_off, float* pack_dst, long long fold_off, int fold_len, int fold_nrep,

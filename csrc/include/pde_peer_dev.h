@@ -1,6 +1,6 @@
 // Device side of the xGMI peer all-reduce for use inside another kernel ("side blocks").
 //
-// peer_ar_f32_vblock(d, in, out, count, scale, vb, nvb, two_shot) runs virtual block vb of nvb of
+// peer_ar_f32_vblock(d, in, out, count, scale, vb, nvb, two_shot, lds2) runs virtual block vb of nvb of
 // one all-reduce call (fp32 SUM * scale, in == out allowed) with exactly the protocol of the
 // standalone kernel in csrc/runtime/peer_allreduce.hip (same flag slots, call counter and parity
 // double-buffering), so fused and standalone calls interleave freely on one stream.  All threads of
@@ -62,7 +62,7 @@ __device__ __forceinline__ peer_vec_t peer_sum(const peer_vec_t (&v)[kPeerMaxRan
 
 // lds2: two words of the caller's LDS (no __shared__ object of our own: a second LDS object next to a
 // kernel's single staging array can change how hipcc schedules that kernel).
-__device__ void peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* out_f, int64_t count, float scale,
+__device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* out_f, int64_t count, float scale,
                                    int vb, int nvb, bool two_shot, uint32_t* lds2) {
   const int T = blockDim.x;
   __syncthreads();                                // lds2 may alias LDS the caller just used
@@ -139,14 +139,20 @@ __device__ void peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
       }
     }
   }
-  // call bookkeeping: the last virtual block of this call advances the call number
+  // call bookkeeping: the last virtual block of this call advances the call number.  Every wave
+  // drains its output stores first, so a consumer in the SAME kernel that sees the call complete
+  // (agent-scope acquire) reads the reduced values.  Returns true in the thread that completed it.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
+  bool completed = false;
   if (threadIdx.x == 0) {
     if (__hip_atomic_fetch_add(d.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nvb - 1) {
       __hip_atomic_store(d.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(d.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      completed = true;
     }
   }
+  return completed;
 }
 
 }  // namespace pde

@@ -9,10 +9,19 @@
 // consecutive int64 counters advanced by the last block (0: none; [0] is the optimizer step);
 // bump < 0: the caller's earlier kernel already advanced the counter, t = *step, no fan-in at all.
 // grad_scale folds the DDP 1/world_size average (or any loss scale) into the update.
+// Optional fused all-reduce (Adam only, the W > 1 "fused" LeNet schedule): the first ar_nvb blocks
+// all-reduce the flat range [ar_lo4, n4) (the conv-gradient bucket) across ranks with the xGMI peer
+// protocol while the other blocks update [0, ar_lo4); those blocks then wait for the reduction (the
+// completing side block publishes the optimizer step t in *ar_epoch) before updating the rest.
+// Side blocks have the lowest block ids, so they are dispatched first: no wait can starve them.
 // Optional epilogue: repack the LeNet conv2 weight [50][20][5][5] into the [k'][64] layout the
 // conv2 forward kernel streams (k' = (kh*5+kw)*20+ci), so no separate repack launch exists.
 #include "pde_hip.h"
 #include "pde_kernels.h"
+#include "pde_peer_dev.h"
+
+#include <algorithm>
+#include <cstring>
 
 namespace {
 
@@ -77,12 +86,50 @@ __device__ __forceinline__ bool last_block(unsigned* arrive, long long t) {
   return is_last != 0;
 }
 
+struct FusedAR {
+  pde::PeerDev pd;
+  long long lo4;            // first float4 of the all-reduced range (range = [lo4, n4))
+  long long* epoch;         // completion word: the optimizer step t of the reduced call
+  int nvb;                  // side blocks (0 = no fused all-reduce)
+  int two;
+};
+
+__device__ __forceinline__ void wait_epoch(const long long* epoch, long long t, const pde::PeerDev& pd) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // relaxed polling (an acquire per poll would invalidate the L2 under the side blocks' feet),
+    // one acquire once the completion word is seen
+    while (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != t) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > 2 * pd.timeout) break;   // failure latched by the side blocks
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, long long n4,
                                               float lr, float b1, float b2, float eps, float wd, int decoupled,
                                               float grad_scale, long long* __restrict__ step,
-                                              unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd) {
+                                              unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd, FusedAR ar) {
   const long long t = bump < 0 ? *step : *step + 1;   // bump < 0: counter pre-advanced by an earlier kernel
+  __shared__ uint32_t lds2[2];
+  long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, istride = (long long)gridDim.x * blockDim.x;
+  long long lo = 0, hi = n4;                          // pass 1 range; pass 2 = [ar.lo4, n4) after the wait
+  if (ar.nvb > 0) {
+    if ((int)blockIdx.x < ar.nvb) {
+      if (pde::peer_ar_f32_vblock(ar.pd, g + 4 * ar.lo4, g + 4 * ar.lo4, 4 * (n4 - ar.lo4), 1.f, blockIdx.x,
+                                  ar.nvb, ar.two != 0, lds2))
+        __hip_atomic_store(ar.epoch, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      i0 = n4;                                        // no parameter work in side blocks
+    } else {
+      i0 = (long long)(blockIdx.x - ar.nvb) * blockDim.x + threadIdx.x;
+      istride = (long long)(gridDim.x - ar.nvb) * blockDim.x;
+      hi = ar.lo4;
+    }
+  }
   const float bc1 = 1.f - powf(b1, (float)t);
   const float bc2 = 1.f - powf(b2, (float)t);
   const float step_size = lr / bc1;
@@ -92,7 +139,14 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   float4* g4 = reinterpret_cast<float4*>(g);
   float4* m4 = reinterpret_cast<float4*>(m);
   float4* v4 = reinterpret_cast<float4*>(v);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+  for (int pass = 0; pass < 2; ++pass) {
+  if (pass == 1) {
+    if (ar.nvb == 0 || (int)blockIdx.x < ar.nvb) break;   // block-uniform: wait_epoch has barriers
+    wait_epoch(ar.epoch, t, ar.pd);                   // the all-reduced range is ready
+    lo = ar.lo4;
+    hi = n4;
+  }
+  for (long long i = lo + i0; i < hi; i += istride) {
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
     if (!fold_grad(fd, g4, i, gg)) continue;
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
@@ -110,6 +164,7 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
       pack_store(pk, 4 * i + j, pa[j]);
     }
     p4[i] = pp; m4[i] = mm; v4[i] = vv;
+  }
   }
   if (bump > 0 && last_block(arrive, t) && threadIdx.x == 0) {
     step[0] = t;
@@ -181,12 +236,23 @@ extern "C" {
 hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, float lr, float b1, float b2,
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
                          int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
-                         int fold_nrep, int fold_stride, hipStream_t st) {
+                         int fold_nrep, int fold_stride, const void* peer_dev, long long ar_off, long long* ar_epoch,
+                         int ar_two, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(k_adam, dim3(grid_for(n4)), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps, wd, decoupled,
-                     grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
-                     Fold{fold_off, fold_len, fold_nrep, fold_stride});
+  FusedAR ar{};
+  if (peer_dev != nullptr && ar_epoch != nullptr) {
+    if (ar_off % 4 || ar_off < 0 || ar_off >= n) return hipErrorInvalidValue;
+    std::memcpy(&ar.pd, peer_dev, sizeof(ar.pd));
+    ar.lo4 = ar_off / 4;
+    ar.epoch = ar_epoch;
+    ar.two = ar_two;
+    const long long m4 = n4 - ar.lo4, work = ar_two ? (m4 + ar.pd.world - 1) / ar.pd.world : m4;
+    ar.nvb = (int)std::min<long long>(32, std::max<long long>(1, (work + 255) / 256));
+  }
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n4) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps, wd,
+                     decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
+                     Fold{fold_off, fold_len, fold_nrep, fold_stride}, ar);
   return hipGetLastError();
 }
 

@@ -199,8 +199,25 @@ void lenet_conv_bwd(const at::Tensor& X, const at::Tensor& rows, const at::Tenso
 void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v, double lr,
                double b1, double b2, double eps, double wd, bool decoupled, double grad_scale, const at::Tensor& step,
                const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst, int64_t fold_off,
-               int64_t fold_len, int64_t fold_nrep, int64_t fold_stride) {
+               int64_t fold_len, int64_t fold_nrep, int64_t fold_stride, const OptT& peer_dev, int64_t ar_off,
+               const OptT& ar_epoch, int64_t ar_two) {
   const int64_t n = p.numel();
+  // fused all-reduce of [ar_off, n) by side blocks (peer_dev = CPU bytes of PeerAllReduce.device_args())
+  const void* pdev = nullptr;
+  long long* ep = nullptr;
+  if (peer_dev.has_value() && peer_dev->defined()) {
+    TORCH_CHECK(!peer_dev->is_cuda() && peer_dev->scalar_type() == at::kByte &&
+                    peer_dev->numel() == (int64_t)sizeof(pde::PeerDev) && peer_dev->is_contiguous(),
+                "peer_dev must be the CPU uint8 bytes of PeerAllReduce.device_args()");
+    TORCH_CHECK(ar_off >= 0 && ar_off < n && ar_off % 4 == 0, "bad fused all-reduce offset");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr<float>() + ar_off) % 16 == 0, "fused range must be 16-B aligned");
+    const auto* pd = static_cast<const pde::PeerDev*>(peer_dev->data_ptr());
+    TORCH_CHECK((n - ar_off) * 4 <= pd->cap, "fused range exceeds the peer all-reduce capacity");
+    TORCH_CHECK(ar_epoch.has_value() && ar_epoch->defined(), "ar_epoch required with peer_dev");
+    check_cuda(*ar_epoch, "ar_epoch", I64, 1);
+    pdev = peer_dev->data_ptr();
+    ep = ptr<long long>(*ar_epoch);
+  }
   check_cuda(p, "params", F32);
   check_cuda(g, "grads", F32, n);
   check_cuda(m, "exp_avg", F32, n);
@@ -218,7 +235,7 @@ void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, co
   hip_check(pde_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), n, (float)lr, (float)b1,
                           (float)b2, (float)eps, (float)wd, decoupled ? 1 : 0, (float)grad_scale, ptr<long long>(step),
                           ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, fold_off, (int)fold_len,
-                          (int)fold_nrep, (int)fold_stride, cur_stream()),
+                          (int)fold_nrep, (int)fold_stride, pdev, ar_off, ep, (int)ar_two, cur_stream()),
             "adam_flat");
 }
 
@@ -417,7 +434,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("decoupled"), py::arg("grad_scale"), py::arg("step"),
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),
-        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0);
+        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0,
+        py::arg("peer_dev") = py::none(), py::arg("ar_off") = 0, py::arg("ar_epoch") = py::none(),
+        py::arg("ar_two") = 0);
   m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
         py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("grad_scale"), py::arg("step"),
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),

@@ -19,6 +19,7 @@ path on every rank and the caller keeps using RCCL.
 from __future__ import annotations
 
 import os
+import sys
 from typing import Dict, Iterable, Optional
 
 import torch
@@ -82,13 +83,19 @@ class PeerAllReduce:
         ok = _host_allreduce_min(group, 0 if err else 1)
         group.host.barrier()
         if ok and self_test:
+            # first launches load the code object in every process (slow when ranks share a GPU):
+            # generous barrier time-out for the self-test, the steady-state one afterwards
+            self.native.set_timeout_ms(max(int(timeout_ms), 60000))
             try:
                 self._self_test()
             except Exception as e:   # noqa: BLE001
                 err = f"self-test: {e}"
+            self.native.set_timeout_ms(int(timeout_ms))
             ok = _host_allreduce_min(group, 0 if err else 1)
         self.ok = bool(ok)
         self.reason = err or ("" if ok else "disabled by a peer rank")
+        if not self.ok:
+            print(f"[rank {self.rank}] xGMI peer all-reduce disabled: {self.reason}", file=sys.stderr, flush=True)
         if not self.ok and self.native is not None:
             try:
                 self.native.close()

@@ -60,6 +60,7 @@ class LeNetTrainStep:
         # conv bucket after it on the compute stream
         self.mode = "overlap" if overlap else "flat"
         self._peer_dev = None
+        self.ar_epoch = torch.full((1,), -1, device=p0.device, dtype=torch.int64)   # fused-Adam all-reduce
         # force_comm: run the comm-stream/event path even at world size 1 (1-GPU testing of the W>1 path)
         self.comm_on = comm is not None and (self.world > 1 or force_comm)
         self.K = kernels()
@@ -135,18 +136,24 @@ class LeNetTrainStep:
         self.counters[1].zero_()
 
     # ------------------------------------------------------------------ the step
-    def _opt(self, lo: int, hi: int, conv: bool):
+    def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None):
         """Fused optimizer update of the flat range [lo, hi) (one bucket or everything).  The conv
-        range carries the conv2 weight repack (Wt2) and the conv1 gradient-replica fold."""
+        range carries the conv2 weight repack (Wt2) and the conv1 gradient-replica fold.
+        ``fuse_ar`` ('adam1' / 'adam2'): side blocks of the Adam kernel all-reduce the conv bucket
+        (one- / two-shot peer protocol) while the other blocks update the fc parameters."""
         K, sl = self.K, slice(lo, hi)
         pack_off = self.pack_off - lo if conv else -1
         fold_off = self.c1_off - lo if conv else -1
         pack = self.Wt2 if conv else None
         scale = 1.0 / self.world
         if self.optimizer == "adam":
+            far = {}
+            if fuse_ar is not None:
+                far = dict(peer_dev=self._peer_device_args(), ar_off=self.bucket_ranges[1][0] - lo,
+                           ar_epoch=self.ar_epoch, ar_two=int(fuse_ar == "adam2"))
             K.adam_flat(self.params[sl], self.grads[sl], self.m[sl], self.v[sl], self.lr, self.betas[0],
                         self.betas[1], self.eps, self.wd, False, scale, self.counters, self.arrive, -1, pack_off,
-                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE)
+                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE, **far)
         else:
             K.sgd_flat(self.params[sl], self.grads[sl], self.m[sl], self.lr, self.momentum, 0.0, self.wd, False,
                        scale, self.counters, self.arrive, -1, pack_off, pack, fold_off, C1_STRIDE, C1_NREP,
@@ -180,8 +187,12 @@ class LeNetTrainStep:
         if self.comm_on and self.mode == "fused":
             fc_route = self.comm.routes.get(self.bucket_grads[0].numel(), "peer2")
             K.lenet_conv_bwd(*conv_args, 0, self._peer_device_args(), self.bucket_grads[0], int(fc_route == "peer2"))
-            self.comm.all_reduce_(self.bucket_grads[1])
-            self._opt(0, self.params.numel(), True)
+            conv_route = self.comm.routes.get(self.bucket_grads[1].numel(), "rccl")
+            if conv_route in ("adam1", "adam2") and self.optimizer == "adam":
+                self._opt(0, self.params.numel(), True, fuse_ar=conv_route)
+            else:
+                self.comm.all_reduce_(self.bucket_grads[1])
+                self._opt(0, self.params.numel(), True)
             return
         if self.comm_on and self.mode == "overlap":
             ev["fc"].record(cur)
@@ -337,6 +348,7 @@ class LeNetTrainStep:
             if "momentum_buffer" in st and st["momentum_buffer"] is not None:
                 self.layout.view(self.m, n).copy_(st["momentum_buffer"])
             self.counters[0].fill_(int(float(st["step"])))
+        self.ar_epoch.fill_(-1)
         self.sync_params()
 
     def sync_params(self):
@@ -356,6 +368,8 @@ class LeNetTrainStep:
         out += [(m, {nall: a}) for m in ("flat", "serial") for a in routes]
         if getattr(self.comm, "peer", None) is not None:
             out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in routes]
+            if self.optimizer == "adam":         # last: a failing candidate poisons the peer protocol
+                out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in ("adam1", "adam2")]
         return out
 
     def autotune_schedule(self, steps: int = 40, graph_steps: int = 10, candidates=None):
@@ -390,6 +404,7 @@ class LeNetTrainStep:
                 continue
             for t, s0 in zip(state, snap):       # every candidate starts from the same (replicated) state
                 t.copy_(s0)
+            self.ar_epoch.fill_(-1)              # optimizer steps repeat: no stale completion word
             self.sync_params()
             self.mode = mode
             self.comm.routes = dict(routes)
@@ -427,6 +442,7 @@ class LeNetTrainStep:
         # restore the training state the trial steps advanced
         for t, s0 in zip(state, snap):
             t.copy_(s0)
+        self.ar_epoch.fill_(-1)
         self.sync_params()
         self.idx, self.nfull, self.tail, self.nbatches = saved_idx
         self.loss_sum.zero_()
