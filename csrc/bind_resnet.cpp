@@ -197,6 +197,31 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, 
             "conv_wgrad");
 }
 
+int64_t stem_stats_blocks(int64_t Bn, int64_t OH) { return pde_stem_stats_blocks((int)Bn, (int)OH); }
+
+// ResNet stem: y = conv7x7/s2/p3(x, w) with x NHWC bf16 [B, 3, H, W], w channels-last [64, 3, 7, 7];
+// wp: bf16 scratch >= 64*224 (packed weights); stats: optional BN partials [stem_stats_blocks][2][64]
+void stem_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& wp, const at::Tensor& y,
+              const OptT& stats) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == BF16 && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: x must be channels-last bf16 [B, 3, H, W]");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == BF16 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 &&
+                  w.size(3) == 7 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: w must be channels-last bf16 [64, 3, 7, 7]");
+  const int64_t Bn = x.size(0), H = x.size(2), W = x.size(3), OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(OW <= 112, "stem: input width must be <= 224");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == BF16 && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  y.size(0) == Bn && y.size(1) == 64 && y.size(2) == OH && y.size(3) == OW,
+              "stem: y must be channels-last bf16 [B, 64, OH, OW]");
+  TORCH_CHECK(Bn * std::max(H * W * 3, OH * OW * 64) * 2 < (int64_t(1) << 31), "stem: tensors must be < 2 GiB");
+  check_cuda(wp, "wp", BF16, 64 * 224);
+  float* sp = optr<float>(stats, "stats", F32, stem_stats_blocks(Bn, OH) * 2 * 64);
+  hip_check(pde_stem_fwd(x.data_ptr(), w.data_ptr(), wp.data_ptr(), y.data_ptr(), sp, (int)Bn, (int)H, (int)W,
+                         cur_stream()),
+            "stem_fwd");
+}
+
 }  // namespace
 
 void register_resnet(pybind11::module& m) {
@@ -207,6 +232,8 @@ void register_resnet(pybind11::module& m) {
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv_stats_blocks", &conv_stats_blocks);
+  m.def("stem_stats_blocks", &stem_stats_blocks);
+  m.def("stem_fwd", &stem_fwd);
   m.def("bn_part_rows", &bn_part_rows);
   m.def("conv_set_stages", [](int64_t n) { pde_conv_set_stages((int)n); });
   m.def("conv_fprop", &conv_fprop);

@@ -114,6 +114,51 @@ class Conv2dNHWCFn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+class StemConvFn(torch.autograd.Function):
+    """ResNet stem conv (7x7 / s2 / p3, 3 -> 64) over channels-last bf16 on the stem MFMA kernel
+    (csrc/kernels/stem.hip), optionally with the following BN's batch statistics."""
+
+    @staticmethod
+    def forward(ctx, x, w, with_stats=False):
+        K = kernels()
+        N, _, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, 64, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+        wp = torch.empty(64 * 224, device=x.device, dtype=x.dtype)
+        stats = None
+        if with_stats:
+            nblk = K.stem_stats_blocks(N, OH)
+            stats = torch.empty(K.bn_part_rows(nblk) * 2 * 64, device=x.device, dtype=torch.float32)
+            ctx.nblk = nblk
+            ctx.mark_non_differentiable(stats)
+            ctx.set_materialize_grads(False)
+        K.stem_fwd(x, w, wp, y, stats)
+        ctx.save_for_backward(x, w)
+        return (y, stats) if with_stats else y
+
+    @staticmethod
+    def backward(ctx, dy, dstats=None):
+        x, w = ctx.saved_tensors
+        if dy is None:
+            return None, None, None
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        if dw is not None:
+            slot = flat_grad_slot(w)
+            if slot is not None and slot.is_contiguous(memory_format=torch.channels_last):
+                slot.copy_(dw)
+                dw = slot
+        return dx, dw, None
+
+
+def stem_eligible(x, w, stride: int, pad: int) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape[1] == 3 and tuple(w.shape) == (64, 3, 7, 7) and stride == 2 and pad == 3
+            and (x.shape[3] - 1) // 2 + 1 <= 112)
+
+
 def igemm_eligible(x, w, stride: int, pad: int) -> bool:
     """True when the MFMA implicit-GEMM kernels cover this convolution."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
@@ -126,6 +171,13 @@ def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0, with_stats: bool = False):
     ``with_stats``: return ``(y, stats)`` where ``stats`` is ``(partials, nblk)`` -- per-channel
     (sum, sum of squares) partials of y for a following training-mode BatchNorm -- or None when
     the library path ran."""
+    if stem_eligible(x, w, stride, pad):
+        out = StemConvFn.apply(x.contiguous(memory_format=torch.channels_last),
+                               w.contiguous(memory_format=torch.channels_last), with_stats)
+        if with_stats:
+            y, part = out
+            return y, (part, kernels().stem_stats_blocks(y.shape[0], y.shape[2]))
+        return out
     if igemm_eligible(x, w, stride, pad):
         out = Conv2dNHWCFn.apply(x.contiguous(memory_format=torch.channels_last),
                                  w.contiguous(memory_format=torch.channels_last), stride, pad, with_stats)

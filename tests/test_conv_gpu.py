@@ -87,3 +87,46 @@ def test_conv_fprop_bn_stats(N):
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, N)
     assert torch.allclose(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+
+
+# ---------------------------------------------------------------------------------------------- stem
+from pytorch_distributed_example_amd.ops.resnet import stem_eligible  # noqa: E402
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 224, 224), (3, 64, 64), (2, 37, 51), (1, 10, 7)])
+def test_stem_conv_fwd_bwd(B, H, W):
+    """7x7 / s2 / p3 stem kernel (csrc/kernels/stem.hip) vs fp32 conv2d on the same bf16 operands."""
+    torch.manual_seed(B * 100 + H + W)
+    x = cl(torch.randn(B, 3, H, W, device=dev).to(torch.bfloat16)).requires_grad_()
+    w = cl((torch.randn(64, 3, 7, 7, device=dev) / 147 ** 0.5).to(torch.bfloat16)).requires_grad_()
+    assert stem_eligible(x, w, 2, 3)
+    y = conv2d_nhwc(x, w, 2, 3)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    dy = cl(torch.randn_like(y))
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 2, 3)
+    yr.backward(dy.float())
+    assert y.shape == yr.shape
+    assert max_rel(y, yr) < 1e-2
+    assert max_rel(w.grad, wr.grad) < 2e-2
+    assert max_rel(x.grad, xr.grad) < 2e-2
+
+
+def test_stem_exact_integer_and_stats():
+    """Integer data is exact in bf16 / fp32: any tap or padding slip shows; BN partials sum to the
+    per-channel (sum, sum of squares) of the bf16 output."""
+    torch.manual_seed(3)
+    K = kernels()
+    B, H, W = 2, 30, 26
+    x = cl(torch.randint(-2, 3, (B, 3, H, W), device=dev).to(torch.bfloat16))
+    w = cl(torch.randint(-1, 2, (64, 3, 7, 7), device=dev).to(torch.bfloat16))
+    y, (part, nblk) = conv2d_nhwc(x, w, 2, 3, with_stats=True)
+    yr = F.conv2d(x.double().cpu(), w.double().cpu(), None, 2, 3)
+    assert torch.equal(y.double().cpu(), yr)
+    assert nblk == K.stem_stats_blocks(B, y.shape[2])
+    st = part[: nblk * 128].view(nblk, 2, 64).sum(0).double().cpu()
+    yf = yr.permute(0, 2, 3, 1).reshape(-1, 64)
+    assert torch.allclose(st[0], yf.sum(0), rtol=1e-6, atol=1e-3)
+    assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
