@@ -222,6 +222,28 @@ void stem_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& wp, co
             "stem_fwd");
 }
 
+int64_t stem_wgrad_blocks(int64_t Bn, int64_t OH) { return pde_stem_wgrad_blocks((int)Bn, (int)OH); }
+
+// dW (bf16, channels-last [64, 3, 7, 7]) of the stem from x and dy; part: fp32 scratch
+// >= stem_wgrad_blocks(B, OH) * 64 * 147
+void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& part, const at::Tensor& dw) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == BF16 && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem wgrad: x must be channels-last bf16 [B, 3, H, W]");
+  const int64_t Bn = x.size(0), H = x.size(2), W = x.size(3), OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(OW <= 112, "stem: input width must be <= 224");
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.size(0) == Bn && dy.size(1) == 64 && dy.size(2) == OH && dy.size(3) == OW,
+              "stem wgrad: dy must be channels-last bf16 [B, 64, OH, OW]");
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == BF16 && dw.numel() == 64 * 147 &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem wgrad: dw must be channels-last bf16 [64, 3, 7, 7]");
+  check_cuda(part, "part", F32, stem_wgrad_blocks(Bn, OH) * 64 * 147);
+  hip_check(pde_stem_wgrad(x.data_ptr(), dy.data_ptr(), ptr<float>(part), dw.data_ptr(), (int)Bn, (int)H, (int)W,
+                           cur_stream()),
+            "stem_wgrad");
+}
+
 }  // namespace
 
 void register_resnet(pybind11::module& m) {
@@ -234,6 +256,8 @@ void register_resnet(pybind11::module& m) {
   m.def("conv_stats_blocks", &conv_stats_blocks);
   m.def("stem_stats_blocks", &stem_stats_blocks);
   m.def("stem_fwd", &stem_fwd);
+  m.def("stem_wgrad_blocks", &stem_wgrad_blocks);
+  m.def("stem_wgrad", &stem_wgrad);
   m.def("bn_part_rows", &bn_part_rows);
   m.def("conv_set_stages", [](int64_t n) { pde_conv_set_stages((int)n); });
   m.def("conv_fprop", &conv_fprop);

@@ -99,6 +99,9 @@ int pde_conv_fprop_mtiles(int M, int N);
 int pde_stem_stats_blocks(int Bn, int OH);
 hipError_t pde_stem_fwd(const void* X, const void* W, void* Wp, void* Y, float* stats, int Bn, int H, int Wd,
                         hipStream_t st);
+int pde_stem_wgrad_blocks(int Bn, int OH);
+hipError_t pde_stem_wgrad(const void* X, const void* dY, float* part, void* dW, int Bn, int H, int Wd,
+                          hipStream_t st);
 hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, int Bn, int H, int W, int C, int N,
                           int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
 hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStream_t st);

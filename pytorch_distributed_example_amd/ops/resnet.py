@@ -142,14 +142,18 @@ class StemConvFn(torch.autograd.Function):
         if dy is None:
             return None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dw, _ = torch.ops.aten.convolution_backward(
-            dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
-        if dw is not None:
-            slot = flat_grad_slot(w)
-            if slot is not None and slot.is_contiguous(memory_format=torch.channels_last):
-                slot.copy_(dw)
-                dw = slot
+        dx = dw = None
+        if ctx.needs_input_grad[0]:      # the network input never needs it; library dgrad for generality
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            K = kernels()
+            part = torch.empty(K.stem_wgrad_blocks(x.shape[0], dy.shape[2]) * 64 * 147, device=x.device,
+                               dtype=torch.float32)
+            dw = flat_grad_slot(w)
+            if dw is None or not dw.is_contiguous(memory_format=torch.channels_last):
+                dw = torch.empty_like(w, memory_format=torch.channels_last)
+            K.stem_wgrad(x, dy, part, dw)
         return dx, dw, None
 
 
