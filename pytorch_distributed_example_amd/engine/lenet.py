@@ -167,7 +167,11 @@ class LeNetTrainStep:
 
         (Measured and rejected: moving the fc weight-gradient roles and the fc-bucket optimizer to a
         side stream beside conv_bwd -- conv_bwd already fills the GPU, so it slowed from 24 to 31 us,
-        and the two cross-stream joins cost 5-7 us each: 91 us/step vs 81 us single-stream.)"""
+        and the two cross-stream joins cost 5-7 us each: 91 us/step vs 81 us single-stream.  Also
+        rejected: folding the head into fc1, the last column block of each 16-row tile running the
+        head -- with __threadfence() in every block (L2 write-back/invalidate per block) 99 us/step,
+        with write-through H1 stores + agent-scope loads 83 us, against 69 us for two launches: one
+        wave doing 4 latency-bound rows serially costs more than the kernel boundary it saves.)"""
         K, p, g = self.K, self.p, self.g
         K.lenet_conv_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
                          p["conv1.weight"], p["conv1.bias"], self.Wt2, p["conv2.bias"], self.P1, self.A1, self.P2,
