@@ -431,6 +431,67 @@ def case_ddp_model(model="gpt2", steps="3"):
     dist.destroy_process_group()
 
 
+def case_torch_backend(device="cpu"):
+    """Reference-style code on ``torch.distributed`` itself with the framework registered as the
+    c10d backend "pde": the toy's per-step new_group + deprecated reduce_op loop, the usual
+    collectives, and torch's own DistributedDataParallel on top."""
+    import torch.distributed as tdist
+    import pytorch_distributed_example_amd.dist.torch_backend  # noqa: F401  (registers "pde")
+
+    if device == "cuda":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    dev = torch.device(device)
+    tdist.init_process_group("pde", init_method=f"tcp://127.0.0.1:{os.environ['MASTER_PORT']}", rank=R,
+                             world_size=W)
+    assert tdist.get_backend() == "pde" and tdist.get_rank() == R and tdist.get_world_size() == W
+    sums = []
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", FutureWarning)
+        for step in range(3):                          # toy/main.py:9-25 pattern
+            group = tdist.new_group(list(range(W)))
+            t = torch.IntTensor([R + step])
+            tdist.all_reduce(t, op=tdist.reduce_op.SUM, group=group)
+            sums.append(float(t))
+    assert sums == [float(sum(r + s for r in range(W))) for s in range(3)], sums
+    x = torch.arange(10, dtype=torch.float32, device=dev) * (R + 1)
+    tdist.all_reduce(x)
+    assert torch.equal(x.cpu(), torch.arange(10, dtype=torch.float32) * (W * (W + 1) // 2))
+    y = torch.full((4,), float(R), device=dev)
+    tdist.all_reduce(y, op=tdist.ReduceOp.MAX)
+    assert torch.all(y.cpu() == W - 1)
+    b = torch.full((5,), float(R), device=dev)
+    tdist.broadcast(b, src=W - 1)
+    assert torch.all(b.cpu() == W - 1)
+    outs = [torch.empty(3, device=dev) for _ in range(W)]
+    tdist.all_gather(outs, torch.full((3,), float(R), device=dev))
+    assert [float(o[0]) for o in outs] == [float(r) for r in range(W)]
+    big = torch.empty(3 * W, device=dev)
+    tdist.all_gather_into_tensor(big, torch.full((3,), float(R), device=dev))
+    assert big.cpu().tolist() == [float(r) for r in range(W) for _ in range(3)]
+    rs = torch.empty(2, device=dev)
+    tdist.reduce_scatter_tensor(rs, torch.arange(2 * W, dtype=torch.float32, device=dev))
+    assert rs.cpu().tolist() == [float(W * (2 * R)), float(W * (2 * R + 1))]
+    a2a = torch.empty(W, device=dev)
+    tdist.all_to_all_single(a2a, torch.tensor([100.0 * R + j for j in range(W)], device=dev))
+    assert a2a.cpu().tolist() == [100.0 * j + R for j in range(W)]
+    tdist.barrier()
+    # torch's own DDP over the "pde" process group == the mean gradient of the global batch
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3)).to(dev)
+    ddp = torch.nn.parallel.DistributedDataParallel(net)
+    gx, gy = torch.randn(4 * W, 8), torch.randint(0, 3, (4 * W,))
+    loss = torch.nn.functional.cross_entropy(ddp(gx[4 * R:4 * R + 4].to(dev)), gy[4 * R:4 * R + 4].to(dev))
+    loss.backward()
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+    ref.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
+    torch.nn.functional.cross_entropy(ref(gx), gy).backward()
+    for p, q in zip(net.parameters(), ref.parameters()):
+        assert torch.allclose(p.grad.cpu(), q.grad, atol=1e-5, rtol=1e-4), (p.grad, q.grad)
+    emit({"rank": R, "sums": sums})
+    tdist.destroy_process_group()
+
+
 if __name__ == "__main__":
     name = sys.argv[1]
     globals()["case_" + name](*sys.argv[2:])

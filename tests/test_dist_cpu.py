@@ -77,3 +77,12 @@ def test_rank_none_error():
     from pytorch_distributed_example_amd import dist
     with pytest.raises((ValueError, TypeError), match="rank must be an integer"):
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=None, world_size=2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_distributed_backend_pde(world):
+    """torch.distributed with backend="pde" (the framework runtime registered as a c10d backend):
+    reference-style toy loop, collectives and torch's own DDP, on the CPU host collectives."""
+    rc, res, logs = run_ranks("torch_backend", world, "cpu")
+    assert rc == 0, "\n".join(logs)
+    assert all(r["sums"] == res[0]["sums"] for r in res)

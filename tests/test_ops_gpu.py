@@ -187,3 +187,10 @@ def test_mnist_script_fused_gpu():
     assert "device = cuda" in lines
     ep = [l for l in lines if l.startswith("Epoch: ")]
     assert len(ep) == 2
+
+
+def test_torch_distributed_backend_pde_gpu():
+    """torch.distributed(backend="pde") on GPU tensors: RCCL communicators of the framework runtime
+    behind torch's API, incl. per-step new_group and torch's own DDP (W=1 on the 1-GPU box)."""
+    rc, res, logs = _mp("torch_backend", "cuda")
+    assert rc == 0, "\n".join(logs)
