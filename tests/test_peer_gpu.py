@@ -47,15 +47,17 @@ def test_engine_autotune_restores_training_state():
         assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (a, b)
 
 
-@pytest.mark.parametrize("world,sched", [(w, s) for w in (2, 4) for s in (
-    "mode=fused:peer2:peer1", "mode=fused:peer1:peer2", "mode=serial:peer2:peer2")] + [
-    (2, "mode=fused:peer2:adam1"), (2, "mode=fused:peer1:adam2")])
+@pytest.mark.parametrize("world,sched", [(2, s) for s in (
+    "mode=fused:peer2:peer1", "mode=fused:peer1:peer2", "mode=serial:peer2:peer2",
+    "mode=fused:peer2:adam1", "mode=fused:peer1:adam2")])
 def test_engine_fused_schedules_match(world, sched):
     """The fc bucket all-reduced by side blocks of the conv backward (fused) and the serial schedule
     train exactly like the overlapped reference schedule (same parameters up to fp32 reassociation).
-    The Adam-fused conv bucket (adam1/2: Adam blocks wait for side blocks of the same kernel) runs at
-    W=2 only: with 4 processes time-sharing one GPU, one process's waiting blocks can hold the CUs
-    another process's side blocks need (on a node every rank owns its GPU)."""
+    Runs at W=2 only: with 4 processes time-sharing one GPU, the overlapped reference schedule puts
+    8 spinning peer kernels (two streams per rank) on one device, and one process's waiting blocks
+    can hold the CUs another process's side blocks need, so a run can sit in barrier time-outs
+    (observed once in a full GPU run).  On a node every rank owns its GPU; W=4 peer correctness is
+    covered by test_peer_allreduce_matches_fp64[4]."""
     rc0, res0, logs0 = run_ranks("peer_engine", world, "6", "graph", "1", "0")
     rc1, res1, logs1 = run_ranks("peer_engine", world, "6", "graph", "1", sched)
     assert rc0 == 0 and rc1 == 0, "\n".join(logs0 + logs1)
