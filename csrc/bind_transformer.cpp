@@ -7,7 +7,7 @@ namespace pde {
 namespace {
 
 void ln_fwd(const at::Tensor& X, const at::Tensor& G, const at::Tensor& B, const at::Tensor& Y,
-            const at::Tensor& mean, const at::Tensor& rstd, double eps) {
+            const at::Tensor& mean, const at::Tensor& rstd, double eps, const OptT& D, const OptT& S) {
   const int64_t C = X.size(-1), N = X.numel() / C;
   TORCH_CHECK(C % 4 == 0 && C <= 2048, "ln: C must be a multiple of 4 and <= 2048");
   check_cuda(X, "X", BF16);
@@ -16,7 +16,10 @@ void ln_fwd(const at::Tensor& X, const at::Tensor& G, const at::Tensor& B, const
   check_cuda(Y, "Y", BF16, N * C);
   check_cuda(mean, "mean", F32, N);
   check_cuda(rstd, "rstd", F32, N);
-  hip_check(pde_ln_fwd(X.data_ptr(), G.data_ptr(), B.data_ptr(), Y.data_ptr(), ptr<float>(mean), ptr<float>(rstd),
+  const void* dp = optr<void>(D, "D", BF16, N * C);
+  void* sp = optr<void>(S, "S", BF16, N * C);
+  TORCH_CHECK((dp == nullptr) == (sp == nullptr), "ln_fwd: D (residual input) and S (sum output) go together");
+  hip_check(pde_ln_fwd(X.data_ptr(), dp, sp, G.data_ptr(), B.data_ptr(), Y.data_ptr(), ptr<float>(mean), ptr<float>(rstd),
                        (int)N, (int)C, (float)eps, cur_stream()),
             "ln_fwd");
 }
@@ -206,7 +209,8 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
 
 void register_transformer(pybind11::module& m) {
   namespace py = pybind11;
-  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("X"), py::arg("G"), py::arg("B"), py::arg("Y"), py::arg("mean"), py::arg("rstd"),
+        py::arg("eps"), py::arg("D") = py::none(), py::arg("S") = py::none());
   m.def("ln_bwd_blocks", &ln_bwd_blocks);
   m.def("ln_bwd", &ln_bwd);
   m.def("sum_slabs_bf16", &sum_slabs_bf16);

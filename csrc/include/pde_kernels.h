@@ -69,8 +69,8 @@ hipError_t pde_gather_rows(const float* src, const long long* idx, int n, int ro
 
 
 // ---- transformer (transformer.hip) ----
-hipError_t pde_ln_fwd(const void* X, const void* G, const void* B, void* Y, float* mean, float* rstd, int N, int C,
-                      float eps, hipStream_t st);
+hipError_t pde_ln_fwd(const void* X, const void* D, void* S, const void* G, const void* B, void* Y, float* mean,
+                      float* rstd, int N, int C, float eps, hipStream_t st);
 int pde_ln_bwd_blocks(int N);
 hipError_t pde_ln_bwd(const void* dY, const void* X, const float* mean, const float* rstd, const void* G,
                       const void* dRes, void* dX, float* part, void* dG, void* dB, int N, int C, int accumulate,

@@ -13,7 +13,11 @@ namespace {
 
 // ---------------------------------------------------------------------------------- LayerNorm
 template <int NCH>
-__global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ X, const bf16_t* __restrict__ G,
+// With D != nullptr the row is first summed with D (the residual add of a pre-LN block), rounded to
+// bf16 exactly like a separate bf16 add would, written to S, and normalised: one pass instead of an
+// elementwise add kernel (read 2, write 1) followed by the LayerNorm (read 1).
+__global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ X, const bf16_t* __restrict__ D,
+                                                bf16_t* __restrict__ S, const bf16_t* __restrict__ G,
                                                 const bf16_t* __restrict__ Bt, bf16_t* __restrict__ Y,
                                                 float* __restrict__ mean_out, float* __restrict__ rstd_out, int N,
                                                 int C, float eps) {
@@ -25,13 +29,28 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ X, co
   const uint2* g4 = reinterpret_cast<const uint2*>(G);
   const uint2* b4 = reinterpret_cast<const uint2*>(Bt);
   float v[NCH][4], gg[NCH][4], bb[NCH][4];
-  uint2 wx[NCH], wg[NCH], wb[NCH];
+  uint2 wx[NCH], wd[NCH], wg[NCH], wb[NCH];
+  const uint2* dr = D ? reinterpret_cast<const uint2*>(D + (size_t)row * C) : nullptr;
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {  // issue every load first (clamped index, no branch)
     const int c = min(lane + 64 * j, nc - 1);
     wx[j] = xr[c];
+    wd[j] = dr ? dr[c] : make_uint2(0u, 0u);
     wg[j] = g4[c];
     wb[j] = b4[c];
+  }
+  if (D) {  // residual add, rounded to bf16 (the stored residual stream is bf16)
+    uint2* sr = reinterpret_cast<uint2*>(S + (size_t)row * C);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      float a[4], b[4];
+      unpack4(wx[j], a);
+      unpack4(wd[j], b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += b[e];
+      wx[j] = pack4(a);
+      if (lane + 64 * j < nc) sr[lane + 64 * j] = wx[j];
+    }
   }
   float s = 0.f;
 #pragma unroll
@@ -90,20 +109,30 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dY, c
     for (int e = 0; e < 4; ++e) dg[j][e] = db[j][e] = 0.f;
   }
   const int row0 = blockIdx.x * 4 * rpw;
-  for (int i = 0; i < rpw; ++i) {
-    const int row = row0 + w + 4 * i;
-    if (row >= N) break;  // wave-uniform
+  // register double buffer: row i+1's loads are in flight while row i is reduced and written
+  uint2 wdy[NCH], wx[NCH], wr[NCH];
+  float mu = 0.f, rs = 0.f;
+  auto load_row = [&](int row, uint2 (&ldy)[NCH], uint2 (&lx)[NCH], uint2 (&lr)[NCH], float& lmu, float& lrs) {
     const uint2* dyr = reinterpret_cast<const uint2*>(dY + (size_t)row * C);
     const uint2* xr = reinterpret_cast<const uint2*>(X + (size_t)row * C);
-    uint2 wdy[NCH], wx[NCH], wr[NCH];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const int c = min(lane + 64 * j, nc - 1);
-      wdy[j] = dyr[c];
-      wx[j] = xr[c];
-      wr[j] = dRes ? reinterpret_cast<const uint2*>(dRes + (size_t)row * C)[c] : make_uint2(0u, 0u);
+      ldy[j] = dyr[c];
+      lx[j] = xr[c];
+      lr[j] = dRes ? reinterpret_cast<const uint2*>(dRes + (size_t)row * C)[c] : make_uint2(0u, 0u);
     }
-    const float mu = mean[row], rs = rstd[row];
+    lmu = mean[row];
+    lrs = rstd[row];
+  };
+  if (row0 + w < N) load_row(row0 + w, wdy, wx, wr, mu, rs);
+  for (int i = 0; i < rpw; ++i) {
+    const int row = row0 + w + 4 * i;
+    if (row >= N) break;  // wave-uniform
+    uint2 ndy[NCH], nx[NCH], nr[NCH];
+    float nmu = 0.f, nrs = 0.f;
+    const bool more = i + 1 < rpw && row + 4 < N;  // wave-uniform
+    if (more) load_row(row + 4, ndy, nx, nr, nmu, nrs);
     float xh[NCH][4], gy[NCH][4];
     float a = 0.f, b = 0.f;
 #pragma unroll
@@ -134,6 +163,16 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dY, c
       for (int e = 0; e < 4; ++e) o[e] = rs * (gy[j][e] - a - xh[j][e] * b) + r[e];
       if (c < nc) dxr[c] = pack4(o);
     }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        wdy[j] = ndy[j];
+        wx[j] = nx[j];
+        wr[j] = nr[j];
+      }
+      mu = nmu;
+      rs = nrs;
+    }
   }
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
@@ -154,27 +193,30 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dY, c
 }
 
 // Sum per-block partials: out[k] = sum_b part[b][k], k < 2C; writes dgamma | dbeta as bf16 (or
-// accumulates into them when accumulate != 0).  Block = 64 columns x 4 row-groups.
-__global__ __launch_bounds__(256) void k_ln_reduce(const float* __restrict__ part, int nblk, int C2,
-                                                   bf16_t* __restrict__ dG, bf16_t* __restrict__ dB, int C,
-                                                   int accumulate) {
-  __shared__ float sh[4][64];
+// accumulates into them when accumulate != 0).  Block = 64 columns x 16 row-groups (16 waves, 4
+// independent loads each in flight: the pass is latency-bound, it has only 2C/64 blocks).
+__global__ __launch_bounds__(1024) void k_ln_reduce(const float* __restrict__ part, int nblk, int C2,
+                                                    bf16_t* __restrict__ dG, bf16_t* __restrict__ dB, int C,
+                                                    int accumulate) {
+  __shared__ float sh[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
   const int kc = min(k, C2 - 1);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int b = w;
-  for (; b + 12 < nblk; b += 16) {
+  for (; b + 48 < nblk; b += 64) {
     s0 += part[(size_t)b * C2 + kc];
-    s1 += part[(size_t)(b + 4) * C2 + kc];
-    s2 += part[(size_t)(b + 8) * C2 + kc];
-    s3 += part[(size_t)(b + 12) * C2 + kc];
+    s1 += part[(size_t)(b + 16) * C2 + kc];
+    s2 += part[(size_t)(b + 32) * C2 + kc];
+    s3 += part[(size_t)(b + 48) * C2 + kc];
   }
-  for (; b < nblk; b += 4) s0 += part[(size_t)b * C2 + kc];
+  for (; b < nblk; b += 16) s0 += part[(size_t)b * C2 + kc];
   sh[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (w == 0 && k < C2) {
-    float t = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t += sh[r][lane];
     bf16_t* dst = k < C ? dG + k : dB + (k - C);
     if (accumulate) t += bf2f(*dst);
     *dst = f2bf(t);
@@ -549,13 +591,14 @@ inline int grid_for(int64_t n, int per_block, int cap = 4096) {
 // ------------------------------------------------------------------------------------ launchers
 extern "C" {
 
-hipError_t pde_ln_fwd(const void* X, const void* G, const void* B, void* Y, float* mean, float* rstd, int N, int C,
-                      float eps, hipStream_t st) {
+hipError_t pde_ln_fwd(const void* X, const void* D, void* S, const void* G, const void* B, void* Y, float* mean,
+                      float* rstd, int N, int C, float eps, hipStream_t st) {
   const int nch = (C / 4 + 63) / 64;
   dim3 grid((N + 3) / 4);
 #define LNF(K)                                                                                          \
   case K:                                                                                               \
-    hipLaunchKernelGGL(k_ln_fwd<K>, grid, dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)G,          \
+    hipLaunchKernelGGL(k_ln_fwd<K>, grid, dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)D,          \
+                       (bf16_t*)S, (const bf16_t*)G,                                                    \
                        (const bf16_t*)B, (bf16_t*)Y, mean, rstd, N, C, eps);                            \
     break;
   switch (nch) {
@@ -566,8 +609,12 @@ hipError_t pde_ln_fwd(const void* X, const void* G, const void* B, void* Y, floa
   return hipGetLastError();
 }
 
+// Rows per wave: ~512 blocks of 4 waves (2 blocks per CU) so the memory-bound backward has enough
+// waves in flight; the per-block dgamma/dbeta partials (2C floats each) stay small next to dY / X.
+static int ln_bwd_rpw(int N) { return (N + 4 * 512 - 1) / (4 * 512); }
+
 int pde_ln_bwd_blocks(int N) {
-  const int rpw = (N + 4 * 256 - 1) / (4 * 256);
+  const int rpw = ln_bwd_rpw(N);
   return (N + 4 * rpw - 1) / (4 * rpw);
 }
 
@@ -575,7 +622,7 @@ hipError_t pde_ln_bwd(const void* dY, const void* X, const float* mean, const fl
                       const void* dRes, void* dX, float* part, void* dG, void* dB, int N, int C, int accumulate,
                       hipStream_t st) {
   const int nch = (C / 4 + 63) / 64;
-  const int rpw = (N + 4 * 256 - 1) / (4 * 256);
+  const int rpw = ln_bwd_rpw(N);
   const int nblk = (N + 4 * rpw - 1) / (4 * rpw);
   const size_t lds = (size_t)8 * C * sizeof(float);
 #define LNB(K)                                                                                          \
@@ -588,7 +635,7 @@ hipError_t pde_ln_bwd(const void* dY, const void* X, const float* mean, const fl
     default: return hipErrorInvalidValue;
   }
 #undef LNB
-  hipLaunchKernelGGL(k_ln_reduce, dim3((2 * C + 63) / 64), dim3(256), 0, st, part, nblk, 2 * C, (bf16_t*)dG,
+  hipLaunchKernelGGL(k_ln_reduce, dim3((2 * C + 63) / 64), dim3(1024), 0, st, part, nblk, 2 * C, (bf16_t*)dG,
                      (bf16_t*)dB, C, accumulate);
   return hipGetLastError();
 }

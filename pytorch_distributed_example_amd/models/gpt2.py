@@ -82,12 +82,19 @@ class Block(tnn.Module):
         self.ln_2 = _LN(cfg.n_embd, cfg.ln_eps)
         self.mlp = _MLP(cfg)
 
-    def forward(self, x):
-        # (residual, LN(x)) from one op: the residual-gradient add is fused into the LN backward
-        x, h = T.layer_norm_residual(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
-        x = x + self.attn(h)
-        x, h = T.layer_norm_residual(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
-        return x + self.mlp(h)
+    def forward(self, x, delta=None):
+        return sum(self.forward_deferred(x, delta))
+
+    def forward_deferred(self, x, delta=None):
+        """(residual, mlp_out) with the block output = residual + mlp_out left unsummed, so the next
+        LayerNorm adds it inside its kernel.  ``delta`` is the previous block's deferred mlp_out.
+        (residual, LN(x)) come from one op: the residual-gradient add is fused into the LN backward."""
+        if delta is None:
+            x, h = T.layer_norm_residual(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+        else:
+            x, h = T.add_layer_norm_residual(x, delta, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+        x, h = T.add_layer_norm_residual(x, self.attn(h), self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
+        return x, self.mlp(h)
 
 
 class _Transformer(tnn.Module):
@@ -110,9 +117,13 @@ class GPT(tnn.Module):
     def forward(self, idx, targets=None):
         t = self.transformer
         x = T.embedding(idx, t.wte.weight, t.wpe.weight)
+        delta = None
         for blk in t.h:
-            x = blk(x)
-        x = t.ln_f(x)
+            x, delta = blk.forward_deferred(x, delta)
+        if delta is None:
+            x = t.ln_f(x)
+        else:   # last block's residual add fused into ln_f (the summed stream itself is not needed)
+            x = T.add_layer_norm_residual(x, delta, t.ln_f.weight, t.ln_f.bias, t.ln_f.eps)[1]
         if targets is None:
             return torch.matmul(x, t.wte.weight.t())[..., :self.config.vocab_size]
         return T.lm_head_loss(x, t.wte.weight, targets, self.config.vocab_size)

@@ -107,6 +107,39 @@ def layer_norm_residual(x, weight, bias, eps: float = 1e-5):
     return x, F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
 
 
+class AddLayerNormResFn(torch.autograd.Function):
+    """(s, LayerNorm(s)) with s = x + d: the residual add of the previous sub-block runs inside the
+    LayerNorm kernel (one pass writes s and LN(s)).  Backward is LayerNormResFn's single kernel;
+    x and d receive the same gradient."""
+
+    @staticmethod
+    def forward(ctx, x, d, w, b, eps):
+        xc, dc = _c(x), _c(d)
+        C = xc.shape[-1]
+        N = xc.numel() // C
+        s = torch.empty_like(xc)
+        y = torch.empty_like(xc)
+        mean = torch.empty(N, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(N, device=x.device, dtype=torch.float32)
+        kernels().ln_fwd(xc, w, b, y, mean, rstd, eps, dc, s)
+        ctx.save_for_backward(s, w, b, mean, rstd)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        dx, dw, db, _ = LayerNormResFn.backward(ctx, dres, dy)
+        return dx, dx, dw, db, None
+
+
+def add_layer_norm_residual(x, d, weight, bias, eps: float = 1e-5):
+    """Returns ``(x + d, layer_norm(x + d))`` (the residual stream and the normalised input of the
+    next sub-block); on GPU the add is fused into the LayerNorm kernel."""
+    if _gpu(x) and x.shape == d.shape and x.dtype == d.dtype:
+        return AddLayerNormResFn.apply(x, d, weight, bias, eps)
+    s = x + d
+    return s, F.layer_norm(s, (s.shape[-1],), weight, bias, eps)
+
+
 # --------------------------------------------------------------------------------------- GELU
 class GeluFn(torch.autograd.Function):
     @staticmethod

@@ -232,3 +232,27 @@ def test_layer_norm_residual_fused_grad():
     for a, r in ((x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
         err = ((a.float() - r).abs().max() / r.abs().max()).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("N,C", [(96, 384), (16384, 768), (7, 2048)])
+def test_add_layer_norm_residual_fused(N, C):
+    """(x + d, LN(x + d)) with the residual add inside the LN kernel: the stored sum is exactly the
+    bf16 add, LN and all gradients match an fp32 reference (x and d get the same gradient)."""
+    from pytorch_distributed_example_amd.ops.transformer import add_layer_norm_residual
+    torch.manual_seed(22)
+    x = torch.randn(N, C).to(dev, torch.bfloat16).requires_grad_()
+    d = (0.5 * torch.randn(N, C)).to(dev, torch.bfloat16).requires_grad_()
+    w = (1 + 0.1 * torch.randn(C)).to(dev, torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(C)).to(dev, torch.bfloat16).requires_grad_()
+    g1 = torch.randn(N, C, device=dev)
+    g2 = torch.randn(N, C, device=dev)
+    s, y = add_layer_norm_residual(x, d, w, b)
+    assert torch.equal(s, x.detach() + d.detach())
+    ((s.float() * g1).sum() + (y.float() * g2).sum()).backward()
+    xf, df, wf, bf = (t.detach().float().requires_grad_() for t in (x, d, w, b))
+    sf = xf + df
+    yf = F.layer_norm(sf, (C,), wf, bf, 1e-5)
+    ((sf * g1).sum() + (yf * g2).sum()).backward()
+    assert rel_err(y, yf) < 1e-2
+    for a, r in ((x.grad, xf.grad), (d.grad, df.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
+        assert rel_err(a, r) < 2e-2
