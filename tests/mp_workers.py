@@ -288,7 +288,9 @@ def case_peer_allreduce(graph="1"):
     dev = _shared_gpu_init()
     g = dist.get_default_group()
     cap = 4 << 20
-    p = PeerAllReduce(g, dev, cap)
+    # W processes time-share one GPU here: a generous barrier time-out, so scheduling stalls are not
+    # mistaken for a dead peer (a time-out poisons the communicator and later results are garbage)
+    p = PeerAllReduce(g, dev, cap, timeout_ms=120000)
     assert p.ok, p.reason
     sums = []
     for dt in (torch.float32, torch.bfloat16):
@@ -300,6 +302,7 @@ def case_peer_allreduce(graph="1"):
                 x = xs[R].to(dev)
                 p.all_reduce_(x, algo)
                 torch.cuda.synchronize()
+                assert p.error() == 0, ("peer barrier timed out", dt, n, algo, p.error())
                 err = (x.double().cpu() - ref).abs().max().item()
                 tol = 1e-5 * W if dt == torch.float32 else 0.02 * W
                 assert err <= tol * max(1.0, ref.abs().max().item()), (dt, n, algo, err)
