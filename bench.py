@@ -14,22 +14,32 @@ Adam update, loss/accuracy meters.  Each rank trains on its DistributedSampler s
   python bench.py --gpus N --steps K --warmup W
   (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...)
 
-W untimed warm-up steps, then exactly K steps bracketed by barrier + device synchronize on both
-sides; the elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+Every captured hipGraph is replayed once before the W untimed warm-up steps (a graph's first launch
+pays its instantiation/upload, never inside the timed window); then exactly K steps are timed,
+bracketed by barrier + device synchronize on both sides; the elapsed time is the MAX over ranks;
+rank 0 prints one JSON line.  A failure still prints one JSON line (``value`` null, ``error``) and
+exits non-zero, and so does a communication-health failure (peer barrier time-out, RCCL error):
+a poisoned peer path skips its barriers and would otherwise report an inflated number.
+
+At W=1 the line also carries ``w1_rccl_comm``: the same step measured a second time with an RCCL
+communicator initialised and the full W>1 communication path running (config 2 of BASELINE.json:
+"DDP world_size=1 ... RCCL init + HIP kernels"); the headline ``value`` stays the comm-free step.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
+import traceback
 
 BASELINE_METRIC = "images/sec (whole node) + DDP scaling eff, toy CNN synthetic MNIST 1/2/4/8 GPU"
 STOCK_TORCH_W1 = 121442.1   # same-hardware stock-PyTorch reference loop, W=1 (profiles/baseline/)
 
 
-def main():
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -43,54 +53,85 @@ def main():
     ap.add_argument("--force-comm", action="store_true",
                     help="run the W>1 communication path (buckets, routes, split optimizer) even at W=1")
     ap.add_argument("--no-autotune", action="store_true", help="W>1: skip the whole-step schedule autotuning")
+    ap.add_argument("--autotune-budget-s", type=float, default=60.0,
+                    help="wall-clock budget of the schedule autotuner (candidates left untimed past it)")
+    ap.add_argument("--comm-figure", choices=["auto", "on", "off"], default="auto",
+                    help="W=1: also time the step with RCCL initialised + the comm path on (auto = on at W=1)")
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--model", choices=["lenet", "gpt2", "resnet18"], default="lenet",
                     help="lenet = the BASELINE headline (default); gpt2 / resnet18 = the driver-added configs")
     ap.add_argument("--seq-len", type=int, default=1024, help="gpt2: sequence length")
-    ap.add_argument("--bucket-mb", type=float, default=64.0, help="gpt2/resnet18: DDP gradient bucket size")
-    args = ap.parse_args()
-    if args.model != "lenet":
-        from bench_models import run_model_bench
-        return run_model_bench(args)
+    ap.add_argument("--bucket-mb", type=str, default="auto",
+                    help="gpt2/resnet18: DDP gradient bucket cap in MB, or 'auto' (timed sweep at W>1)")
+    return ap
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Job:
+    """Per-process state shared by the headline run and the W=1 comm figure."""
+
+    def __init__(self, args):
+        self.args = args
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = 0 if args.shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _comm_info(dist, comm, eng):
+    """What the communication path actually ran on (proof that RCCL saw N ranks)."""
+    if comm is None:
+        return {}
+    info = {"rccl_world": None, "rccl_device": None, "peer_ok": comm.peer is not None}
+    rc = comm.group.rccl
+    if rc is not None:
+        try:
+            info["rccl_world"] = rc.comm_count()
+            info["rccl_device"] = rc.cu_device()
+        except Exception as e:   # noqa: BLE001 - report, never fail the bench on a query
+            info["rccl_query_error"] = str(e)
+    if comm.peer is None:
+        reason = getattr(comm, "peer_reason", "")
+        if reason:
+            info["peer_reason"] = reason
+    if eng is not None and eng.comm_on:
+        info["schedule"] = getattr(eng, "schedule", eng.mode)
+        info["routes"] = {str(k): v for k, v in comm.routes.items()}
+        info["route_us_per_call"] = {str(k): v for k, v in comm.timings.items()}
+    return info
+
+
+def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world: bool):
+    """Builds the engine, times ``steps`` steps, returns (elapsed_s, eng, comm, extra)."""
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_distributed_example_amd import dist
     from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_mnist
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
     from pytorch_distributed_example_amd.models import build_net
     from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
-    if args.shared_gpu:
-        local_rank = 0
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    args, world, rank = job.args, job.world, job.rank
+    dev = torch.device("cuda", job.local_rank)
     comm = None
     with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
-        if world > 1 or args.force_comm:
-            init = "env://" if "MASTER_PORT" in os.environ else "tcp://127.0.0.1:29533"
-            dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method=init, rank=rank,
-                                    world_size=world)
+        if comm_world:
+            if not dist.is_initialized():
+                init = ("env://" if "MASTER_PORT" in os.environ
+                        else f"tcp://127.0.0.1:{_free_port()}")
+                dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method=init, rank=rank,
+                                        world_size=world)
             comm = dist.engine_comm(allow_host_only=args.shared_gpu)
         net = build_net(seed=args.seed, device=dev)
         if comm is not None:
             dist.broadcast_parameters(net)            # DDP semantics: replicas start identical
         eng = LeNetTrainStep(net, batch_size=args.batch_size, lr=1e-3, comm=comm, overlap=not args.no_overlap,
-                             force_comm=args.force_comm)
-    routes = {}
-    if comm is not None and eng.comm_on:
-        routes = {"routes": {str(k): v for k, v in comm.routes.items()},
-                  "route_us_per_call": {str(k): v for k, v in comm.timings.items()}}
-        if comm.peer is None and os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0":
-            print("note: xGMI peer all-reduce unavailable, RCCL only", file=sys.stderr)
+                             force_comm=force_comm)
     train = synthetic_mnist(args.train_size, seed=args.seed, device=dev, kind="fashion")
     eng.bind_dataset(train.images, train.labels)
     sampler = DistributedSampler(train, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
@@ -99,6 +140,7 @@ def main():
     eng.set_epoch_indices(idx[: nfull * args.batch_size])   # full batches only: every timed step is B=128
 
     S = max(1, args.graph_steps)
+    extra = {}
 
     def run(n):
         if args.mode == "graph":
@@ -112,68 +154,115 @@ def main():
 
     if eng.comm_on and not args.no_autotune:
         # time every communication schedule (bucket routes x overlap) on whole steps, keep the fastest
-        routes["schedule_us_per_step"] = eng.autotune_schedule(graph_steps=S)
-        routes["schedule"] = eng.schedule
+        extra["schedule_us_per_step"] = eng.autotune_schedule(graph_steps=S, budget_s=args.autotune_budget_s)
+        health = comm.health()
+        if health:
+            raise RuntimeError(f"communication failure during schedule autotuning: {health}")
     if args.mode == "graph":
         eng.capture(steps=S)
         eng.capture(steps=1)
-    run(args.warmup)
+        eng.replay(steps=S)                     # first launch of each graph: untimed
+        eng.replay(steps=1)
+    run(warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps)
+    run(steps)
     torch.cuda.synchronize()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if comm is not None:
+    if comm is not None and world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    health = comm.health() if comm is not None else ""
-    if health:
-        print(f"error: communication failure during the timed steps: {health}", file=sys.stderr)
+    if comm is not None:
+        health = comm.health()
+        if health:
+            raise RuntimeError(f"communication failure during the timed steps: {health}")
+    return elapsed, eng, comm, extra
+
+
+def lenet_main(job: _Job):
+    import torch
+
+    from pytorch_distributed_example_amd import dist
+
+    args, world, rank = job.args, job.world, job.rank
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(job.local_rank)
+    comm_world = world > 1 or args.force_comm
+    elapsed, eng, comm, extra = _run_lenet(job, args.force_comm, args.steps, args.warmup, comm_world)
     loss_sum, correct, _ = eng.read_meters()
     n_img = args.steps * args.batch_size * world
     ips = n_img / elapsed
+    S = max(1, args.graph_steps)
+    out = {
+        "metric": BASELINE_METRIC,
+        "value": round(ips, 1),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (class-conditional MNIST-shaped, device resident), random-init weights",
+        "config": {
+            "model": "toy CNN Net (conv5x5 20 -> conv5x5 50 -> fc 500 -> fc 10), 431,080 params",
+            "global_batch": args.batch_size * world,
+            "per_gpu_batch": args.batch_size,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "optimizer": "Adam(lr=1e-3)",
+            "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
+            "grad_allreduce": "none" if not eng.comm_on else eng.mode,
+            **_comm_info(dist, comm, eng),
+            **extra,
+        },
+        "stock_torch_same_hw_w1_images_per_s": STOCK_TORCH_W1,
+        "speedup_vs_stock_torch_per_gpu": round(ips / world / STOCK_TORCH_W1, 2),
+        "train_loss_mean_timed_rank0": round(loss_sum / max(1, args.steps * args.batch_size), 5),
+        "train_acc_timed_rank0": round(correct / max(1, args.steps * args.batch_size), 5),
+    }
+    want_fig = args.comm_figure == "on" or (args.comm_figure == "auto" and world == 1 and not args.force_comm)
+    if want_fig and world == 1:
+        # config 2 (BASELINE.json): the same step with RCCL initialised and the comm path running
+        try:
+            e2, eng2, comm2, extra2 = _run_lenet(job, True, args.steps, args.warmup, True)
+            out["w1_rccl_comm"] = {"value": round(args.steps * args.batch_size / e2, 1),
+                                   "ms_per_step": round(e2 / args.steps * 1e3, 5),
+                                   "grad_allreduce": eng2.mode, **_comm_info(dist, comm2, eng2), **extra2}
+        except Exception as e:   # noqa: BLE001 - the headline stands; report the secondary failure
+            out["w1_rccl_comm"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
-        out = {
-            "metric": BASELINE_METRIC,
-            "value": round(ips, 1),
-            "unit": "images/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (class-conditional MNIST-shaped, device resident), random-init weights",
-            "config": {
-                "model": "toy CNN Net (conv5x5 20 -> conv5x5 50 -> fc 500 -> fc 10), 431,080 params",
-                "global_batch": args.batch_size * world,
-                "per_gpu_batch": args.batch_size,
-                "seq_len": None,
-                "parallelism": f"dp{world}",
-                "optimizer": "Adam(lr=1e-3)",
-                "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
-                "grad_allreduce": "none" if not eng.comm_on else eng.mode,
-                **routes,
-            },
-            "comm_errors": health or None,
-            "stock_torch_same_hw_w1_images_per_s": STOCK_TORCH_W1,
-            "speedup_vs_stock_torch_per_gpu": round(ips / world / STOCK_TORCH_W1, 2),
-            "train_loss_mean_timed_rank0": round(loss_sum / max(1, args.steps * args.batch_size), 5),
-            "train_acc_timed_rank0": round(correct / max(1, args.steps * args.batch_size), 5),
-        }
         print(json.dumps(out), flush=True)
-    if comm is not None:
+    if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def main():
+    args = build_parser().parse_args()
+    job = _Job(args)
+    try:
+        if args.model != "lenet":
+            from bench_models import run_model_bench
+            return run_model_bench(args)
+        return lenet_main(job)
+    except Exception as e:   # noqa: BLE001 - always one JSON line, then a non-zero exit
+        traceback.print_exc(file=sys.stderr)
+        if job.rank == 0:
+            print(json.dumps({"metric": BASELINE_METRIC if args.model == "lenet" else args.model, "value": None,
+                              "n_gpus": job.world, "steps": args.steps, "warmup": args.warmup,
+                              "error": f"{type(e).__name__}: {e}"}), flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

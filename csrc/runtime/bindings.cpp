@@ -137,6 +137,13 @@ PYBIND11_MODULE(_runtime, m) {
              return run(c, async, [=] { cp->alltoall(ptr(in), ptr(out), bytes); });
            },
            py::arg("inp"), py::arg("out"), py::arg("bytes_per_rank"), py::arg("async_op") = false)
+      .def("p2p",
+           [](HostComm& c, std::vector<std::tuple<int, uintptr_t, int64_t>> sends,
+              std::vector<std::tuple<int, uintptr_t, int64_t>> recvs, bool async) {
+             HostComm* cp = &c;
+             return run(c, async, [=] { cp->p2p(sends, recvs); });
+           },
+           py::arg("sends"), py::arg("recvs"), py::arg("async_op") = false)
       .def("send",
            [](HostComm& c, uintptr_t buf, int64_t bytes, int dst, bool async) {
              HostComm* cp = &c;
@@ -184,7 +191,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("split", &RcclComm::split, py::call_guard<py::gil_scoped_release>())
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy, py::call_guard<py::gil_scoped_release>())
-      .def("async_error", &RcclComm::async_error);
+      .def("async_error", &RcclComm::async_error)
+      .def("comm_count", &RcclComm::comm_count)
+      .def("cu_device", &RcclComm::cu_device);
   py::class_<CommWatchdog, std::shared_ptr<CommWatchdog>>(m, "CommWatchdog")
       .def(py::init<std::shared_ptr<RcclComm>, int64_t, int>(), py::arg("comm"), py::arg("timeout_ms"),
            py::arg("poll_ms") = 20)

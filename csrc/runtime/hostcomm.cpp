@@ -259,9 +259,17 @@ void HostComm::exchange(std::vector<Xfer>& ops) {
     pf.clear();
     idx.clear();
     for (size_t i = 0; i < ops.size(); ++i) {
+      // several transfers to one peer (point-to-point batches) progress strictly in list order per
+      // direction: the byte streams of two sends to one socket must not interleave
+      bool send_turn = true, recv_turn = true;
+      for (size_t j = 0; j < i; ++j) {
+        if (ops[j].peer != ops[i].peer) continue;
+        if (sent[j] < ops[j].sn) send_turn = false;
+        if (got[j] < ops[j].rn) recv_turn = false;
+      }
       short ev = 0;
-      if (sent[i] < ops[i].sn) ev |= POLLOUT;
-      if (got[i] < ops[i].rn) ev |= POLLIN;
+      if (send_turn && sent[i] < ops[i].sn) ev |= POLLOUT;
+      if (recv_turn && got[i] < ops[i].rn) ev |= POLLIN;
       if (ev) {
         pf.push_back({fds_[ops[i].peer], ev, 0});
         idx.push_back((int)i);
@@ -439,6 +447,24 @@ void HostComm::alltoall(const void* in, void* out, int64_t b) {
   std::vector<Xfer> ops;
   for (int j = 0; j < world_; ++j)
     if (j != rank_) ops.push_back({j, i + (size_t)j * b, (size_t)b, o + (size_t)j * b, (size_t)b});
+  exchange(ops);
+}
+
+void HostComm::p2p(const std::vector<std::tuple<int, uintptr_t, int64_t>>& sends,
+                   const std::vector<std::tuple<int, uintptr_t, int64_t>>& recvs) {
+  // one full-duplex exchange for a whole batch of sends and receives: a pairwise exchange whose
+  // payload exceeds the socket buffers cannot deadlock (both sides read while they write)
+  std::vector<Xfer> ops;
+  for (const auto& s : sends) {
+    const int p = std::get<0>(s);
+    if (p < 0 || p >= world_ || p == rank_) throw std::invalid_argument("p2p: bad destination rank");
+    ops.push_back({p, reinterpret_cast<const char*>(std::get<1>(s)), (size_t)std::get<2>(s), nullptr, 0});
+  }
+  for (const auto& r : recvs) {
+    const int p = std::get<0>(r);
+    if (p < 0 || p >= world_ || p == rank_) throw std::invalid_argument("p2p: bad source rank");
+    ops.push_back({p, nullptr, 0, reinterpret_cast<char*>(std::get<1>(r)), (size_t)std::get<2>(r)});
+  }
   exchange(ops);
 }
 

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "store.h"
@@ -57,6 +58,8 @@ class HostComm {
   void gather(const void* in, void* out, int64_t bytes, int root);
   void scatter(const void* in, void* out, int64_t bytes, int root);
   void alltoall(const void* in, void* out, int64_t bytes_per_rank);
+  void p2p(const std::vector<std::tuple<int, uintptr_t, int64_t>>& sends,
+           const std::vector<std::tuple<int, uintptr_t, int64_t>>& recvs);
   void send(const void* buf, int64_t bytes, int dst);
   void recv(void* buf, int64_t bytes, int src);
   void barrier();

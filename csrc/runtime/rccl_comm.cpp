@@ -173,6 +173,18 @@ void RcclComm::destroy() {
   if (c) ncclCommDestroy(c);
 }
 
+int RcclComm::comm_count() const {
+  int n = 0;
+  nccl_check(ncclCommCount(get(), &n), "ncclCommCount");
+  return n;
+}
+
+int RcclComm::cu_device() const {
+  int d = -1;
+  nccl_check(ncclCommCuDevice(get(), &d), "ncclCommCuDevice");
+  return d;
+}
+
 std::string RcclComm::async_error() {
   ncclComm_t c = comm_.load();
   if (!c) return "destroyed";

@@ -45,6 +45,8 @@ class RcclComm {
   void abort();
   void destroy();
   std::string async_error();
+  int comm_count() const;   // ncclCommCount: ranks RCCL itself sees in this communicator
+  int cu_device() const;    // ncclCommCuDevice: the HIP device RCCL bound this rank to
 
  private:
   explicit RcclComm(ncclComm_t c, int device);

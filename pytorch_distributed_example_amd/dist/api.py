@@ -141,6 +141,22 @@ class Work:
             self._group.check_health()
 
 
+class _DeferredP2P(Work):
+    """Handle of a batched host isend/irecv: waiting starts the group's pending batch."""
+
+    def __init__(self, group, keep):
+        super().__init__(keep=keep)
+        self._pg = group
+
+    def wait(self, timeout=None):
+        self._pg.p2p_flush()
+        return super().wait(timeout)
+
+    def is_completed(self):
+        self._pg.p2p_flush()
+        return super().is_completed()
+
+
 class _Completed(Work):
     def __init__(self):
         super().__init__()
@@ -167,6 +183,20 @@ class ProcessGroup:
         self.watchdog = None
         if rccl is not None and os.environ.get("PDE_RCCL_WATCHDOG", "1") != "0":
             self.watchdog = runtime().CommWatchdog(rccl, timeout_ms)
+        # host isend/irecv are batched until the first wait / collective: one full-duplex exchange
+        # then moves them all, so a pairwise exchange larger than the socket buffers cannot deadlock
+        self._p2p_pending = []
+
+    def p2p_flush(self):
+        """Start every deferred host isend/irecv as ONE exchange (in program order)."""
+        if not self._p2p_pending:
+            return
+        pend, self._p2p_pending = self._p2p_pending, []
+        sends = [(peer, t.data_ptr(), t.numel() * t.element_size()) for kind, peer, t, _ in pend if kind == "s"]
+        recvs = [(peer, t.data_ptr(), t.numel() * t.element_size()) for kind, peer, t, _ in pend if kind == "r"]
+        native = self.host.p2p(sends, recvs, True)
+        for _, _, t, w in pend:
+            w._native = native
 
     def check_health(self):
         if self.watchdog is not None:
@@ -437,6 +467,12 @@ def _gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool, what: str = "colle
     return None
 
 
+def _host(g: ProcessGroup):
+    """The group's host collective, after any deferred point-to-point batch (program order)."""
+    g.p2p_flush()
+    return g.host
+
+
 def _host_staged(tensors, fn):
     """GPU tensors on a host-only group: stage through CPU (gloo semantics)."""
     cpu = [t.detach().cpu() for t in tensors]
@@ -455,9 +491,9 @@ def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool
         return _gpu_launch(g, [tensor], lambda s: g.rccl.all_reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt,
                                                                      code, s), async_op)
     if tensor.is_cuda:
-        _host_staged([tensor], lambda c: g.host.allreduce(c[0].data_ptr(), n, dt, code))
+        _host_staged([tensor], lambda c: _host(g).allreduce(c[0].data_ptr(), n, dt, code))
         return _Completed() if async_op else None
-    w = g.host.allreduce(tensor.data_ptr(), n, dt, code, async_op)
+    w = _host(g).allreduce(tensor.data_ptr(), n, dt, code, async_op)
     return Work(native=w, keep=(tensor,)) if async_op else None
 
 
@@ -472,9 +508,9 @@ def broadcast(tensor: torch.Tensor, src: int = 0, group=None, async_op: bool = F
                                                                     tensor.numel(), _DTYPES[tensor.dtype], root, s),
                            async_op)
     if tensor.is_cuda:
-        _host_staged([tensor], lambda c: g.host.broadcast(c[0].data_ptr(), c[0].numel() * c[0].element_size(), root))
+        _host_staged([tensor], lambda c: _host(g).broadcast(c[0].data_ptr(), c[0].numel() * c[0].element_size(), root))
         return _Completed() if async_op else None
-    w = g.host.broadcast(tensor.data_ptr(), tensor.numel() * tensor.element_size(), root, async_op)
+    w = _host(g).broadcast(tensor.data_ptr(), tensor.numel() * tensor.element_size(), root, async_op)
     return Work(native=w, keep=(tensor,)) if async_op else None
 
 
@@ -494,10 +530,10 @@ def all_gather_into_tensor(output_tensor: torch.Tensor, input_tensor: torch.Tens
                            async_op)
     if input_tensor.is_cuda:
         def f(c):
-            g.host.allgather(c[1].data_ptr(), c[0].data_ptr(), c[1].numel() * c[1].element_size())
+            _host(g).allgather(c[1].data_ptr(), c[0].data_ptr(), c[1].numel() * c[1].element_size())
         _host_staged([output_tensor, input_tensor], f)
         return _Completed() if async_op else None
-    w = g.host.allgather(input_tensor.data_ptr(), output_tensor.data_ptr(),
+    w = _host(g).allgather(input_tensor.data_ptr(), output_tensor.data_ptr(),
                          input_tensor.numel() * input_tensor.element_size(), async_op)
     return Work(native=w, keep=(output_tensor, input_tensor)) if async_op else None
 
@@ -534,10 +570,10 @@ def reduce_scatter_tensor(output: torch.Tensor, input: torch.Tensor, op=ReduceOp
         return _gpu_launch(g, [output, input], lambda s: g.rccl.reduce_scatter(input.data_ptr(), output.data_ptr(),
                                                                                output.numel(), dt, code, s), async_op)
     if input.is_cuda:
-        _host_staged([output, input], lambda c: g.host.reduce_scatter(c[1].data_ptr(), c[0].data_ptr(),
+        _host_staged([output, input], lambda c: _host(g).reduce_scatter(c[1].data_ptr(), c[0].data_ptr(),
                                                                       c[0].numel(), dt, code))
         return _Completed() if async_op else None
-    w = g.host.reduce_scatter(input.data_ptr(), output.data_ptr(), output.numel(), dt, code, async_op)
+    w = _host(g).reduce_scatter(input.data_ptr(), output.data_ptr(), output.numel(), dt, code, async_op)
     return Work(native=w, keep=(output, input)) if async_op else None
 
 
@@ -556,9 +592,9 @@ def reduce(tensor: torch.Tensor, dst: int = 0, op=ReduceOp.SUM, group=None, asyn
         return _gpu_launch(g, [tensor], lambda s: g.rccl.reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt, code,
                                                                  root, s), async_op)
     if tensor.is_cuda:
-        _host_staged([tensor], lambda c: g.host.reduce(c[0].data_ptr(), n, dt, code, root))
+        _host_staged([tensor], lambda c: _host(g).reduce(c[0].data_ptr(), n, dt, code, root))
         return _Completed() if async_op else None
-    w = g.host.reduce(tensor.data_ptr(), n, dt, code, root, async_op)
+    w = _host(g).reduce(tensor.data_ptr(), n, dt, code, root, async_op)
     return Work(native=w, keep=(tensor,)) if async_op else None
 
 
@@ -590,7 +626,7 @@ def scatter(tensor: torch.Tensor, scatter_list: Optional[List[torch.Tensor]] = N
     cpu_in = (torch.stack([t.detach().cpu().reshape(tensor.shape) for t in scatter_list]).contiguous()
               if g.rank() == root else torch.empty(0, dtype=tensor.dtype))
     out = torch.empty(tensor.shape, dtype=tensor.dtype).contiguous()
-    g.host.scatter(cpu_in.data_ptr() if g.rank() == root else 0, out.data_ptr(), out.numel() * out.element_size(),
+    _host(g).scatter(cpu_in.data_ptr() if g.rank() == root else 0, out.data_ptr(), out.numel() * out.element_size(),
                    root)
     tensor.copy_(out)
     return _Completed() if async_op else None
@@ -610,10 +646,10 @@ def all_to_all_single(output: torch.Tensor, input: torch.Tensor, output_split_si
         return _gpu_launch(g, [output, input], lambda s: g.rccl.all_to_all(input.data_ptr(), output.data_ptr(), per,
                                                                            _DTYPES[input.dtype], s), async_op)
     if input.is_cuda:
-        _host_staged([output, input], lambda c: g.host.alltoall(c[1].data_ptr(), c[0].data_ptr(),
+        _host_staged([output, input], lambda c: _host(g).alltoall(c[1].data_ptr(), c[0].data_ptr(),
                                                                 per * c[1].element_size()))
         return _Completed() if async_op else None
-    w = g.host.alltoall(input.data_ptr(), output.data_ptr(), per * input.element_size(), async_op)
+    w = _host(g).alltoall(input.data_ptr(), output.data_ptr(), per * input.element_size(), async_op)
     return Work(native=w, keep=(output, input)) if async_op else None
 
 
@@ -626,7 +662,7 @@ def send(tensor: torch.Tensor, dst: int, group=None, tag: int = 0):
                                                        peer, s), False)
         return
     t = tensor.detach().cpu().contiguous() if tensor.is_cuda else tensor
-    g.host.send(t.data_ptr(), t.numel() * t.element_size(), peer)
+    _host(g).send(t.data_ptr(), t.numel() * t.element_size(), peer)
 
 
 def recv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int = 0):
@@ -641,11 +677,18 @@ def recv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int =
         return src
     if tensor.is_cuda:
         c = torch.empty(tensor.shape, dtype=tensor.dtype)
-        g.host.recv(c.data_ptr(), c.numel() * c.element_size(), peer)
+        _host(g).recv(c.data_ptr(), c.numel() * c.element_size(), peer)
         tensor.copy_(c)
     else:
-        g.host.recv(tensor.data_ptr(), tensor.numel() * tensor.element_size(), peer)
+        _host(g).recv(tensor.data_ptr(), tensor.numel() * tensor.element_size(), peer)
     return src
+
+
+def _defer(g: ProcessGroup, kind: str, tensor: torch.Tensor, peer: int) -> Work:
+    _check(tensor)
+    w = _DeferredP2P(g, keep=(tensor,))
+    g._p2p_pending.append((kind, g.group_rank(peer), tensor, w))
+    return w
 
 
 def isend(tensor: torch.Tensor, dst: int, group=None, tag: int = 0):
@@ -653,8 +696,7 @@ def isend(tensor: torch.Tensor, dst: int, group=None, tag: int = 0):
     if tensor.is_cuda:
         send(tensor, dst, g, tag)
         return _Completed()
-    return Work(native=g.host.send(tensor.data_ptr(), tensor.numel() * tensor.element_size(), g.group_rank(dst),
-                                   True), keep=(tensor,))
+    return _defer(g, "s", tensor, dst)
 
 
 def irecv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int = 0):
@@ -662,8 +704,7 @@ def irecv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int 
     if tensor.is_cuda or src is None:
         recv(tensor, src, g, tag)
         return _Completed()
-    return Work(native=g.host.recv(tensor.data_ptr(), tensor.numel() * tensor.element_size(), g.group_rank(src),
-                                   True), keep=(tensor,))
+    return _defer(g, "r", tensor, src)
 
 
 class P2POp:
@@ -678,7 +719,7 @@ class P2POp:
 def batch_isend_irecv(p2p_op_list: List[P2POp]) -> List[Work]:
     """Issue a set of sends/receives together.  GPU: one ``ncclGroupStart/End`` on the comm stream, so
     any send/recv pattern (rings, exchanges, all-to-all by hand) progresses without deadlock.  Host:
-    all sends are queued asynchronously before the receives are posted."""
+    one full-duplex socket exchange over all of the batch's sends and receives."""
     if not p2p_op_list:
         return []
     g = _group(p2p_op_list[0].group)
@@ -698,21 +739,23 @@ def batch_isend_irecv(p2p_op_list: List[P2POp]) -> List[Work]:
                 g.rccl.group_end()
         w = _gpu_launch(g, [o.tensor for o in p2p_op_list], fn, True)
         return [w]
-    sends = [o for o in p2p_op_list if o.op is isend]
-    recvs = [o for o in p2p_op_list if o.op is irecv]
+    # host: every send and receive of the batch in ONE full-duplex exchange (GPU tensors staged)
+    staged = []
     works = []
-    for o in sends:
-        t = o.tensor.detach().cpu().contiguous() if o.tensor.is_cuda else o.tensor
-        works.append(Work(native=g.host.send(t.data_ptr(), t.numel() * t.element_size(), g.group_rank(o.peer),
-                                             True), keep=(t,)))
-    for o in recvs:
-        if o.tensor.is_cuda:
-            recv(o.tensor, o.peer, g)
-            works.append(_Completed())
-        else:
-            t = o.tensor
-            works.append(Work(native=g.host.recv(t.data_ptr(), t.numel() * t.element_size(), g.group_rank(o.peer),
-                                                 True), keep=(t,)))
+    for o in p2p_op_list:
+        t = o.tensor
+        if t.is_cuda:
+            c = t.detach().cpu().contiguous() if o.op is isend else torch.empty(t.shape, dtype=t.dtype)
+            staged.append((o, c))
+            t = c
+        works.append(_defer(g, "s" if o.op is isend else "r", t, o.peer))
+    g.p2p_flush()
+    if staged:
+        for w in works:
+            w.wait()
+        for o, c in staged:
+            if o.op is irecv:
+                o.tensor.copy_(c)
     return works
 
 
@@ -722,7 +765,7 @@ def barrier(group=None, async_op: bool = False, device_ids=None):
         return None
     if g.rccl is not None and torch.cuda.is_available():
         torch.cuda.synchronize(g.device)          # device work issued before the barrier is done
-    w = g.host.barrier(async_op)
+    w = _host(g).barrier(async_op)
     return Work(native=w) if async_op else None
 
 
@@ -745,6 +788,7 @@ class EngineComm:
         self.world_size = group.size()
         self.rank = group.rank()
         self.peer = None
+        self.peer_reason = ""
         self.routes = {}
         self.timings = {}
 
@@ -761,7 +805,10 @@ class EngineComm:
         if os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0":
             self.peer = PeerAllReduce(self.group, torch.device(device), cap)
             if not self.peer.ok:
+                self.peer_reason = self.peer.reason
                 self.peer = None
+        else:
+            self.peer_reason = "disabled by PDE_PEER_ALLREDUCE=0"
         rccl_fn = self._rccl if self.group.rccl is not None else None
         if tune:
             self.routes, self.timings = tune_routes(self.group, self.peer, rccl_fn, sizes, device, dtype)

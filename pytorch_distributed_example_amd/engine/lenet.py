@@ -374,9 +374,12 @@ class LeNetTrainStep:
             out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in routes]
             if self.optimizer == "adam":         # last: a failing candidate poisons the peer protocol
                 out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in ("adam1", "adam2")]
-        return out
+        # RCCL-only schedules first: they are timed even if the budget or the peer protocol runs out
+        uses_peer = lambda c: c[0] == "fused" or any(r != "rccl" for r in c[1].values())
+        return sorted(out, key=uses_peer)
 
-    def autotune_schedule(self, steps: int = 40, graph_steps: int = 10, candidates=None):
+    def autotune_schedule(self, steps: int = 40, graph_steps: int = 10, candidates=None,
+                          budget_s: float = 60.0):
         """Pick the fastest communication schedule by timing WHOLE training steps on this node.
 
         Isolated all-reduce timings (``dist.peer.tune_routes``) miss the interaction with the kernels
@@ -384,7 +387,13 @@ class LeNetTrainStep:
         RCCL kernel may not get a CU until it finishes), so every candidate schedule runs ``steps``
         real steps (hipGraph replays, as in training); the per-candidate MAX over ranks decides, so
         every rank picks the same one.  Model / optimizer / data-position state is snapshotted and
-        restored: autotuning does not change training.  Returns {candidate label: us per step}."""
+        restored: autotuning does not change training.  Returns {candidate label: us per step}.
+
+        Bounded: candidates are timed in order (RCCL-only schedules first, the peer-protocol ones
+        after) until ``budget_s`` of wall clock has passed; the stop decision is the MAX of the
+        ranks' elapsed times, so every rank stops at the same candidate and the rest count as
+        untimed.  A peer-protocol failure (barrier time-out) invalidates every later peer candidate
+        on every rank; if no candidate survives, the RCCL-only "overlap" schedule is kept."""
         if not self.comm_on:
             return {}
         cands = candidates or self.schedule_candidates()
@@ -397,7 +406,15 @@ class LeNetTrainStep:
         times, invalid = [], []
         peer = getattr(self.comm, "peer", None)
         wd = g.watchdog
+        import time as _time
+        t_start = _time.perf_counter()
         for mode, routes in cands:
+            el = torch.tensor([_time.perf_counter() - t_start], dtype=torch.float64)
+            g.host.allreduce(el.data_ptr(), 1, 1, 3)          # float64 MAX: one decision for all ranks
+            if el.item() > budget_s:
+                times.append(float("inf"))
+                invalid.append(1)
+                continue
             uses_peer = mode == "fused" or any(r != "rccl" for r in routes.values())
             perr0 = peer.error() if peer is not None else 0
             anyerr = torch.tensor([perr0], dtype=torch.int64)
@@ -439,7 +456,11 @@ class LeNetTrainStep:
         g.host.allreduce(bad.data_ptr(), bad.numel(), 3, 3)  # int64 MAX: invalid anywhere -> invalid
         times = [float("inf") if b else x for x, b in zip(t.tolist(), bad.tolist())]
         if all(x == float("inf") for x in times):
-            raise RuntimeError("no communication schedule kept the replicas identical (comm failure?)")
+            if g.rccl is None:
+                raise RuntimeError("no communication schedule kept the replicas identical (comm failure?)")
+            n0, n1 = self.bucket_grads[0].numel(), self.bucket_grads[1].numel()
+            cands = list(cands) + [("overlap", {n0: "rccl", n1: "rccl"})]   # bounded fallback: RCCL only
+            times.append(0.0)
         best = min(range(len(cands)), key=lambda i: times[i])
         self.mode, self.comm.routes = cands[best][0], dict(cands[best][1])
         self.graphs.clear()

@@ -86,8 +86,10 @@ class Trainer(object):
         self.manual_average = manual_average    # reference path: per-parameter all-reduce after backward
         self.printer = print
 
-    def fit(self, epochs):
-        for epoch in range(1, epochs + 1):
+    def fit(self, epochs, start_epoch: int = 0):
+        """Epochs ``start_epoch+1 .. epochs`` (a resumed run passes the checkpoint's epoch, so the
+        sampler's ``set_epoch`` and the printed ``e/E`` use the absolute epoch)."""
+        for epoch in range(start_epoch + 1, epochs + 1):
             if hasattr(self.train_loader.sampler, "set_epoch") and getattr(self, "set_epoch", False):
                 self.train_loader.sampler.set_epoch(epoch)
             train_loss, train_acc = self.train()
@@ -170,8 +172,8 @@ class FusedTrainer(object):
         self.printer = print
         engine.bind_dataset(train_set.images, train_set.labels)
 
-    def fit(self, epochs):
-        for epoch in range(1, epochs + 1):
+    def fit(self, epochs, start_epoch: int = 0):
+        for epoch in range(start_epoch + 1, epochs + 1):
             if self.set_epoch and hasattr(self.sampler, "set_epoch"):
                 self.sampler.set_epoch(epoch)
             train_loss, train_acc = self.train()
@@ -184,10 +186,24 @@ class FusedTrainer(object):
                 'train loss: {}, train acc: {},'.format(train_loss, train_acc),
                 'test loss: {}, test acc: {}.'.format(test_loss, test_acc))
 
+    def check_comm_health(self):
+        """Raise if the engine's communication path failed (xGMI peer barrier time-out, RCCL error).
+
+        A timed-out peer barrier poisons the peer protocol on purpose: later all-reduces skip their
+        barriers and would reduce stale data, so replicas would diverge silently.  Raising makes the
+        rank exit non-zero and the launcher tear the gang down instead."""
+        comm = getattr(self.engine, "comm", None)
+        if comm is None or not hasattr(comm, "health"):
+            return
+        h = comm.health()
+        if h:
+            raise RuntimeError(f"data-parallel communication failed: {h}")
+
     def train(self):
         self.engine.set_epoch_indices(self.sampler.indices_tensor())
         self.engine.run_epoch(use_graph=self.use_graph)
-        loss_sum, correct, n = self.engine.read_meters()
+        loss_sum, correct, n = self.engine.read_meters()     # synchronises: the epoch's comm is done
+        self.check_comm_health()
         a, acc = Average(), Accuracy()
         a.sum, a.count = loss_sum, n
         acc.correct, acc.count = correct, n

@@ -5,7 +5,9 @@ its own shell -- /root/reference/README.md, mnist/main.py:215-220 -- and pins al
     python -m pytorch_distributed_example_amd.launch -n 3 --module some.module -- args
 
 Each child gets ``RANK``, ``LOCAL_RANK``, ``WORLD_SIZE``, ``LOCAL_WORLD_SIZE``, ``MASTER_ADDR``,
-``MASTER_PORT`` (rendezvous ``env://``) and, on ROCm, ``HSA_ENABLE_IPC_MODE_LEGACY=0`` is kept.
+``MASTER_PORT`` (rendezvous ``env://``) and, on ROCm, ``HSA_ENABLE_IPC_MODE_LEGACY=0`` is kept;
+with several ranks per node ``OMP_NUM_THREADS`` defaults to cores / ranks (CPU ranks would otherwise
+oversubscribe the host nproc-fold).
 The launcher never initialises the GPU itself (it only spawns children), monitors them, and on the
 first non-zero exit terminates the remaining ranks' process groups (so a failed rank never leaves
 its peers hung inside a collective), then exits with that code.  ``--max-restarts`` re-launches the
@@ -70,6 +72,9 @@ def run_gang(cmd, nproc, master_addr, master_port, node_rank=0, nnodes=1, log_di
                     "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": str(node_rank),
                     "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if nproc > 1 and "OMP_NUM_THREADS" not in (extra_env or {}) and "OMP_NUM_THREADS" not in os.environ:
+            # CPU ranks share the host: split its cores instead of oversubscribing them nproc-fold
+            env["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // nproc))
         p, f = _spawn(cmd, env, log_dir, rank)
         procs.append(p)
         files.append(f)

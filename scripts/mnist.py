@@ -145,21 +145,10 @@ def run(args):
     trainer.printer = printer
 
     epochs = args.epochs
-    if start_epoch:
-        # resume: run the remaining epochs but keep the "e/E" numbering of the full run
-        remaining = max(0, epochs - start_epoch)
-        orig = printer.__call__
-
-        def shifted(*parts):
-            p0 = parts[0]
-            if p0.startswith("Epoch: "):
-                e, E = p0[len("Epoch: "):-1].split("/")
-                parts = ("Epoch: {}/{},".format(int(e) + start_epoch, epochs),) + parts[1:]
-            orig(*parts)
-        trainer.printer = shifted
-        trainer.fit(remaining) if remaining else None
-    else:
-        trainer.fit(epochs)
+    # resume: epochs start_epoch+1..E, numbered (and --set-epoch seeded) as in an uninterrupted run
+    trainer.fit(epochs, start_epoch=start_epoch)
+    if engine == "fused":
+        trainer.check_comm_health()        # never checkpoint replicas a failed all-reduce let diverge
     if args.save:
         save_checkpoint(args.save, net, opt_state(), epoch=epochs, rank=rank)
 
@@ -228,7 +217,11 @@ if __name__ == '__main__':
         if '-r' in argv or '--rank' in argv:
             k = argv.index('-r') if '-r' in argv else argv.index('--rank')
             rank = argv[k + 1]
-        if rank is not None and os.environ.get("WORLD_SIZE", "1") != "1" or ('-s' in argv and argv[argv.index('-s') + 1] != '1'):
+        multi = os.environ.get("WORLD_SIZE", "1") != "1"
+        for flag in ('-s', '--world-size'):
+            if flag in argv:
+                multi = argv[argv.index(flag) + 1] != '1'
+        if rank is not None and multi:
             path = f"{path}.rank{rank}"
         cProfile.run('main()', path)
     else:

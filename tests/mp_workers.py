@@ -160,6 +160,38 @@ def case_collectives(backend="gloo", method="env"):
     dist.destroy_process_group()
 
 
+def case_p2p_large(mb="8"):
+    """Pairwise host exchange far above the socket buffers (one worker thread per group
+    used to sit in send() on both ranks): isend+irecv, batch_isend_irecv, and two sends in a row
+    to one peer (their byte streams must not interleave)."""
+    _init("gloo")
+    n = int(float(mb) * (1 << 20)) // 4
+    nxt, prv = (R + 1) % W, (R - 1) % W
+    s = torch.arange(n, dtype=torch.float32) + R * 1e6
+    r = torch.empty(n)
+    w1 = dist.isend(s, nxt)
+    w2 = dist.irecv(r, prv)
+    w1.wait()
+    w2.wait()
+    assert torch.equal(r, torch.arange(n, dtype=torch.float32) + prv * 1e6)
+    s2, r2 = s * 2, torch.empty(n)
+    for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s2, nxt), dist.P2POp(dist.irecv, r2, prv)]):
+        w.wait()
+    assert torch.equal(r2, (torch.arange(n, dtype=torch.float32) + prv * 1e6) * 2)
+    a, b = torch.full((n // 2,), 1.0 + R), torch.full((n // 3,), -2.0 - R)
+    ra, rb = torch.empty(n // 2), torch.empty(n // 3)
+    ops = [dist.P2POp(dist.isend, a, nxt), dist.P2POp(dist.isend, b, nxt),
+           dist.P2POp(dist.irecv, ra, prv), dist.P2POp(dist.irecv, rb, prv)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    assert torch.equal(ra, torch.full((n // 2,), 1.0 + prv)) and torch.equal(rb, torch.full((n // 3,), -2.0 - prv))
+    t = torch.ones(3)
+    dist.all_reduce(t)                    # a collective after p2p traffic still lines up
+    assert torch.equal(t, torch.full((3,), float(W)))
+    emit({"rank": R, "ok": True})
+    dist.destroy_process_group()
+
+
 def case_groups(backend="gloo"):
     _init(backend)
     dev = _dev(backend)

@@ -59,6 +59,13 @@ def test_collectives_tcp_w4():
     assert all(r and r["ok"] for r in res)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_p2p_large_exchange(world):
+    rc, res, logs = run_ranks("p2p_large", world, "8")
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_groups_and_toy_pattern(world):
     rc, res, logs = run_ranks("groups", world)

@@ -1,6 +1,7 @@
 """Golden-output tests for the reference-compatible CLIs (survey §4 item 7, Appendix B): the
 toy all-reduce script and the MNIST trainer on the CPU/gloo path, launched both the reference way
 (one process per rank with -i/-r/-s) and through the framework launcher."""
+import json
 import os
 import re
 import subprocess
@@ -79,6 +80,25 @@ def test_mnist_gloo_two_ranks(ddp):
     assert last[0].group(5) == last[1].group(5) and last[0].group(6) == last[1].group(6)
 
 
+def test_config1_mlp_gloo_two_ranks(tmp_path):
+    """BASELINE.json config 1: 2-layer MLP, gloo (host TCP) backend, world_size 2, CPU only."""
+    metrics = str(tmp_path / "m.jsonl")
+    lines = _mnist(["--backend", "gloo", "--eval", "--model", "mlp", "--epochs", "3", "--metrics", metrics], n=2)
+    assert lines.count("called init_process_group") == 2
+    ep = [m for m in map(EPOCH_LINE.match, lines) if m]
+    assert len(ep) == 6
+    by_rank_epoch = {}
+    for m in ep:
+        by_rank_epoch.setdefault(m.group(1), []).append(m)
+    # replicas identical: every epoch's full-test-set loss / accuracy agree to the printed digit
+    for e, ms in by_rank_epoch.items():
+        assert len(ms) == 2 and ms[0].group(5) == ms[1].group(5) and ms[0].group(6) == ms[1].group(6), e
+    train = [float(by_rank_epoch[str(e)][0].group(3)) for e in (1, 2, 3)]
+    assert train[2] < train[1] < train[0], train                 # loss decreases
+    recs = [json.loads(l) for l in open(metrics)]
+    assert len(recs) == 3 and all(r["images_per_s"] > 0 for r in recs)
+
+
 def test_mnist_save_resume(tmp_path):
     ck = str(tmp_path / "ck.pt")
     _mnist(["-s", "1", "--save", ck, "--epochs", "1"])
@@ -86,6 +106,18 @@ def test_mnist_save_resume(tmp_path):
     lines = _mnist(["-s", "1", "--resume", ck, "--epochs", "2"])
     ep = [m for m in map(EPOCH_LINE.match, lines) if m]
     assert [m.group(1) for m in ep] == ["2"]
+
+
+def test_resume_set_epoch_matches_uninterrupted(tmp_path):
+    """--resume continues the sampler's epoch numbering: with --set-epoch, epochs 1+2 in
+    one run print the same epoch-2 line as epoch 1, save, resume, epoch 2."""
+    ck = str(tmp_path / "ck.pt")
+    common = ["--backend", "gloo", "--set-epoch", "--model", "mlp", "--log-rank0-only"]
+    full = [m for m in map(EPOCH_LINE.match, _mnist(common + ["--epochs", "2"], n=2)) if m]
+    _mnist(common + ["--epochs", "1", "--save", ck], n=2)
+    res = [m for m in map(EPOCH_LINE.match, _mnist(common + ["--epochs", "2", "--resume", ck], n=2)) if m]
+    assert [m.group(1) for m in res] == ["2"]
+    assert res[0].group(0) == full[1].group(0)
 
 
 def test_read_stats(tmp_path):
