@@ -46,7 +46,8 @@ def build_parser():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch-size", type=int, default=128, help="per-GPU batch (reference default 128)")
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
-    ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph (graph mode)")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps captured per hipGraph (graph mode); 0 = the largest divisor of --steps <= 100")
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward (no bucketing)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo control group, peer all-reduce for the data")
@@ -65,6 +66,14 @@ def build_parser():
     ap.add_argument("--bucket-mb", type=str, default="auto",
                     help="gpt2/resnet18: DDP gradient bucket cap in MB, or 'auto' (timed sweep at W>1)")
     return ap
+
+
+def _graph_steps(args) -> int:
+    """Steps per captured hipGraph: fewer, longer graphs mean fewer graph-to-graph transitions in the
+    timed window (--steps 20 is one replay of a 20-step graph)."""
+    if args.graph_steps > 0:
+        return args.graph_steps
+    return max(d for d in range(1, min(100, max(1, args.steps)) + 1) if args.steps % d == 0)
 
 
 def _free_port() -> int:
@@ -139,7 +148,7 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     nfull = idx.numel() // args.batch_size
     eng.set_epoch_indices(idx[: nfull * args.batch_size])   # full batches only: every timed step is B=128
 
-    S = max(1, args.graph_steps)
+    S = _graph_steps(args)
     extra = {}
 
     def run(n):
@@ -201,7 +210,7 @@ def lenet_main(job: _Job):
     loss_sum, correct, _ = eng.read_meters()
     n_img = args.steps * args.batch_size * world
     ips = n_img / elapsed
-    S = max(1, args.graph_steps)
+    S = _graph_steps(args)
     out = {
         "metric": BASELINE_METRIC,
         "value": round(ips, 1),
