@@ -37,6 +37,11 @@ def _setup():
     return torch, dist, rank, world, torch.device("cuda", local_rank)
 
 
+def _cap(args) -> float:
+    """Initial DDP bucket cap (MB); 'auto' starts at 25 MB and ``tune_buckets`` sweeps at W>1."""
+    return 25.0 if str(args.bucket_mb) == "auto" else float(args.bucket_mb)
+
+
 def _timed(torch, dist, world, step, warmup, steps):
     for _ in range(warmup):
         step()
@@ -69,7 +74,7 @@ def bench_gpt2(args):
     T = args.seq_len
     cfg = GPTConfig(block_size=max(1024, T))
     model = build_gpt2(cfg, seed=args.seed, device=dev)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
     opt = AdamWMaster(model.decay_groups(0.1), lr=6e-4, betas=(0.9, 0.95), max_grad_norm=1.0)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + rank)

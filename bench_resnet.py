@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import json
 
-from bench_models import _setup, _timed
+from bench_models import _cap, _setup, _timed
 
 
 def bench_resnet18(args):
@@ -17,7 +17,7 @@ def bench_resnet18(args):
 
     B = args.batch_size if args.batch_size != 128 else 256
     model = build_resnet18(seed=args.seed, device=dev)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb) if world > 1 else model
+    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
     opt = SGDMaster(model.decay_groups(5e-5), lr=0.1, momentum=0.9)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + rank)

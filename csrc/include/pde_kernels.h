@@ -31,6 +31,9 @@ hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, 
                               unsigned long long* correct, int dbg, const void* peer_dev, float* ar_buf, int64_t ar_n, int ar_two,
                               hipStream_t st);
 
+void pde_lenet_set_prof(unsigned long long* buf);
+unsigned long long* pde_lenet_prof_slot(int kid);
+
 // ---- optimizers: csrc/kernels/optim.hip ----
 // fold_*: gradient replicas folded before the update: for e in [fold_off, fold_off + fold_len),
 // g[e] = sum_{r < fold_nrep} g[e + r * fold_stride] (written back); replica storage r >= 1 is skipped.
@@ -38,12 +41,29 @@ hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, fl
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
                          int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
                          int fold_nrep, int fold_stride, const void* peer_dev, long long ar_off,
-                         long long* ar_epoch, int ar_two, hipStream_t st);
+                         long long* ar_epoch, int ar_two, int pack_mode, long long fold2_off, int fold2_len,
+                         int fold2_nrep, int fold2_stride, hipStream_t st);
 hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, float momentum, float dampening,
                         float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
                         long long pack_off, float* pack_dst, long long fold_off, int fold_len, int fold_nrep,
-                        int fold_stride, hipStream_t st);
+                        int fold_stride, int pack_mode, long long fold2_off, int fold2_len, int fold2_nrep,
+                        int fold2_stride, hipStream_t st);
 hipError_t pde_lenet_pack_w2(const float* w2, float* dst, hipStream_t st);
+
+// ---- LeNet step v2: csrc/kernels/lenet_v2.hip ----
+hipError_t pde_lenet_conv_fwd2(const float* Xb, int B, const float* w1, const float* b1, const float* Wp,
+                               const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2, float* zero_ptr,
+                               int zero_n, hipStream_t st);
+hipError_t pde_lenet_gather(const float* X, const long long* labels, const int* idx, int n_idx, const long long* ctr,
+                            int nbatches, int B, float* Xdst, long long* Ydst, int* rows_dst, hipStream_t st);
+hipError_t pde_lenet_pack_w2_v2(const float* w2, float* dst, hipStream_t st);
+hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,
+                               const uint8_t* A2, const float* W2c, int B, float* gW1c, float* gb1c, int c1_nrep,
+                               int c1_rep_stride, float* gW2c, float* gb2c, int slab_stride, const float* row_loss,
+                               const int* row_hit, double* loss_sum, unsigned long long* correct, const float* gX,
+                               const long long* glabels, const int* gidx, int gn_idx, const long long* gctr,
+                               int gnbatches, int gstride, float* gXdst, long long* gYdst, int* grows, int dbg,
+                               hipStream_t st);
 hipError_t pde_scale(float* x, long long n, float s, hipStream_t st);
 
 // ---- generic ops: csrc/kernels/generic.hip ----

@@ -38,6 +38,22 @@ constexpr int kFeat = 800;     // 50*4*4
 constexpr int kHid = 500;
 constexpr int kCls = 10;
 
+// In-kernel phase timestamps (tools/lenet_phases.py): PROF instantiations record s_memrealtime
+// (100 MHz, chip-global) per block at phase boundaries into prof[block * 8 + phase]; slot 7 holds
+// the block's role.  Production launches use the PROF = false instantiations (no extra code).
+#define PMARK(ph)                                                                             \
+  do {                                                                                        \
+    if constexpr (PROF) {                                                                     \
+      if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                         \
+  } while (0)
+#define PROLE(r)                                                                              \
+  do {                                                                                        \
+    if constexpr (PROF) {                                                                     \
+      if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8 + 7] = (r);                          \
+    }                                                                                         \
+  } while (0)
+
 // -------------------------------------------------------------------------------------------------
 // Batch bookkeeping: the batch's sample rows either come from an explicit index list, or from an
 // epoch permutation indexed by a device-side batch counter (hipGraph replay needs no host work).
@@ -82,6 +98,7 @@ __device__ __forceinline__ f32x16 conv2_mainloop(const float* wa, const float* x
 constexpr int kFwdWs = 500 * 32;           // staged weight slice (floats)
 constexpr int kFwdLds = kFwdWs + kP1 + kImg + 528;
 
+template <bool PROF>
 __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, BatchSrc src,
                                                   const long long* __restrict__ labels_all,
                                                   const float* __restrict__ w1, const float* __restrict__ b1,
@@ -89,7 +106,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
                                                   float* __restrict__ P1, uint8_t* __restrict__ A1,
                                                   float* __restrict__ P2, uint8_t* __restrict__ A2,
                                                   int* __restrict__ cur_row, long long* __restrict__ cur_lbl,
-                                                  float* __restrict__ zero_ptr, int zero_n, int dbg) {
+                                                  float* __restrict__ zero_ptr, int zero_n, int dbg,
+                                                  unsigned long long* __restrict__ prof) {
+  PMARK(0);
   // dbg (ablation only): 1 skip conv1 compute, 2 skip conv2 MFMA, 4 skip weight-slice staging,
   // 8 row = b (no counter -> idx -> image load chain), 16 no P1/A1 stores, 32 no bucket zeroing
   __shared__ __attribute__((aligned(16))) float smem[kFwdLds];
@@ -103,6 +122,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
     for (int i = bid * 256 + t; i < zero_n; i += nb * 256) zero_ptr[i] = 0.f;
   }
   const int row = (dbg & 8) ? b : sample_row(src, b);
+  PMARK(1);
   // ---- phase 0: issue every global load (image + conv1 weights first, then the weight slice) ----
   const float4 xv = reinterpret_cast<const float4*>(X + (size_t)row * kImg)[min(t, kImg / 4 - 1)];
   const float4 wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
@@ -124,6 +144,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
     if (cur_lbl && labels_all) cur_lbl[b] = labels_all[row];
   }
   __syncthreads();
+  PMARK(2);
   // ---- phase 1: conv1 on v_mfma_f32_32x32x2_f32 + bias + relu + maxpool ----
   // C[m][ch] = sum_tap im2col[m][tap] * W1[ch][tap] with m = 4 * pooled_pos + sub (sub = dy*2+dx):
   // rows (r&3) of the accumulator are the 4 sub-positions of one pooled position, so the 2x2 max
@@ -169,10 +190,12 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
       }
     }
   }
+  PMARK(3);
 #pragma unroll
   for (int i = 0; i < 16; ++i)
     if (t + 256 * i < 4000) reinterpret_cast<float4*>(ws)[t + 256 * i] = tmp[i];
   __syncthreads();
+  PMARK(4);
   // ---- phase 2: conv2 implicit GEMM ----
   const int ph2 = w & 1, kk = w >> 1, khalf = l >> 5, pl = l & 31;
   const float* xb = xs + khalf * 144 + (ph2 * 4 + (pl >> 3)) * 12 + (pl & 7);
@@ -180,12 +203,14 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
   f32x16 acc = {0.f};
   if (!(dbg & 2)) acc = kk == 0 ? conv2_mainloop<0>(wa, xb) : conv2_mainloop<1>(wa, xb);
   else acc[0] = wa[0] + xb[0];
+  PMARK(5);
   __syncthreads();                         // ws is reused as the reduction buffer below
   float* red = smem;                       // [2][32][65]
 #pragma unroll
   for (int r = 0; r < 16; ++r)
     red[(kk * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 65 + ph2 * 32 + pl] = acc[r];
   __syncthreads();
+  PMARK(6);
   const int nco = ct == 0 ? 32 : 18;
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -205,6 +230,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
       A2[oi] = (uint8_t)code;
     }
   }
+  PMARK(7);
 }
 
 // =================================================================================================
@@ -215,9 +241,12 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float* __restrict__ X, B
 // counters (optimizer step, batch position): F1 of this step has already consumed them and the
 // fused Adam that follows reads the new optimizer step.
 // =================================================================================================
+template <bool PROF>
 __global__ __launch_bounds__(256) void k_fc1_fwd(const float* __restrict__ P2, int B, const float* __restrict__ W,
                                                  const float* __restrict__ bias, float* __restrict__ H1,
-                                                 long long* __restrict__ ctr, int nctr) {
+                                                 long long* __restrict__ ctr, int nctr,
+                                                 unsigned long long* __restrict__ prof) {
+  PMARK(0);
   __shared__ float red[4][16][17];
   const int nt = blockIdx.x, mt = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
   if (ctr && nt == 0 && mt == 0 && t == 0)
@@ -257,6 +286,7 @@ __global__ __launch_bounds__(256) void k_fc1_fwd(const float* __restrict__ P2, i
       }
     }
   }
+  PMARK(1);
 }
 
 // =================================================================================================
@@ -271,12 +301,15 @@ __global__ __launch_bounds__(256) void k_fc1_fwd(const float* __restrict__ P2, i
 // atomic per block after an LDS reduction.
 // Modes: dZ1 == nullptr -> forward/eval only.
 // =================================================================================================
+template <bool PROF>
 __global__ __launch_bounds__(256) void k_head(const float* __restrict__ H1, int B, const float* __restrict__ W2,
                                               const float* __restrict__ b2, const long long* __restrict__ labels,
                                               float inv_b, float* __restrict__ logp_out, float* __restrict__ dZ2,
                                               float* __restrict__ dZ1, float* __restrict__ row_loss,
                                               int* __restrict__ row_hit, double* __restrict__ loss_sum,
-                                              unsigned long long* __restrict__ correct) {
+                                              unsigned long long* __restrict__ correct,
+                                              unsigned long long* __restrict__ prof) {
+  PMARK(0);
   __shared__ float sl[4];
   __shared__ int sh[4];
   const int t = threadIdx.x, l = t & 63, wv = t >> 6, row = blockIdx.x * 4 + wv;
@@ -378,6 +411,7 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ H1, int 
     const int n = l + 64 * j;
     if (n < kHid) dZ1[(size_t)row * kHid + n] = h[j] > 0.f ? s : 0.f;
   }
+  PMARK(1);
 }
 
 // F3b (autograd path): backward of log_softmax + fc2 + ReLU from an arbitrary upstream gradient
@@ -439,6 +473,7 @@ __device__ __forceinline__ float block_sum256(float v, float* scratch) {
 // =================================================================================================
 constexpr int kBChunk = 128;   // batch rows per unrolled load batch (role A / B)
 
+template <bool PROF>
 __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, const float* __restrict__ H1,
                                                 const float* __restrict__ dZ1, const float* __restrict__ dZ2,
                                                 const float* __restrict__ W1, int B, float* __restrict__ dP2m,
@@ -446,7 +481,8 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
                                                 float* __restrict__ gW2, float* __restrict__ gb2,
                                                 const float* __restrict__ row_loss, const int* __restrict__ row_hit,
                                                 double* __restrict__ loss_sum, unsigned long long* __restrict__ correct,
-                                                int dbg, int part) {
+                                                int dbg, int part, unsigned long long* __restrict__ prof) {
+  PMARK(0);
   // dbg (ablation only): 1 skip role C, 2 skip role A, 4 skip role B
   // part: 0 = all roles in one launch, 1 = role C only (critical path), 2 = roles A+B only (side stream)
   __shared__ float red[4][16][17];
@@ -464,6 +500,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
   else if (part == 2) { role = 2; bid = h - nB; }
   else if (h < nB + nC) { role = 1; bid = h - nB; }
   else { role = 2; bid = h - nB - nC; }
+  PROLE(role + 1);
   if (role == 1) {
     if (dbg & 1) return;
     // ---- role C: dP2 tile (mt, nt) over K = 500 (hidden); wave w takes K-chunks w, w+4, ... ----
@@ -501,6 +538,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
       const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j];
       dP2m[(size_t)gm * kFeat + gn] = pm > 0.f ? v : 0.f;
     }
+    PMARK(1);
     return;
   }
   if (role == 2) {
@@ -543,6 +581,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
         else if (gn == kFeat) gb1[gm] = v;
       }
     }
+    PMARK(1);
     return;
   }
   if (dbg & 4) return;
@@ -590,6 +629,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
       correct[0] += (unsigned long long)(th + 0.5f);
     }
   }
+  PMARK(1);
 }
 
 // =================================================================================================
@@ -616,6 +656,7 @@ constexpr int kDysS = 3264;                    // role D carve: dys [50][65] (la
 constexpr int kTS = 128 * 65;                  // T [128 k][65]
 constexpr int kBwdLds = kDysS + kTS + 720 + kImg + kFeat + 200 + 720 + 180;
 
+template <bool PROF>
 __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, const int* __restrict__ rows,
                                                   const float* __restrict__ P1, const uint8_t* __restrict__ A1,
                                                   const float* __restrict__ dP2m, const uint8_t* __restrict__ A2,
@@ -626,7 +667,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
                                                   const int* __restrict__ row_hit, double* __restrict__ loss_sum,
                                                   unsigned long long* __restrict__ correct, int dbg,
                                                   pde::PeerDev pd, float* __restrict__ ar_buf, int64_t ar_n,
-                                                  int ar_nvb, int ar_two) {
+                                                  int ar_nvb, int ar_two, unsigned long long* __restrict__ prof) {
+  PMARK(0);
   // Side blocks (ar_nvb > 0, the W > 1 "fused" schedule): the first ar_nvb blocks after the meters
   // block all-reduce the fc-gradient bucket (complete since fc_bwd) across ranks with the xGMI peer
   // protocol while the other blocks compute the conv gradients -- comm/compute overlap with no
@@ -668,6 +710,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
         loss_sum[0] += (double)tl;
         correct[0] += (unsigned long long)(th + 0.5f);
       }
+      PROLE(3);
+      PMARK(6);
       return;
     }
     bid -= 1;
@@ -682,6 +726,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
   }
   if (bid < nW) {
     if (dbg & 1) return;
+    PROLE(1);
     const int ig = bid >> 4, kp = bid & 15;
     const int ci_base = (32 * kp) / 25;
     // ---- loads for the 8 images: pooled grad (200 float4), codes (50 uint4), P1 slice (108 float4) ----
@@ -709,6 +754,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
     }
     if (t < 160) smem[kWImgs * kWImgStride + t] = t < 80 ? 1.f : 0.f;   // B operand of the k >= 500 columns
     __syncthreads();
+    PMARK(1);
     const int ct = w & 3, kt = 2 * kp + (w >> 2);
     const int co = ct * 16 + (l & 15), coc = min(co, 49);
     const float com = co < 50 ? 1.f : 0.f;
@@ -740,6 +786,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
         }
       }
     }
+    PMARK(2);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int cor = ct * 16 + lg * 4 + r;
@@ -749,10 +796,12 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
         else if (kk == 500) atomicAdd(&gb2c[cor], v);
       }
     }
+    PMARK(6);
     return;
   }
   bid -= nW;
   if (dbg & 2) return;
+  PROLE(2);
   // ---- role D ----
   const int b = bid >> 2, cg = bid & 3;
   if (b >= B) return;
@@ -783,6 +832,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
   if (t < 180) reinterpret_cast<float4*>(p1m)[t] = pv;
   if (t < 45) reinterpret_cast<uint4*>(cds)[t] = cv;
   __syncthreads();
+  PMARK(1);
   // (0) dY2[co][px] from the pooled gradient + codes
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
@@ -794,6 +844,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
     }
   }
   __syncthreads();
+  PMARK(2);
   // (1) dgrad tile (dmt, dpt): 25 x 32x32x2 over co = 50
   {
     const float* bp = dys + (l >> 5) * 65 + dpt * 32 + (l & 31);
@@ -808,6 +859,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
       T[(dmt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 65 + dpt * 32 + (l & 31)] = acc[r];
   }
   __syncthreads();
+  PMARK(3);
   // (2) col2im gather + maxpool1/relu mask: dP1[cl][ih][iw] = sum_{kh,kw} T[cl*25+kh*5+kw][(ih-kh)*8+iw-kw]
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -831,6 +883,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
     }
   }
   __syncthreads();
+  PMARK(4);
   // (3) dense dY1 [5][576] (into the dead dys region) from dP1 + maxpool1 codes
   float* dy1 = dys;
 #pragma unroll
@@ -846,6 +899,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
     }
   }
   __syncthreads();
+  PMARK(5);
   if (dbg & 16) return;
   // (4) conv1 wgrad|bgrad: C[c][tap] = sum_pos dY1[c][pos] * [X(pos+tap) | 1]; wave = (tap-tile, K-quarter)
   float* red = T;                                             // T is dead: [4][16][33] partials
@@ -882,6 +936,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
       else atomicAdd(&gb1c[rep + ch], v);
     }
   }
+  PMARK(6);
 }
 
 }  // namespace
@@ -889,29 +944,53 @@ __global__ __launch_bounds__(512) void k_conv_bwd(const float* __restrict__ X, c
 // =================================================================================================
 // Host launchers (extern "C": no torch headers in device TUs)
 // =================================================================================================
+namespace {
+unsigned long long* g_prof = nullptr;   // host-side switch: non-null -> PROF instantiations
+constexpr size_t kProfKernelStride = 4096 * 8;
+unsigned long long* prof_slot(int kid) { return g_prof ? g_prof + (size_t)kid * kProfKernelStride : nullptr; }
+}  // namespace
+
 extern "C" {
+
+// Phase profiling of the LeNet kernels (tools/lenet_phases.py).  buf: [kernels][4096 blocks][8] u64,
+// kernel slots 0 conv_fwd, 1 fc1_fwd, 2 head, 3 fc_bwd, 4 conv_bwd, 5 adam; nullptr switches it off.
+void pde_lenet_set_prof(unsigned long long* buf) { g_prof = buf; }
+unsigned long long* pde_lenet_prof_slot(int kid) { return prof_slot(kid); }
 
 hipError_t pde_lenet_conv_fwd(const float* X, const int* idx, int n_idx, const long long* step, int nbatches,
                               int stride, const long long* labels_all, int B, const float* w1, const float* b1,
                               const float* Wt2, const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2,
                               int* cur_row, long long* cur_lbl, float* zero_ptr, int zero_n, int dbg, hipStream_t st) {
   BatchSrc src{idx, step, nbatches, stride > 0 ? stride : B, n_idx};
-  hipLaunchKernelGGL(k_conv_fwd, dim3(B, 2), dim3(256), 0, st, X, src, labels_all, w1, b1, Wt2, b2, P1, A1, P2, A2,
-                     cur_row, cur_lbl, zero_ptr, zero_n, dbg);
+  if (g_prof)
+    hipLaunchKernelGGL(k_conv_fwd<true>, dim3(B, 2), dim3(256), 0, st, X, src, labels_all, w1, b1, Wt2, b2, P1, A1, P2,
+                       A2, cur_row, cur_lbl, zero_ptr, zero_n, dbg, prof_slot(0));
+  else
+    hipLaunchKernelGGL(k_conv_fwd<false>, dim3(B, 2), dim3(256), 0, st, X, src, labels_all, w1, b1, Wt2, b2, P1, A1,
+                       P2, A2, cur_row, cur_lbl, zero_ptr, zero_n, dbg, nullptr);
   return hipGetLastError();
 }
 
 hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float* bias, float* H1, long long* ctr,
                              int nctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_fc1_fwd, dim3(32, (B + 15) / 16), dim3(256), 0, st, P2, B, W, bias, H1, ctr, nctr);
+  if (g_prof)
+    hipLaunchKernelGGL(k_fc1_fwd<true>, dim3(32, (B + 15) / 16), dim3(256), 0, st, P2, B, W, bias, H1, ctr, nctr,
+                       prof_slot(1));
+  else
+    hipLaunchKernelGGL(k_fc1_fwd<false>, dim3(32, (B + 15) / 16), dim3(256), 0, st, P2, B, W, bias, H1, ctr, nctr,
+                       nullptr);
   return hipGetLastError();
 }
 
 hipError_t pde_lenet_head(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
                           float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
                           double* loss_sum, unsigned long long* correct, hipStream_t st) {
-  hipLaunchKernelGGL(k_head, dim3((B + 3) / 4), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2, dZ1,
-                     row_loss, row_hit, loss_sum, correct);
+  if (g_prof)
+    hipLaunchKernelGGL(k_head<true>, dim3((B + 3) / 4), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2,
+                       dZ1, row_loss, row_hit, loss_sum, correct, prof_slot(2));
+  else
+    hipLaunchKernelGGL(k_head<false>, dim3((B + 3) / 4), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out,
+                       dZ2, dZ1, row_loss, row_hit, loss_sum, correct, nullptr);
   return hipGetLastError();
 }
 
@@ -927,8 +1006,12 @@ hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, 
                             hipStream_t st) {
   const int nC = ((B + 15) / 16) * 50, nAB = 32 * 51 + 32;
   const int nblk = part == 1 ? nC : (part == 2 ? nAB : nC + nAB);
-  hipLaunchKernelGGL(k_fc_bwd, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2,
-                     row_loss, row_hit, loss_sum, correct, dbg, part);
+  if (g_prof)
+    hipLaunchKernelGGL(k_fc_bwd<true>, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2, gb2,
+                       row_loss, row_hit, loss_sum, correct, dbg, part, prof_slot(3));
+  else
+    hipLaunchKernelGGL(k_fc_bwd<false>, dim3(nblk), dim3(256), 0, st, P2, H1, dZ1, dZ2, W1, B, dP2m, gW1, gb1, gW2,
+                       gb2, row_loss, row_hit, loss_sum, correct, dbg, part, nullptr);
   return hipGetLastError();
 }
 
@@ -947,10 +1030,16 @@ hipError_t pde_lenet_conv_bwd(const float* X, const int* rows, const float* P1, 
     ar_nvb = (int)std::min<int64_t>(64, std::max<int64_t>(1, (work + 511) / 512));
   }
   const int nblk = ((B + kWImgs - 1) / kWImgs) * 16 + 4 * B + meters + ar_nvb;
-  hipLaunchKernelGGL(k_conv_bwd, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
-                     gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, meters ? row_loss : nullptr,
-                     meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg, pd,
-                     ar_buf, ar_n, ar_nvb, ar_two);
+  if (g_prof)
+    hipLaunchKernelGGL(k_conv_bwd<true>, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
+                       gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, meters ? row_loss : nullptr,
+                       meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg, pd,
+                       ar_buf, ar_n, ar_nvb, ar_two, prof_slot(4));
+  else
+    hipLaunchKernelGGL(k_conv_bwd<false>, dim3(nblk), dim3(512), 0, st, X, rows, P1, A1, dP2m, A2, W2c, B, gW1c,
+                       gb1c, gW2c, gb2c, c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, meters ? row_loss : nullptr,
+                       meters ? row_hit : nullptr, meters ? loss_sum : nullptr, meters ? correct : nullptr, dbg, pd,
+                       ar_buf, ar_n, ar_nvb, ar_two, nullptr);
   return hipGetLastError();
 }
 

@@ -1,0 +1,624 @@
+// LeNet training step, second generation (the reference "toy CNN", /root/reference/mnist/main.py:130-147).
+//
+// Differences from lenet.hip's F1 (measured in-step with tools/lenet_phases.py, profiles/lenet_phases_*.md):
+//  * the batch is PREFETCHED: the previous step gathered its sampler rows into Xb (double-buffered by
+//    step parity, chosen on the host at launch/capture time), so the kernel starts with ONE dependent
+//    global load instead of counter -> index -> image (0.9 us of chain + 3.4 us to the first barrier);
+//  * the conv2 weight slice (72 KB per co-half) is staged by LDS-DMA (global_load_lds_dwordx4, 9 per
+//    wave, issued after the image loads) while conv1 computes: no 64-VGPR register staging that the
+//    compiler sank past conv1 (2.5 us of exposed weight latency), and no LDS write pass;
+//  * 8 waves per block: conv1 tiles (v_mfma_f32_32x32x2_f32, pooling on the accumulator rows) spread
+//    over 8 waves, conv2 as one 16x16 output tile per wave on v_mfma_f32_16x16x4_f32 over the full
+//    K = 500 (no K-split partial sums, no LDS reduction); the A operand comes from LDS by ds_read_b128
+//    (4 k-steps per read), the B operand (conv1 output im2col) by conflict-free ds_read_b32: 4x4-pixel
+//    output tiles with a channel stride of 144 floats (== 16 mod 32 banks) put the two K-lane groups
+//    of each 32-lane half on disjoint bank sets;
+//  * bias + ReLU + 2x2 max-pool (first maximum in scan order, as ATen) on the accumulator registers with
+//    lane shuffles (pixel neighbours are lanes ^1 / ^4 / ^5 of a 4x4 tile);
+//  * P1 / A1 (conv1 pooled output + argmax codes, kept for backward) are written at the END from LDS,
+//    split between the two co-half blocks, so no store sits in the VMEM queue ahead of the LDS-DMA wait.
+//
+// Packed conv2 weight ("Wp"), written by the optimizer's repack epilogue (optim.hip, pack mode 2):
+//   Wp[ct][cotile][kq][co16][132]  (ct = co >> 5, cotile = (co >> 4) & 1, co16 = co & 15)
+//   holding W2[co][ci][kh][kw] at k-step s = k' >> 2, kq = k' & 3, k' = (kh*5 + kw)*20 + ci;
+//   rows are 132 floats (125 k-steps + zero pad; 528 B, a multiple of 16 B: co rows 4 banks apart ->
+//   the b128 A reads are conflict-free); each co-half region is padded to 72 KB = 72 LDS-DMA
+//   wave-instructions (9 per wave, a compile-time count, so the compiler's vmcnt bookkeeping stays exact).
+#include "pde_hip.h"
+#include "pde_kernels.h"
+#include "pde_lenet.h"
+
+namespace {
+
+constexpr int kImg = 784, kP1 = 2880, kFeat = 800;
+constexpr int kRowS = 132;
+constexpr int kWpHalf = 72 * 256;            // floats per co-half region (72 KB)
+constexpr int kL_W = 0;
+constexpr int kL_XS = kWpHalf;               // [20][144] pooled conv1 output
+constexpr int kL_CODE = kL_XS + kP1;         // [20][144] uint8 argmax codes (720 floats)
+constexpr int kL_IMG = kL_CODE + 720;        // [784]
+constexpr int kL_W1 = kL_IMG + kImg;         // conv1 weight [500] + bias [20] (+pad)
+constexpr int kL_TOT = kL_W1 + 528;          // 23344 floats = 91 KB
+
+#define PMARK(ph)                                                                             \
+  do {                                                                                        \
+    if constexpr (PROF) {                                                                     \
+      if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                         \
+  } while (0)
+
+template <bool PROF>
+__global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb, const float* __restrict__ w1,
+                                                   const float* __restrict__ b1, const float* __restrict__ Wp,
+                                                   const float* __restrict__ b2, float* __restrict__ P1,
+                                                   uint8_t* __restrict__ A1, float* __restrict__ P2,
+                                                   uint8_t* __restrict__ A2, float* __restrict__ zero_ptr, int zero_n,
+                                                   unsigned long long* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) float smem[kL_TOT];
+  const int b = blockIdx.x, ct = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
+  PMARK(0);
+  // ---- phase 0: register loads first (image, conv1 weights, this wave's conv2 biases) ----
+  const float4 xv = reinterpret_cast<const float4*>(Xb + (size_t)b * kImg)[min(t, kImg / 4 - 1)];
+  const float4 wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
+  const float bv1 = b1[min(t, 19)];
+  const int cotile = w >> 2, pxt = w & 3, kq = l >> 4, j = l & 15;
+  const int co_base = ct * 32 + cotile * 16 + kq * 4;          // + r: the accumulator row's channel
+  float bias2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias2[r] = b2[min(co_base + r, 49)];
+  if (t < kImg / 4) reinterpret_cast<float4*>(smem + kL_IMG)[t] = xv;
+  if (t < 125) reinterpret_cast<float4*>(smem + kL_W1)[t] = wv;
+  if (t < 20) smem[kL_W1 + 500 + t] = bv1;
+  // ---- then the conv2 weight image by LDS-DMA: 72 x 1 KB, exactly 9 per wave ----
+  {
+    const float* wsrc = Wp + (size_t)ct * kWpHalf;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int c = w + 8 * i;
+      __builtin_amdgcn_global_load_lds(wsrc + c * 256 + l * 4, smem + kL_W + c * 256, 16, 0, 0);
+    }
+  }
+  // barrier without draining the LDS-DMA (a __syncthreads() would wait vmcnt(0))
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  PMARK(1);
+  // ---- phase 1: conv1 (1->20, 5x5) + bias + ReLU + 2x2 max-pool on v_mfma_f32_32x32x2_f32 ----
+  // C[m][ch] = sum_tap im2col[m][tap] * W1[ch][tap], m = 4 * pooled_pos + (dy*2+dx): accumulator rows
+  // 4g..4g+3 are the 4 sub-positions of one pooled position -> pooled in registers.
+  {
+    const float* xin = smem + kL_IMG;
+    const float* w1s = smem + kL_W1;
+    float* xs = smem + kL_XS;
+    uint8_t* codes = reinterpret_cast<uint8_t*>(smem + kL_CODE);
+    const int ch = l & 31, hi = l >> 5;
+    const float chm = ch < 20 ? 1.f : 0.f;
+    float wb[13];
+#pragma unroll
+    for (int s2 = 0; s2 < 13; ++s2) {
+      const int tap = 2 * s2 + hi;
+      wb[s2] = (tap < 25) ? w1s[min(ch, 19) * 25 + min(tap, 24)] * chm : 0.f;
+    }
+    const float bch = w1s[500 + min(ch, 19)];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int tile = w + 8 * it;
+      if (tile < 18) {
+        const int m = tile * 32 + ch, pp = m >> 2, sub = m & 3;
+        const float* xa = xin + (2 * (pp / 12) + (sub >> 1)) * 28 + 2 * (pp % 12) + (sub & 1);
+        float av[13];
+#pragma unroll
+        for (int s2 = 0; s2 < 13; ++s2) {
+          const int t0 = 2 * s2, t1 = min(2 * s2 + 1, 24);
+          av[s2] = hi ? xa[(t1 / 5) * 28 + t1 % 5] : xa[(t0 / 5) * 28 + t0 % 5];
+        }
+        f32x16 acc = {0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 13; ++s2) acc = mfma32x32x2(av[s2], wb[s2], acc);
+        if (ch < 20) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int pq = tile * 8 + 2 * g + hi;          // pooled position of registers 4g..4g+3
+            float best = fmaxf(acc[4 * g] + bch, 0.f);
+            int code = 0;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const float v = fmaxf(acc[4 * g + q] + bch, 0.f);
+              if (v > best) { best = v; code = q; }
+            }
+            xs[ch * 144 + pq] = best;
+            codes[ch * 144 + pq] = (uint8_t)code;
+          }
+        }
+      }
+    }
+  }
+  PMARK(2);
+  // conv1 output visible + this wave's LDS-DMA landed, then every wave's (barrier)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  PMARK(3);
+  // ---- phase 2: conv2 (20->50, 5x5): wave = (co tile of 16, 4x4 pixel tile), K = 500 ----
+  const int oh = (pxt >> 1) * 4 + (j >> 2), ow = (pxt & 1) * 4 + (j & 3);
+  f32x4 acc = {0.f};
+  {
+    const float* wa = smem + kL_W + ((cotile * 4 + kq) * 16 + j) * kRowS;   // A: W[co = j][k-steps], b128 reads
+    const float* xb = smem + kL_XS + kq * 144 + oh * 12 + ow;             // B: im2col[k][px]
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const float4 a4 = *reinterpret_cast<const float4*>(wa + 4 * u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int s = 4 * u + e;
+        if (s < 125) {
+          const int tap = s / 5, kh = tap / 5, kw = tap % 5, cib = 4 * (s % 5);
+          const float bv = xb[cib * 144 + kh * 12 + kw];
+          acc = mfma16x16x4(e == 0 ? a4.x : e == 1 ? a4.y : e == 2 ? a4.z : a4.w, bv, acc);
+        }
+      }
+    }
+  }
+  PMARK(4);
+  // ---- epilogue: bias + ReLU + 2x2 max-pool across lanes (^1 = dx, ^4 = dy), P2 / A2 ----
+  {
+    const bool anchor = (j & 5) == 0;                  // top-left pixel of a pooling window
+    const int ph = oh >> 1, pw = ow >> 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(acc[r] + bias2[r], 0.f);
+      const float v1 = __shfl_xor(v, 1, 64), v4 = __shfl_xor(v, 4, 64), v5 = __shfl_xor(v, 5, 64);
+      float best = v;
+      int code = 0;
+      if (v1 > best) { best = v1; code = 1; }
+      if (v4 > best) { best = v4; code = 2; }
+      if (v5 > best) { best = v5; code = 3; }
+      const int co = co_base + r;
+      if (anchor && co < 50) {
+        const size_t o = (size_t)b * kFeat + co * 16 + ph * 4 + pw;
+        P2[o] = best;
+        A2[o] = (uint8_t)code;
+      }
+    }
+  }
+  // ---- P1 / A1 for backward: this block's 10 channels, from LDS ----
+  if (t < 360) {
+    const int c0 = ct * 10 * 144;
+    reinterpret_cast<float4*>(P1 + (size_t)b * kP1 + c0)[t] = reinterpret_cast<const float4*>(smem + kL_XS + c0)[t];
+    reinterpret_cast<uint32_t*>(A1 + (size_t)b * kP1 + c0)[t] =
+        reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem + kL_CODE) + c0)[t];
+  }
+  if (zero_ptr) {
+    const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
+    for (int i = bid * 512 + t; i < zero_n; i += nb * 512) zero_ptr[i] = 0.f;
+  }
+  PMARK(5);
+}
+
+// Batch prefetch: rows of sampler batch (*ctr % nbatches) (or batch 0 without a counter) gathered
+// into Xdst [B][784] / Ydst [B] / rows_dst [B]; indices past the end of idx are clamped (the ragged
+// tail batch).  One wave per row, 4 rows per 256-thread block.
+__device__ __forceinline__ void gather_rows(const float* __restrict__ X, const long long* __restrict__ labels,
+                                            const int* __restrict__ idx, int n_idx, const long long* __restrict__ ctr,
+                                            int nbatches, int B, float* __restrict__ Xdst, long long* __restrict__ Ydst,
+                                            int* __restrict__ rows_dst, int gblock) {
+  const int l = threadIdx.x & 63, r = gblock * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const long long batch = ctr ? (*ctr % nbatches) : 0;
+  const int src = idx ? idx[min(batch * B + r, (long long)n_idx - 1)] : r;
+  const float4* s4 = reinterpret_cast<const float4*>(X + (size_t)src * kImg);
+  float4* d4 = reinterpret_cast<float4*>(Xdst + (size_t)r * kImg);
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = s4[min(l + 64 * i, kImg / 4 - 1)];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (l + 64 * i < kImg / 4) d4[l + 64 * i] = v[i];
+  if (l == 0) {
+    if (Ydst) Ydst[r] = labels[src];
+    if (rows_dst) rows_dst[r] = src;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const float* __restrict__ X, const long long* __restrict__ labels,
+                                                const int* __restrict__ idx, int n_idx,
+                                                const long long* __restrict__ ctr, int nbatches, int B,
+                                                float* __restrict__ Xdst, long long* __restrict__ Ydst,
+                                                int* __restrict__ rows_dst) {
+  gather_rows(X, labels, idx, n_idx, ctr, nbatches, B, Xdst, Ydst, rows_dst, blockIdx.x);
+}
+
+// =================================================================================================
+// Conv backward v2.  Two block roles of 512 threads, INTERLEAVED in dispatch order (W, D, W, D, ...)
+// and sized so that at B = 128 all 512 blocks are co-resident (< 64 KB LDS -> 2 per CU on 256 CUs):
+// the first generation's D blocks (60 KB, 769 blocks) waited ~7 us for W blocks to leave.
+//   role W  (ig, kp): conv2 wgrad|bgrad over an image group (G = ceil(B/16) images, 16 groups) for a
+//           32-column k slice, v_mfma_f32_16x16x4_f32, A = pooled gradient scattered by the argmax
+//           codes on the fly, B = im2col of P1 (ones column k = 500 -> bias gradient).  slab_stride > 0:
+//           group ig writes its partial into gradient replica ig (plain stores, deterministic; the
+//           optimizer folds the 16 replicas); slab_stride == 0: float atomics into the gradient.
+//           Side jobs: block w prefetches half (w & 1) of row (w >> 1) of the NEXT batch into the other
+//           parity's buffers (counter -> index -> image; the waits land after the MFMA loop), block 0
+//           folds the head's per-row loss / hit into the device meters.
+//   role D  (image b, half h of 10 input channels): conv2 dgrad in two passes of 5 channels
+//           (T[125 k][64 px] on v_mfma_f32_32x32x2_f32, A = W2 from registers), col2im as an LDS
+//           gather + ReLU mask of P1, conv1 wgrad|bgrad on v_mfma_f32_16x16x4_f32 with the unpooled
+//           gradient produced on the fly from dP1 and the maxpool-1 codes, one atomic per output into
+//           replica (b % c1_nrep).  Synchronises through LDS only (raw s_barrier + lgkmcnt(0)).
+// LDS layouts are padded so every hot access is bank-conflict free (SQ_LDS_BANK_CONFLICT was 3.7 M
+// cycles per step before: 16-way dY2 scatter writes, 4-way gradient / code reads in W, 8-way dP1):
+//   W: pooled gradient rows of 20 floats per channel (float2 reads: lanes co*20 and co*20+2 on
+//      disjoint bank pairs), argmax code rows of 20 bytes (5 dwords), P1 slice [3][144];
+//   D: dY2 [50][64] written in gather order from global loads, dP1 rows of 145 floats and A1 code rows
+//      of 148 bytes (co-prime-ish strides across the 16 channel lanes), conv1-wgrad partials rows of 36.
+// =================================================================================================
+constexpr int kWImgs = 8;
+constexpr int kWG = 0, kWC = 1000, kWP = 1250;     // per image: grad [50][20] | codes [50][20 B] | P1 [3][144]
+constexpr int kWImgStride = kWP + 432;             // 1682 floats
+constexpr int kD_DY2 = 0;                          // [50][64] dY2 (later conv1-wgrad partials [4][16][36])
+constexpr int kD_T = 3200;                         // [128][64] dgrad T of one pass
+constexpr int kD_P1 = kD_T + 8192;                 // [10][144] P1 of the half
+constexpr int kD_C1 = kD_P1 + 1440;                // [10][148 B] A1 codes (370 floats)
+constexpr int kD_X = kD_C1 + 370;                  // [784] image
+constexpr int kD_DP1 = kD_X + kImg;                // [10][145] dP1 (ReLU-masked)
+constexpr int kD_TOT = kD_DP1 + 1450;              // 15436 floats
+constexpr int kW_TOT = kWImgs * kWImgStride + 160; // 13616 floats
+constexpr int kBwd2Lds = (kD_TOT > kW_TOT ? kD_TOT : kW_TOT) + 16;   // + meter scratch
+
+struct Bwd2Gather {      // next-batch prefetch (nullptr X: off)
+  const float* X;
+  const long long* labels;
+  const int* idx;
+  int n_idx;
+  const long long* ctr;  // batch counter, already advanced to the next batch by fc1
+  int nbatches;
+  int stride;            // batch size of the sampler's batches
+  float* Xdst;
+  long long* Ydst;
+  int* rows_dst;
+};
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb, const float* __restrict__ P1,
+                                                   const uint8_t* __restrict__ A1, const float* __restrict__ dP2m,
+                                                   const uint8_t* __restrict__ A2, const float* __restrict__ W2c,
+                                                   int B, float* __restrict__ gW1c, float* __restrict__ gb1c,
+                                                   int c1_nrep, int c1_rep_stride, float* __restrict__ gW2c,
+                                                   float* __restrict__ gb2c, int slab_stride,
+                                                   const float* __restrict__ row_loss, const int* __restrict__ row_hit,
+                                                   double* __restrict__ loss_sum,
+                                                   unsigned long long* __restrict__ correct, Bwd2Gather ga,
+                                                   int dbg, unsigned long long* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) float smem[kBwd2Lds];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lg = l >> 4;
+  PMARK(0);
+  const int nIG = slab_stride > 0 ? 16 : (B + kWImgs - 1) / kWImgs;
+  const int G = slab_stride > 0 ? (B + 15) / 16 : kWImgs;        // images per W group (<= 8)
+  const int nW = nIG * 16, nD = 2 * B, npair = min(nW, nD);
+  const int h = blockIdx.x;
+  int role, idx;
+  if (h < 2 * npair) {
+    role = h & 1;
+    idx = h >> 1;
+  } else {
+    role = nW > nD ? 0 : 1;
+    idx = npair + (h - 2 * npair);
+  }
+  if constexpr (PROF) {
+    if (t == 0) prof[(size_t)blockIdx.x * 8 + 7] = role + 1;
+  }
+  const float4* P1v = reinterpret_cast<const float4*>(P1);
+  if ((dbg >> role) & 1) return;     // ablation only (tools/lenet_phases.py --bwd-dbg): 1 = no W, 2 = no D
+  if (role == 0) {
+    // =============================== role W: conv2 wgrad ===============================
+    const int ig = idx >> 4, kp = idx & 15, img0 = ig * G;
+    const int ci_base = (32 * kp) / 25;
+    const float4* Gv = reinterpret_cast<const float4*>(dP2m);
+    const uint4* Av = reinterpret_cast<const uint4*>(A2);
+    float4 v4[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int e = t + 512 * j;                  // piece id in [0, 8*358)
+      const int ii = min(e / 358, kWImgs - 1), pc = e - (e / 358) * 358;
+      const int b = min(img0 + min(ii, G - 1), B - 1);
+      const int q = max(pc - 250, 0), ch = min(ci_base + q / 36, 19);
+      const float4* src = pc < 200 ? Gv + (size_t)b * 200 + pc
+                        : pc < 250 ? reinterpret_cast<const float4*>(Av + (size_t)b * 50 + (pc - 200))
+                                   : P1v + (size_t)b * 720 + ch * 36 + (q % 36);
+      v4[j] = *src;
+    }
+    // side jobs: meters (block 0) and the next-batch prefetch chain (its waits come after the MFMAs)
+    const bool meter = (idx == 0) && row_loss && loss_sum;
+    float mloss = 0.f, mhit = 0.f;
+    if (meter && t < B) {
+      mloss = row_loss[t];
+      mhit = (float)row_hit[t];
+    }
+    const int grow = idx >> 1, ghalf = idx & 1;
+    const bool gjob = ga.X != nullptr && grow < B;
+    long long gnb = 0;
+    if (gjob) gnb = *ga.ctr;                                                           // link 1
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int e = t + 512 * j;
+      if (e < kWImgs * 358) {
+        const int ii = e / 358, pc = e - ii * 358;
+        float* img = smem + ii * kWImgStride;
+        if (pc < 200) {                             // pooled gradient: co = pc / 4, 4 floats
+          *reinterpret_cast<float4*>(img + kWG + (pc >> 2) * 20 + 4 * (pc & 3)) = v4[j];
+        } else if (pc < 250) {                      // 16 codes of one channel -> 20-byte row
+          uint32_t* cd = reinterpret_cast<uint32_t*>(img + kWC) + (pc - 200) * 5;
+          cd[0] = __float_as_uint(v4[j].x);
+          cd[1] = __float_as_uint(v4[j].y);
+          cd[2] = __float_as_uint(v4[j].z);
+          cd[3] = __float_as_uint(v4[j].w);
+        } else {
+          reinterpret_cast<float4*>(img + kWP)[pc - 250] = v4[j];
+        }
+      }
+    }
+    if (t < 160) smem[kWImgs * kWImgStride + t] = t < 80 ? 1.f : 0.f;   // B operand of the k >= 500 columns
+    if (meter) {
+      const float ls = wave_sum(mloss), hs = wave_sum(mhit);
+      if (l == 0) {
+        smem[kBwd2Lds - 16 + w] = ls;
+        smem[kBwd2Lds - 8 + w] = hs;
+      }
+    }
+    int gsrc = 0;
+    if (gjob) gsrc = ga.idx[min((gnb % ga.nbatches) * ga.stride + grow, (long long)ga.n_idx - 1)];   // link 2
+    lds_barrier();
+    PMARK(1);
+    if (meter && t == 0) {
+      float tl = 0.f, th = 0.f;
+      for (int k = 0; k < 8; ++k) {
+        tl += smem[kBwd2Lds - 16 + k];
+        th += smem[kBwd2Lds - 8 + k];
+      }
+      loss_sum[0] += (double)tl;
+      correct[0] += (unsigned long long)(th + 0.5f);
+    }
+    const int ct = w & 3, kt = 2 * kp + (w >> 2);
+    const int co = ct * 16 + (l & 15), coc = min(co, 49);
+    const float com = co < 50 ? 1.f : 0.f;
+    const int kk = kt * 16 + (l & 15);
+    const int kc = min(kk, 499), ci = kc / 25, rem = kc - ci * 25, kh = rem / 5, kw = rem - kh * 5;
+    const int boff = (ci - ci_base) * 144 + (kh + (lg >> 1)) * 12 + kw + 4 * (lg & 1);
+    const float* cst = smem + kWImgs * kWImgStride + (kk == 500 ? 0 : 80);   // ones | zeros
+    f32x4 acc0 = {0.f}, acc1 = {0.f};
+#pragma unroll 2
+    for (int ii = 0; ii < kWImgs; ++ii) {
+      const float* gi = smem + ii * kWImgStride;
+      const uint8_t* ci8 = reinterpret_cast<const uint8_t*>(gi + kWC) + coc * 20 + 2 * (lg & 1);
+      const float* gq = gi + kWG + coc * 20 + 2 * (lg & 1);
+      const float* p1s = kk < 500 ? gi + kWP + boff : cst;
+      const float bm = (ii < G && img0 + ii < B) ? com : 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float2 gg = *reinterpret_cast<const float2*>(gq + 4 * c);
+        const unsigned short cc = *reinterpret_cast<const unsigned short*>(ci8 + 4 * c);
+        const int c0 = cc & 0xff, c1 = cc >> 8, sb = (lg >> 1) * 2;
+        const float g0 = gg.x * bm, g1 = gg.y * bm;
+        acc0 = mfma16x16x4(c0 == sb ? g0 : 0.f, p1s[24 * c + 0], acc0);
+        acc1 = mfma16x16x4(c0 == sb + 1 ? g0 : 0.f, p1s[24 * c + 1], acc1);
+        acc0 = mfma16x16x4(c1 == sb ? g1 : 0.f, p1s[24 * c + 2], acc0);
+        acc1 = mfma16x16x4(c1 == sb + 1 ? g1 : 0.f, p1s[24 * c + 3], acc1);
+      }
+    }
+    PMARK(2);
+    float4 gx = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gjob && t < 98) gx = reinterpret_cast<const float4*>(ga.X + (size_t)gsrc * kImg)[98 * ghalf + t];   // link 3
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int cor = ct * 16 + lg * 4 + r;
+      const float v = acc0[r] + acc1[r];
+      if (cor < 50) {
+        if (slab_stride > 0) {
+          const size_t rep = (size_t)ig * slab_stride;
+          if (kk < 500) gW2c[rep + cor * 500 + kk] = v;
+          else if (kk == 500) gb2c[rep + cor] = v;
+        } else {
+          if (kk < 500) atomicAdd(&gW2c[cor * 500 + kk], v);
+          else if (kk == 500) atomicAdd(&gb2c[cor], v);
+        }
+      }
+    }
+    if (gjob) {
+      if (t < 98) reinterpret_cast<float4*>(ga.Xdst + (size_t)grow * kImg)[98 * ghalf + t] = gx;
+      if (ghalf == 0 && t == 0) {
+        ga.Ydst[grow] = ga.labels[gsrc];
+        ga.rows_dst[grow] = gsrc;
+      }
+    }
+    PMARK(6);
+    return;
+  }
+  // =============================== role D ===============================
+  const int b = idx >> 1, hh = idx & 1;
+  float* dys = smem + kD_DY2;
+  float* T = smem + kD_T;
+  float* p1s = smem + kD_P1;
+  uint8_t* c1s = reinterpret_cast<uint8_t*>(smem + kD_C1);
+  float* xs = smem + kD_X;
+  float* dp1 = smem + kD_DP1;
+  // ---- loads: dgrad A operand (both passes), dY2 in gather order, image, P1 / A1 of the half ----
+  const int kt = w >> 1, pt = w & 1;
+  const int kl = kt * 32 + (l & 31);
+  const float km = kl < 125 ? 1.f : 0.f;
+  float av[2][25];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float* wa = W2c + (l >> 5) * 500 + (10 * hh + 5 * p) * 25 + min(kl, 124);
+#pragma unroll
+    for (int s2 = 0; s2 < 25; ++s2) av[p][s2] = wa[2 * s2 * 500];
+  }
+  // dY2[co][oh][ow] = g[co][pq] if code[co][pq] == sub else 0: thread i reads the pooled value and its
+  // code straight from global memory and writes dY2 in address order (conflict-free)
+  float gy[7];
+  uint8_t gcode[7];
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const int i = min(t + 512 * r, 3199), co = i >> 6, px = i & 63, oh = px >> 3, ow = px & 7;
+    const int q = co * 16 + (oh >> 1) * 4 + (ow >> 1);
+    gy[r] = dP2m[(size_t)b * kFeat + q];
+    gcode[r] = A2[(size_t)b * kFeat + q];
+  }
+  const float4 xv = reinterpret_cast<const float4*>(Xb + (size_t)b * kImg)[min(t, kImg / 4 - 1)];
+  const float4 pv = P1v[(size_t)b * 720 + hh * 360 + min(t, 359)];
+  const uint32_t cv = reinterpret_cast<const uint32_t*>(A1 + (size_t)b * kP1 + hh * 1440)[min(t, 359)];
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const int i = t + 512 * r;
+    if (i < 3200) {
+      const int px = i & 63, sub = ((px >> 3) & 1) * 2 + (px & 1);
+      dys[i] = gcode[r] == sub ? gy[r] : 0.f;
+    }
+  }
+  if (t < kImg / 4) reinterpret_cast<float4*>(xs)[t] = xv;
+  if (t < 360) {
+    reinterpret_cast<float4*>(p1s)[t] = pv;
+    reinterpret_cast<uint32_t*>(c1s)[(t / 36) * 37 + (t % 36)] = cv;    // 148-byte code rows
+  }
+  lds_barrier();
+  PMARK(1);
+  // ---- two passes of 5 input channels: dgrad -> T, col2im gather -> dP1 (ReLU mask of P1) ----
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    {
+      const float* bp = dys + (l >> 5) * 64 + pt * 32 + (l & 31);
+      f32x16 acc = {0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 25; ++s2) acc = mfma32x32x2(av[p][s2] * km, bp[2 * s2 * 64], acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        T[(kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 64 + pt * 32 + (l & 31)] = acc[r];
+    }
+    lds_barrier();
+    if (p == 0) PMARK(2);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int o = t + 512 * r;
+      if (o < 720) {
+        const int cl = o / 144, pos = o - cl * 144, ih = pos / 12, iw = pos - ih * 12;
+        float sacc = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh) {
+          const int oh = ih - kh;
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const int ow = iw - kw;
+            const bool ok = oh >= 0 && oh < 8 && ow >= 0 && ow < 8;
+            const float tv = T[ok ? (cl * 25 + kh * 5 + kw) * 64 + oh * 8 + ow : 0];
+            sacc += ok ? tv : 0.f;
+          }
+        }
+        const int c = 5 * p + cl;
+        dp1[c * 145 + pos] = p1s[c * 144 + pos] > 0.f ? sacc : 0.f;
+      }
+    }
+    lds_barrier();
+    if (p == 0) PMARK(3);
+  }
+  PMARK(4);
+  // ---- conv1 wgrad|bgrad: C[c][tap] = sum_pos dY1[c][pos] * [X(pos + tap) | 1], dY1 unpooled on the fly:
+  // pos = 144kq + 4s + lg -> pooled index pq = 36kq + ((4s/24)>>1)*12 + (4s%24)/2 + (lg>>1),
+  // window slot sub = ((4s/24)&1)*2 + (lg&1); wave = (tap tile nt, K quarter kq) ----
+  float* red = dys;                                           // dY2 is dead: [4][16][36] partials
+  {
+    const int nt = w & 1, kq = w >> 1;
+    const int c = l & 15, cc = min(c, 9);
+    const float cmask = c < 10 ? 1.f : 0.f;
+    const int tap = nt * 16 + (l & 15);
+    const float tmask = tap < 25 ? 1.f : 0.f, tone = tap == 25 ? 1.f : 0.f;
+    const int tc = min(tap, 24), th = tc / 5, tw = tc - th * 5;
+    const float* dpp = dp1 + cc * 145 + 36 * kq + (lg >> 1);
+    const uint8_t* cdp = c1s + cc * 148 + 36 * kq + (lg >> 1);
+    const int lsub = lg & 1;
+    const float* xp = xs + (6 * kq + th) * 28 + tw + lg;
+    f32x4 acc0 = {0.f}, acc1 = {0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 36; ++s2) {
+      const int rr = (4 * s2) / 24, cq = (4 * s2) % 24;       // pos = 144kq + 4s + lg
+      const int qo = (rr >> 1) * 12 + cq / 2, sub = (rr & 1) * 2 + lsub;
+      const float a = (cdp[qo] == sub ? dpp[qo] : 0.f) * cmask;
+      const float bv = xp[rr * 28 + cq] * tmask + tone;
+      if (s2 & 1) acc1 = mfma16x16x4(a, bv, acc1);
+      else acc0 = mfma16x16x4(a, bv, acc0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(kq * 16 + lg * 4 + r) * 36 + nt * 16 + (l & 15)] = acc0[r] + acc1[r];
+  }
+  lds_barrier();
+  PMARK(5);
+  if (t < 260) {
+    const int c = t / 26, tap = t - c * 26;
+    const float v = red[c * 36 + tap] + red[(16 + c) * 36 + tap] + red[(32 + c) * 36 + tap] + red[(48 + c) * 36 + tap];
+    const int ch = 10 * hh + c;
+    const size_t rep = (size_t)(b % c1_nrep) * c1_rep_stride;
+    if (tap < 25) atomicAdd(&gW1c[rep + ch * 25 + tap], v);
+    else atomicAdd(&gb1c[rep + ch], v);
+  }
+  PMARK(6);
+}
+
+__global__ void k_pack_w2_v2(const float* __restrict__ w2, float* __restrict__ dst) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < 25000) dst[pde_lenet_wp_index(e)] = w2[e];
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t pde_lenet_conv_fwd2(const float* Xb, int B, const float* w1, const float* b1, const float* Wp,
+                               const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2, float* zero_ptr,
+                               int zero_n, hipStream_t st) {
+  unsigned long long* prof = pde_lenet_prof_slot(0);
+  if (prof)
+    hipLaunchKernelGGL(k_conv_fwd2<true>, dim3(B, 2), dim3(512), 0, st, Xb, w1, b1, Wp, b2, P1, A1, P2, A2, zero_ptr,
+                       zero_n, prof);
+  else
+    hipLaunchKernelGGL(k_conv_fwd2<false>, dim3(B, 2), dim3(512), 0, st, Xb, w1, b1, Wp, b2, P1, A1, P2, A2, zero_ptr,
+                       zero_n, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_gather(const float* X, const long long* labels, const int* idx, int n_idx, const long long* ctr,
+                            int nbatches, int B, float* Xdst, long long* Ydst, int* rows_dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_gather, dim3((B + 3) / 4), dim3(256), 0, st, X, labels, idx, n_idx, ctr, nbatches, B, Xdst,
+                     Ydst, rows_dst);
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,
+                               const uint8_t* A2, const float* W2c, int B, float* gW1c, float* gb1c, int c1_nrep,
+                               int c1_rep_stride, float* gW2c, float* gb2c, int slab_stride, const float* row_loss,
+                               const int* row_hit, double* loss_sum, unsigned long long* correct, const float* gX,
+                               const long long* glabels, const int* gidx, int gn_idx, const long long* gctr,
+                               int gnbatches, int gstride, float* gXdst, long long* gYdst, int* grows, int dbg,
+                               hipStream_t st) {
+  if (slab_stride > 0 && B > 128) return hipErrorInvalidValue;      // 16 groups of <= 8 images
+  const int nIG = slab_stride > 0 ? 16 : (B + kWImgs - 1) / kWImgs;
+  const int nblk = nIG * 16 + 2 * B;
+  Bwd2Gather ga{gX, glabels, gidx, gn_idx, gctr, gnbatches, gstride, gXdst, gYdst, grows};
+  unsigned long long* prof = pde_lenet_prof_slot(4);
+  if (prof)
+    hipLaunchKernelGGL(k_conv_bwd2<true>, dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
+                       c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, gW2c, gb2c, slab_stride, row_loss, row_hit, loss_sum,
+                       correct, ga, dbg, prof);
+  else
+    hipLaunchKernelGGL(k_conv_bwd2<false>, dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
+                       c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, gW2c, gb2c, slab_stride, row_loss, row_hit, loss_sum,
+                       correct, ga, dbg, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_pack_w2_v2(const float* w2, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_w2_v2, dim3((25000 + 255) / 256), dim3(256), 0, st, w2, dst);
+  return hipGetLastError();
+}
+
+}  // extern "C"

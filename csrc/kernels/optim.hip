@@ -18,6 +18,7 @@
 // conv2 forward kernel streams (k' = (kh*5+kw)*20+ci), so no separate repack launch exists.
 #include "pde_hip.h"
 #include "pde_kernels.h"
+#include "pde_lenet.h"
 #include "pde_peer_dev.h"
 
 #include <algorithm>
@@ -27,21 +28,25 @@ namespace {
 
 struct Pack {
   long long off;   // flat offset of conv2.weight, -1 = no repack
-  float* dst;      // [500][64]
+  float* dst;      // mode 1: [500][64] (lenet.hip F1); mode 2: the LDS-DMA image of lenet_v2.hip
+  int mode;
 };
 
-struct Fold {
+struct Fold1 {
   long long off;   // first element of the canonical gradient (replica 0); -1 = none
   int len;         // elements per replica unit (multiple of 4)
   int nrep;        // replicas (1 = nothing to fold)
   int stride;      // floats between replicas (multiple of 4)
+};
+struct Fold {      // up to two replicated gradient ranges (LeNet: conv1 atomic replicas, conv2 wgrad slabs)
+  Fold1 f[2];
 };
 
 // Returns false for float4 groups that are replica storage (r >= 1): they are not parameters.
 // For canonical groups, sums the replicas into g4 (written back so p.grad holds the true gradient).
 constexpr int kMaxFold = 16;
 
-__device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long i, float4& gg) {
+__device__ __forceinline__ bool fold_grad1(const Fold1& fd, float4* g4, long long i, float4& gg) {
   if (fd.off < 0 || fd.nrep <= 1) return true;
   const long long e64 = 4 * i - fd.off;
   if (e64 < 0 || e64 >= (long long)fd.stride * fd.nrep) return true;
@@ -64,12 +69,49 @@ __device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long 
   return true;
 }
 
+__device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long i, float4& gg) {
+  return fold_grad1(fd.f[0], g4, i, gg) && fold_grad1(fd.f[1], g4, i, gg);
+}
+
+// Replica storage (r >= 1) of the folded ranges is not parameters: the optimizer's index space skips
+// it without loading anything (the LeNet v2 conv2 slabs are 94 K float4, 46 % of the flat buffer).
+struct Holes {
+  long long lo[2], len[2];   // in float4 units, sorted, lo = huge when unused
+};
+
+__host__ __device__ __forceinline__ Holes make_holes(const Fold& fd) {
+  Holes h{{(long long)1 << 60, (long long)1 << 60}, {0, 0}};
+  for (int k = 0; k < 2; ++k) {
+    const Fold1& f = fd.f[k];
+    if (f.off >= 0 && f.nrep > 1) {
+      h.lo[k] = (f.off + f.stride) / 4;
+      h.len[k] = (long long)(f.nrep - 1) * f.stride / 4;
+    }
+  }
+  if (h.lo[1] < h.lo[0]) {
+    const long long a = h.lo[0], b = h.len[0];
+    h.lo[0] = h.lo[1]; h.len[0] = h.len[1];
+    h.lo[1] = a; h.len[1] = b;
+  }
+  return h;
+}
+
+__device__ __forceinline__ long long hole_map(const Holes& h, long long c) {   // compressed -> real index
+  if (c >= h.lo[0]) c += h.len[0];
+  if (c >= h.lo[1]) c += h.len[1];
+  return c;
+}
+
 __device__ __forceinline__ void pack_store(const Pack& pk, long long i, float v) {
   const long long e64 = i - pk.off;
   if (pk.off >= 0 && e64 >= 0 && e64 < 25000) {
     const int e = (int)e64;                 // 32-bit index math (64-bit division is ~100 instructions)
-    const int co = e / 500, k = e - co * 500, ci = k / 25, r = k - ci * 25;
-    pk.dst[(r * 20 + ci) * 64 + co] = v;
+    if (pk.mode == 2) {
+      pk.dst[pde_lenet_wp_index(e)] = v;
+    } else {
+      const int co = e / 500, k = e - co * 500, ci = k / 25, r = k - ci * 25;
+      pk.dst[(r * 20 + ci) * 64 + co] = v;
+    }
   }
 }
 
@@ -109,15 +151,22 @@ __device__ __forceinline__ void wait_epoch(const long long* epoch, long long t, 
   __syncthreads();
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, long long n4,
                                               float lr, float b1, float b2, float eps, float wd, int decoupled,
                                               float grad_scale, long long* __restrict__ step,
-                                              unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd, FusedAR ar) {
+                                              unsigned* __restrict__ arrive, int bump, Pack pk, Fold fd, FusedAR ar,
+                                              unsigned long long* __restrict__ prof) {
+  if constexpr (PROF) {
+    if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8] = __builtin_amdgcn_s_memrealtime();
+  }
   const long long t = bump < 0 ? *step : *step + 1;   // bump < 0: counter pre-advanced by an earlier kernel
   __shared__ uint32_t lds2[2];
+  const Holes holes = make_holes(fd);
+  const long long n4c = n4 - holes.len[0] - holes.len[1];   // compressed index space (replicas skipped)
   long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, istride = (long long)gridDim.x * blockDim.x;
-  long long lo = 0, hi = n4;                          // pass 1 range; pass 2 = [ar.lo4, n4) after the wait
+  long long lo = 0, hi = n4c;                         // pass 1 range; pass 2 = [ar.lo4, n4c) after the wait
   if (ar.nvb > 0) {
     if ((int)blockIdx.x < ar.nvb) {
       if (pde::peer_ar_f32_vblock(ar.pd, g + 4 * ar.lo4, g + 4 * ar.lo4, 4 * (n4 - ar.lo4), 1.f, blockIdx.x,
@@ -144,9 +193,10 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
     if (ar.nvb == 0 || (int)blockIdx.x < ar.nvb) break;   // block-uniform: wait_epoch has barriers
     wait_epoch(ar.epoch, t, ar.pd);                   // the all-reduced range is ready
     lo = ar.lo4;
-    hi = n4;
+    hi = n4c;
   }
-  for (long long i = lo + i0; i < hi; i += istride) {
+  for (long long ic = lo + i0; ic < hi; ic += istride) {
+    const long long i = hole_map(holes, ic);
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
     if (!fold_grad(fd, g4, i, gg)) continue;
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
@@ -171,6 +221,9 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
     for (int c = 1; c < bump; ++c) step[c] += 1;   // extra device counters (e.g. batch position)
     *arrive = 0u;
   }
+  if constexpr (PROF) {
+    if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // torch.optim.SGD semantics (torch/optim/sgd.py): d_p = g + wd*p; buf = momentum*buf + (1-dampening)*d_p
@@ -183,7 +236,10 @@ __global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, float* __res
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* g4 = reinterpret_cast<float4*>(g);
   float4* b4 = reinterpret_cast<float4*>(buf);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+  const Holes holes = make_holes(fd);
+  const long long n4c = n4 - holes.len[0] - holes.len[1];
+  for (long long ic = (long long)blockIdx.x * blockDim.x + threadIdx.x; ic < n4c; ic += (long long)gridDim.x * blockDim.x) {
+    const long long i = hole_map(holes, ic);
     float4 pp = p4[i], gg = g4[i];
     if (!fold_grad(fd, g4, i, gg)) continue;
     float4 bb = momentum != 0.f ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -237,7 +293,8 @@ hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, fl
                          float eps, float wd, int decoupled, float grad_scale, long long* step, unsigned* arrive,
                          int bump, long long pack_off, float* pack_dst, long long fold_off, int fold_len,
                          int fold_nrep, int fold_stride, const void* peer_dev, long long ar_off, long long* ar_epoch,
-                         int ar_two, hipStream_t st) {
+                         int ar_two, int pack_mode, long long fold2_off, int fold2_len, int fold2_nrep,
+                         int fold2_stride, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
   FusedAR ar{};
@@ -250,21 +307,34 @@ hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, fl
     const long long m4 = n4 - ar.lo4, work = ar_two ? (m4 + ar.pd.world - 1) / ar.pd.world : m4;
     ar.nvb = (int)std::min<long long>(32, std::max<long long>(1, (work + 255) / 256));
   }
-  hipLaunchKernelGGL(k_adam, dim3(grid_for(n4) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps, wd,
-                     decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
-                     Fold{fold_off, fold_len, fold_nrep, fold_stride}, ar);
+  const Fold fdh{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}};
+  const Holes hh = make_holes(fdh);
+  const long long n4c = n4 - hh.len[0] - hh.len[1];
+  if (ar.nvb > 0 && (hh.len[0] || hh.len[1]) && hh.lo[0] < ar.lo4) return hipErrorInvalidValue;   // holes above ar range start
+  unsigned long long* prof = pde_lenet_prof_slot(5);
+  if (prof)
+    hipLaunchKernelGGL(k_adam<true>, dim3(grid_for(n4c) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
+                       wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
+                       Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, prof);
+  else
+    hipLaunchKernelGGL(k_adam<false>, dim3(grid_for(n4c) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
+                       wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
+                       Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, nullptr);
   return hipGetLastError();
 }
 
 hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, float momentum, float dampening,
                         float wd, int nesterov, float grad_scale, long long* step, unsigned* arrive, int bump,
                         long long pack_off, float* pack_dst, long long fold_off, int fold_len, int fold_nrep,
-                        int fold_stride, hipStream_t st) {
+                        int fold_stride, int pack_mode, long long fold2_off, int fold2_len, int fold2_nrep,
+                        int fold2_stride, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4)), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
-                     nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst},
-                     Fold{fold_off, fold_len, fold_nrep, fold_stride});
+  const Holes hh = make_holes(Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride},
+                                    Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}});
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4 - hh.len[0] - hh.len[1])), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
+                     nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
+                     Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}});
   return hipGetLastError();
 }
 

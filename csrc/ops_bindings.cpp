@@ -11,6 +11,7 @@
 #include <optional>
 
 #include "pde_kernels.h"
+#include "pde_lenet.h"
 #include "pde_bind.h"
 #include "pde_peer.h"
 
@@ -200,7 +201,8 @@ void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, co
                double b1, double b2, double eps, double wd, bool decoupled, double grad_scale, const at::Tensor& step,
                const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst, int64_t fold_off,
                int64_t fold_len, int64_t fold_nrep, int64_t fold_stride, const OptT& peer_dev, int64_t ar_off,
-               const OptT& ar_epoch, int64_t ar_two) {
+               const OptT& ar_epoch, int64_t ar_two, int64_t pack_mode, int64_t fold2_off, int64_t fold2_len,
+               int64_t fold2_nrep, int64_t fold2_stride) {
   const int64_t n = p.numel();
   // fused all-reduce of [ar_off, n) by side blocks (peer_dev = CPU bytes of PeerAllReduce.device_args())
   const void* pdev = nullptr;
@@ -225,24 +227,31 @@ void adam_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, co
     TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
                     fold_off + fold_stride * fold_nrep <= n && fold_nrep <= 16,
                 "bad gradient fold layout (at most 16 replicas)");
+  if (fold2_off >= 0 && fold2_nrep > 1)
+    TORCH_CHECK(fold2_off % 4 == 0 && fold2_len % 4 == 0 && fold2_stride % 4 == 0 && fold2_len <= fold2_stride &&
+                    fold2_off + fold2_stride * fold2_nrep <= n && fold2_nrep <= 16,
+                "bad second gradient fold layout (at most 16 replicas)");
   check_cuda(v, "exp_avg_sq", F32, n);
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
   TORCH_CHECK(bump >= -1, "bump must be >= -1");
   check_cuda(arrive, "arrive", I32, 1);
   TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
-  float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
+  TORCH_CHECK(pack_mode == 1 || pack_mode == 2, "pack_mode must be 1 ([500][64]) or 2 (lenet_v2 image)");
+  float* pd = optr<float>(pack_dst, "pack_dst", F32, pack_mode == 2 ? kPdeWpFloats : 500 * 64);
   if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
   hip_check(pde_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), n, (float)lr, (float)b1,
                           (float)b2, (float)eps, (float)wd, decoupled ? 1 : 0, (float)grad_scale, ptr<long long>(step),
                           ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, fold_off, (int)fold_len,
-                          (int)fold_nrep, (int)fold_stride, pdev, ar_off, ep, (int)ar_two, cur_stream()),
+                          (int)fold_nrep, (int)fold_stride, pdev, ar_off, ep, (int)ar_two, (int)pack_mode, fold2_off,
+                          (int)fold2_len, (int)fold2_nrep, (int)fold2_stride, cur_stream()),
             "adam_flat");
 }
 
 void sgd_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, double lr, double momentum,
               double dampening, double wd, bool nesterov, double grad_scale, const at::Tensor& step,
               const at::Tensor& arrive, int64_t bump, int64_t pack_off, const OptT& pack_dst, int64_t fold_off,
-              int64_t fold_len, int64_t fold_nrep, int64_t fold_stride) {
+              int64_t fold_len, int64_t fold_nrep, int64_t fold_stride, int64_t pack_mode, int64_t fold2_off,
+              int64_t fold2_len, int64_t fold2_nrep, int64_t fold2_stride) {
   const int64_t n = p.numel();
   check_cuda(p, "params", F32);
   check_cuda(g, "grads", F32, n);
@@ -251,17 +260,127 @@ void sgd_flat(const at::Tensor& p, const at::Tensor& g, const at::Tensor& buf, d
     TORCH_CHECK(fold_off % 4 == 0 && fold_len % 4 == 0 && fold_stride % 4 == 0 && fold_len <= fold_stride &&
                     fold_off + fold_stride * fold_nrep <= n && fold_nrep <= 16,
                 "bad gradient fold layout (at most 16 replicas)");
+  if (fold2_off >= 0 && fold2_nrep > 1)
+    TORCH_CHECK(fold2_off % 4 == 0 && fold2_len % 4 == 0 && fold2_stride % 4 == 0 && fold2_len <= fold2_stride &&
+                    fold2_off + fold2_stride * fold2_nrep <= n && fold2_nrep <= 16,
+                "bad second gradient fold layout (at most 16 replicas)");
   check_cuda(step, "step", I64, std::max<int64_t>(1, bump));
   TORCH_CHECK(bump >= -1, "bump must be >= -1");
   check_cuda(arrive, "arrive", I32, 1);
   TORCH_CHECK(n % 4 == 0, "flat buffer length must be a multiple of 4");
-  float* pd = optr<float>(pack_dst, "pack_dst", F32, 500 * 64);
+  TORCH_CHECK(pack_mode == 1 || pack_mode == 2, "pack_mode must be 1 ([500][64]) or 2 (lenet_v2 image)");
+  float* pd = optr<float>(pack_dst, "pack_dst", F32, pack_mode == 2 ? kPdeWpFloats : 500 * 64);
   if (pack_off >= 0) TORCH_CHECK(pd && pack_off + 25000 <= n, "bad pack target");
   hip_check(pde_sgd_flat(ptr<float>(p), ptr<float>(g), ptr<float>(buf), n, (float)lr, (float)momentum,
                          (float)dampening, (float)wd, nesterov ? 1 : 0, (float)grad_scale, ptr<long long>(step),
                          ptr<unsigned>(arrive), (int)bump, pd ? pack_off : -1, pd, fold_off, (int)fold_len,
-                         (int)fold_nrep, (int)fold_stride, cur_stream()),
+                         (int)fold_nrep, (int)fold_stride, (int)pack_mode, fold2_off, (int)fold2_len,
+                         (int)fold2_nrep, (int)fold2_stride, cur_stream()),
             "sgd_flat");
+}
+
+void lenet_pack_w2_v2(const at::Tensor& w2, const at::Tensor& dst) {
+  check_cuda(w2, "conv2.weight", F32, 25000);
+  check_cuda(dst, "Wp", F32, kPdeWpFloats);
+  hip_check(pde_lenet_pack_w2_v2(ptr<float>(w2), ptr<float>(dst), cur_stream()), "lenet_pack_w2_v2");
+}
+
+void lenet_conv_fwd2(const at::Tensor& Xb, int64_t B, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& Wp,
+                     const at::Tensor& b2, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& P2,
+                     const at::Tensor& A2, const OptT& zero) {
+  TORCH_CHECK(B >= 1 && B <= 65535, "batch must be in [1, 65535]");
+  check_cuda(Xb, "Xb", F32, B * 784);
+  check_cuda(w1, "conv1.weight", F32, 500);
+  check_cuda(b1, "conv1.bias", F32, 20);
+  check_cuda(Wp, "Wp", F32, kPdeWpFloats);
+  check_cuda(b2, "conv2.bias", F32, 50);
+  check_cuda(P1, "P1", F32, B * 2880);
+  check_cuda(A1, "A1", U8, B * 2880);
+  check_cuda(P2, "P2", F32, B * 800);
+  check_cuda(A2, "A2", U8, B * 800);
+  for (const at::Tensor* t : {&Xb, &w1, &Wp, &P1})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv_fwd2 operands must be 16-B aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A1.data_ptr()) % 4 == 0, "A1 must be 4-B aligned");
+  float* zp = optr<float>(zero, "zero", F32);
+  hip_check(pde_lenet_conv_fwd2(ptr<float>(Xb), (int)B, ptr<float>(w1), ptr<float>(b1), ptr<float>(Wp), ptr<float>(b2),
+                                ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(P2), ptr<uint8_t>(A2), zp,
+                                zp ? (int)zero->numel() : 0, cur_stream()),
+            "lenet_conv_fwd2");
+}
+
+void lenet_gather(const at::Tensor& X, const at::Tensor& labels, const OptT& idx, const OptT& ctr, int64_t nbatches,
+                  int64_t B, const at::Tensor& Xdst, const at::Tensor& Ydst, const OptT& rows_dst) {
+  check_cuda(X, "X", F32);
+  TORCH_CHECK(X.numel() % 784 == 0, "X must be [N,1,28,28]");
+  check_cuda(labels, "labels", I64, X.numel() / 784);
+  const int* ip = optr<int>(idx, "idx", I32, 1);
+  if (!ip) TORCH_CHECK(X.numel() >= B * 784, "X smaller than batch");
+  const long long* cp = optr<long long>(ctr, "ctr", I64, 1);
+  if (cp) TORCH_CHECK(ip && nbatches >= 1, "counter-indexed batches need idx");
+  check_cuda(Xdst, "Xdst", F32, B * 784);
+  check_cuda(Ydst, "Ydst", I64, B);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(Xdst.data_ptr()) % 16 == 0,
+              "gather buffers must be 16-B aligned");
+  hip_check(pde_lenet_gather(ptr<float>(X), ptr<long long>(labels), ip, ip ? (int)idx->numel() : 0, cp, (int)nbatches,
+                             (int)B, ptr<float>(Xdst), ptr<long long>(Ydst), optr<int>(rows_dst, "rows_dst", I32, B),
+                             cur_stream()),
+            "lenet_gather");
+}
+
+void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& dP2m,
+                     const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& gW1c,
+                     const at::Tensor& gb1c, int64_t c1_nrep, int64_t c1_rep_stride, const at::Tensor& gW2c,
+                     const at::Tensor& gb2c, int64_t slab_stride, const OptT& row_loss, const OptT& row_hit,
+                     const OptT& loss_sum, const OptT& correct, const OptT& gX, const OptT& glabels, const OptT& gidx,
+                     const OptT& gctr, int64_t gnbatches, int64_t gstride, const OptT& gXdst, const OptT& gYdst,
+                     const OptT& grows, int64_t dbg) {
+  TORCH_CHECK(B >= 1 && B <= 512, "conv_bwd2: batch must be in [1, 512]");
+  TORCH_CHECK(slab_stride == 0 || B <= 128, "conv_bwd2: gradient slabs need B <= 128");
+  check_cuda(Xb, "Xb", F32, B * 784);
+  check_cuda(P1, "P1", F32, B * 2880);
+  check_cuda(A1, "A1", U8, B * 2880);
+  check_cuda(dP2m, "dP2m", F32, B * 800);
+  check_cuda(A2, "A2", U8, B * 800);
+  check_cuda(W2c, "conv2.weight", F32, 25000);
+  const int64_t nrep = std::max<int64_t>(1, c1_nrep);
+  check_cuda(gW1c, "conv1 grad", F32, (nrep - 1) * c1_rep_stride + 500);
+  check_cuda(gb1c, "conv1 bias grad", F32, (nrep - 1) * c1_rep_stride + 20);
+  check_cuda(gW2c, "conv2 grad", F32, slab_stride > 0 ? 15 * slab_stride + 25000 : 25000);
+  check_cuda(gb2c, "conv2 bias grad", F32, slab_stride > 0 ? 15 * slab_stride + 50 : 50);
+  for (const at::Tensor* t : {&Xb, &P1, &dP2m})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv_bwd2 operands must be 16-B aligned");
+  const bool meters = row_loss.has_value() && row_hit.has_value() && loss_sum.has_value() && correct.has_value();
+  const bool gather = gX.has_value();
+  if (gather) {
+    TORCH_CHECK(glabels.has_value() && gidx.has_value() && gctr.has_value() && gXdst.has_value() &&
+                    gYdst.has_value() && grows.has_value() && gnbatches >= 1 && gstride >= B,
+                "conv_bwd2 prefetch needs labels, idx, counter, destinations");
+    check_cuda(*gX, "gX", F32);
+    check_cuda(*gXdst, "gXdst", F32, B * 784);
+    check_cuda(*gYdst, "gYdst", I64, B);
+    check_cuda(*grows, "grows", I32, B);
+  }
+  hip_check(pde_lenet_conv_bwd2(ptr<float>(Xb), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(dP2m), ptr<uint8_t>(A2),
+                                ptr<float>(W2c), (int)B, ptr<float>(gW1c), ptr<float>(gb1c), (int)nrep,
+                                (int)c1_rep_stride, ptr<float>(gW2c), ptr<float>(gb2c), (int)slab_stride,
+                                meters ? ptr<float>(*row_loss) : nullptr, meters ? ptr<int>(*row_hit) : nullptr,
+                                meters ? ptr<double>(*loss_sum) : nullptr,
+                                meters ? reinterpret_cast<unsigned long long*>(correct->data_ptr<int64_t>()) : nullptr,
+                                gather ? ptr<float>(*gX) : nullptr, gather ? ptr<long long>(*glabels) : nullptr,
+                                gather ? ptr<int>(*gidx) : nullptr, gather ? (int)gidx->numel() : 0,
+                                gather ? ptr<long long>(*gctr) : nullptr, (int)gnbatches, (int)gstride,
+                                gather ? ptr<float>(*gXdst) : nullptr, gather ? ptr<long long>(*gYdst) : nullptr,
+                                gather ? ptr<int>(*grows) : nullptr, (int)dbg, cur_stream()),
+            "lenet_conv_bwd2");
+}
+
+void lenet_set_prof(const OptT& buf) {
+  if (buf.has_value()) {
+    check_cuda(*buf, "prof", I64, 6 * 4096 * 8);
+    pde_lenet_set_prof(reinterpret_cast<unsigned long long*>(buf->data_ptr<int64_t>()));
+  } else {
+    pde_lenet_set_prof(nullptr);
+  }
 }
 
 void lenet_pack_w2(const at::Tensor& w2, const at::Tensor& dst) {
@@ -436,12 +555,29 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),
         py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0,
         py::arg("peer_dev") = py::none(), py::arg("ar_off") = 0, py::arg("ar_epoch") = py::none(),
-        py::arg("ar_two") = 0);
+        py::arg("ar_two") = 0, py::arg("pack_mode") = 1, py::arg("fold2_off") = -1, py::arg("fold2_len") = 0,
+        py::arg("fold2_nrep") = 1, py::arg("fold2_stride") = 0);
   m.def("sgd_flat", &sgd_flat, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
         py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("grad_scale"), py::arg("step"),
         py::arg("arrive"), py::arg("bump"), py::arg("pack_off") = -1, py::arg("pack_dst") = py::none(),
-        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0);
+        py::arg("fold_off") = -1, py::arg("fold_len") = 0, py::arg("fold_nrep") = 1, py::arg("fold_stride") = 0,
+        py::arg("pack_mode") = 1, py::arg("fold2_off") = -1, py::arg("fold2_len") = 0, py::arg("fold2_nrep") = 1,
+        py::arg("fold2_stride") = 0);
   m.def("lenet_pack_w2", &lenet_pack_w2);
+  m.def("lenet_pack_w2_v2", &lenet_pack_w2_v2);
+  m.def("lenet_conv_fwd2", &lenet_conv_fwd2, py::arg("Xb"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wp"),
+        py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("zero") = py::none());
+  m.def("lenet_conv_bwd2", &lenet_conv_bwd2, py::arg("Xb"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
+        py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("c1_nrep"),
+        py::arg("c1_rep_stride"), py::arg("gW2c"), py::arg("gb2c"), py::arg("slab_stride"),
+        py::arg("row_loss") = py::none(), py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(),
+        py::arg("correct") = py::none(), py::arg("gX") = py::none(), py::arg("glabels") = py::none(),
+        py::arg("gidx") = py::none(), py::arg("gctr") = py::none(), py::arg("gnbatches") = 1, py::arg("gstride") = 0,
+        py::arg("gXdst") = py::none(), py::arg("gYdst") = py::none(), py::arg("grows") = py::none(),
+        py::arg("dbg") = 0);
+  m.def("lenet_gather", &lenet_gather, py::arg("X"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
+        py::arg("nbatches"), py::arg("B"), py::arg("Xdst"), py::arg("Ydst"), py::arg("rows_dst"));
+  m.def("lenet_set_prof", &lenet_set_prof, py::arg("buf") = py::none());
   m.def("scale_", &scale_);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("transA") = false,

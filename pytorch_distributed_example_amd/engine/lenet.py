@@ -23,6 +23,7 @@ xGMI peer kernel -- by timing whole steps on the node: ``autotune_schedule``)
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -35,12 +36,14 @@ FC_BUCKET = ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"]
 CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv1.grad_replicas", "conv2.weight", "conv2.bias"]
 C1_NREP = 16          # conv1 gradient replicas (atomic contention: 128 images -> 8 adders per address)
 C1_STRIDE = 576       # conv1.weight (500 -> 512 slot) + conv1.bias (20 -> 64 slot)
+C2_NREP = 16          # conv2 wgrad slabs of the v2 step (one per 8-image group, folded by the optimizer)
+C2_STRIDE = 25088     # conv2.weight (25000 -> 25024 slot) + conv2.bias (50 -> 64 slot)
 
 
 class LeNetTrainStep:
     def __init__(self, net: torch.nn.Module, batch_size: int = 128, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, optimizer: str = "adam", momentum: float = 0.0,
-                 comm=None, overlap: bool = True, force_comm: bool = False):
+                 comm=None, overlap: bool = True, force_comm: bool = False, v2: Optional[bool] = None):
         self.net = net
         p0 = next(net.parameters())
         if not p0.is_cuda:
@@ -65,8 +68,19 @@ class LeNetTrainStep:
         self.comm_on = comm is not None and (self.world > 1 or force_comm)
         self.K = kernels()
         dev = self.device
-        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, CONV_BUCKET],
-                                 extra_shapes={"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,)})
+        # v2 step (csrc/kernels/lenet_v2.hip): prefetched batches, LDS-DMA weight staging, 8-wave conv
+        # forward, co-resident conv backward.  W = 1 (no comm path): the conv2 weight gradient is
+        # written as 16 deterministic per-image-group slabs folded by the optimizer; with a comm path
+        # the slabs would multiply the all-reduced bytes, so it is accumulated with float atomics.
+        self.v2 = (os.environ.get("PDE_LENET_V2", "1") != "0") if v2 is None else bool(v2)
+        self.slabs = self.v2 and not self.comm_on and self.B <= 128
+        extra = {"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,)}
+        conv_bucket = list(CONV_BUCKET)
+        if self.slabs:
+            extra["conv2.grad_replicas"] = ((C2_NREP - 1) * C2_STRIDE,)
+            conv_bucket.append("conv2.grad_replicas")
+        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, conv_bucket],
+                                 extra_shapes=extra)
         self.params, self.grads = self.layout.bind(net)
         V = self.layout.view
         self.p = {n: V(self.params, n) for n in self.layout.param_names}
@@ -77,12 +91,30 @@ class LeNetTrainStep:
         self.c1_off = c1
         self.g_c1w_rep = self.grads[c1: c1 + C1_NREP * C1_STRIDE]
         self.g_c1b_rep = self.grads[c1 + 512: c1 + C1_NREP * C1_STRIDE]
+        c2 = self.layout.slots["conv2.weight"].offset
+        assert self.layout.slots["conv2.bias"].offset == c2 + 25024
+        self.c2_off = c2
+        if self.slabs:
+            assert self.layout.slots["conv2.grad_replicas"].offset == c2 + C2_STRIDE
+            self.g_c2w_rep = self.grads[c2: c2 + C2_NREP * C2_STRIDE]
+            self.g_c2b_rep = self.grads[c2 + 25024: c2 + C2_NREP * C2_STRIDE]
+            self.zero_view = self.grads[c1: c1 + C1_NREP * C1_STRIDE]    # only the atomic targets
+        else:
+            self.g_c2w_rep = self.grads[c2: c2 + 25000]
+            self.g_c2b_rep = self.grads[c2 + 25024: c2 + 25024 + 50]
         self.bucket_grads = [self.layout.bucket_view(self.grads, i) for i in range(2)]
+        if not self.slabs:
+            self.zero_view = self.bucket_grads[1]
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params) if optimizer == "adam" else self.m
         self.counters = torch.zeros(2, device=dev, dtype=torch.int64)   # [optimizer step, batch in epoch]
         self.arrive = torch.zeros(1, device=dev, dtype=torch.int32)
-        self.Wt2 = pack_conv2_weight(self.p["conv2.weight"])
+        if self.v2:
+            self.Wp = torch.zeros(2 * 72 * 256, device=dev, dtype=torch.float32)   # padding stays zero
+            self.K.lenet_pack_w2_v2(self.p["conv2.weight"].detach().contiguous(), self.Wp)
+            self.Wt2 = None
+        else:
+            self.Wt2 = pack_conv2_weight(self.p["conv2.weight"])
         self.pack_off = self.layout.slots["conv2.weight"].offset
         f32 = dict(device=dev, dtype=torch.float32)
         B = self.B
@@ -96,6 +128,11 @@ class LeNetTrainStep:
         self.dP2m = torch.empty(B * 800, **f32)
         self.cur_row = torch.zeros(B, device=dev, dtype=torch.int32)
         self.cur_lbl = torch.zeros(B, device=dev, dtype=torch.int64)
+        # v2 prefetch buffers, double-buffered by step parity q (host-tracked; baked into captured graphs)
+        self.Xb = torch.zeros(2, B, 784, **f32)
+        self.Yb = torch.zeros(2, B, device=dev, dtype=torch.int64)
+        self.rowsb = torch.zeros(2, B, device=dev, dtype=torch.int32)
+        self.q = 0
         self.row_loss = torch.zeros(B, **f32)
         self.row_hit = torch.zeros(B, device=dev, dtype=torch.int32)
         self.loss_sum = torch.zeros(1, device=dev, dtype=torch.float64)
@@ -113,6 +150,7 @@ class LeNetTrainStep:
         self.X = self.Y = self.idx = None
         self.nbatches = 0
         self.graphs = {}
+        self.bwd_dbg = 0          # ablation switch of the v2 conv backward (tools/lenet_phases.py only)
 
     # ------------------------------------------------------------------ data binding
     def bind_dataset(self, images: torch.Tensor, labels: torch.Tensor):
@@ -134,6 +172,9 @@ class LeNetTrainStep:
         self.tail = n - self.nfull * self.B
         self.nbatches = self.nfull + (1 if self.tail else 0)
         self.counters[1].zero_()
+        if self.v2:      # prefetch batch 0 of the epoch into the current parity's buffers
+            self.K.lenet_gather(self.X, self.Y, self.idx, None, self.nbatches, self.B, self.Xb[self.q],
+                                self.Yb[self.q], self.rowsb[self.q])
 
     # ------------------------------------------------------------------ the step
     def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None):
@@ -144,8 +185,13 @@ class LeNetTrainStep:
         K, sl = self.K, slice(lo, hi)
         pack_off = self.pack_off - lo if conv else -1
         fold_off = self.c1_off - lo if conv else -1
+        f2 = dict(fold2_off=self.c2_off - lo, fold2_len=C2_STRIDE, fold2_nrep=C2_NREP,
+                  fold2_stride=C2_STRIDE) if (conv and self.slabs) else {}
         pack = self.Wt2 if conv else None
         scale = 1.0 / self.world
+        mode = 1
+        if conv and self.v2:
+            pack, mode = self.Wp, 2
         if self.optimizer == "adam":
             far = {}
             if fuse_ar is not None:
@@ -153,11 +199,11 @@ class LeNetTrainStep:
                            ar_epoch=self.ar_epoch, ar_two=int(fuse_ar == "adam2"))
             K.adam_flat(self.params[sl], self.grads[sl], self.m[sl], self.v[sl], self.lr, self.betas[0],
                         self.betas[1], self.eps, self.wd, False, scale, self.counters, self.arrive, -1, pack_off,
-                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE, **far)
+                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE, pack_mode=mode, **f2, **far)
         else:
             K.sgd_flat(self.params[sl], self.grads[sl], self.m[sl], self.lr, self.momentum, 0.0, self.wd, False,
                        scale, self.counters, self.arrive, -1, pack_off, pack, fold_off, C1_STRIDE, C1_NREP,
-                       C1_STRIDE)
+                       C1_STRIDE, pack_mode=mode, **f2)
 
     def _launch(self, B: int):
         """One step on the current stream: conv_fwd -> fc1 -> head -> fc_bwd -> conv_bwd -> opt.
@@ -173,22 +219,46 @@ class LeNetTrainStep:
         with write-through H1 stores + agent-scope loads 83 us, against 69 us for two launches: one
         wave doing 4 latency-bound rows serially costs more than the kernel boundary it saves.)"""
         K, p, g = self.K, self.p, self.g
-        K.lenet_conv_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
-                         p["conv1.weight"], p["conv1.bias"], self.Wt2, p["conv2.bias"], self.P1, self.A1, self.P2,
-                         self.A2, self.cur_row, self.cur_lbl, self.bucket_grads[1])
+        q = self.q
+        if self.v2:
+            K.lenet_conv_fwd2(self.Xb[q], B, p["conv1.weight"], p["conv1.bias"], self.Wp, p["conv2.bias"], self.P1,
+                              self.A1, self.P2, self.A2, self.zero_view)
+            rows, labels = self.rowsb[q], self.Yb[q]
+        else:
+            K.lenet_conv_fwd(self.X, self.idx, self.counters[1:], self.nbatches, self.B, self.Y, B,
+                             p["conv1.weight"], p["conv1.bias"], self.Wt2, p["conv2.bias"], self.P1, self.A1, self.P2,
+                             self.A2, self.cur_row, self.cur_lbl, self.bucket_grads[1])
+            rows, labels = self.cur_row, self.cur_lbl
         K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1, self.counters)   # bumps counters
-        K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], self.cur_lbl, 1.0 / B, None, self.dZ2, self.dZ1,
+        K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], labels, 1.0 / B, None, self.dZ2, self.dZ1,
                      self.row_loss, self.row_hit, None, None)
+        fused = self.comm_on and self.mode == "fused"
+        if self.v2:
+            self.q = 1 - q
+            if fused:       # the first-generation conv backward (peer side blocks) has no prefetch role
+                K.lenet_gather(self.X, self.Y, self.idx, self.counters[1:], self.nbatches, self.B, self.Xb[1 - q],
+                               self.Yb[1 - q], self.rowsb[1 - q])
         # the loss / accuracy meters are folded by an extra block of conv_bwd (off fc_bwd's chain)
         fc_args = (self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
                    g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], None, None, None, None)
-        conv_args = (self.X, self.cur_row, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
+        conv_args = (self.X, rows, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
                      self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE,
                      self.row_loss, self.row_hit, self.loss_sum, self.correct)
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)
-        if self.comm_on and self.mode == "fused":
+        if self.v2 and not fused:
+            # conv backward v2; D blocks also prefetch the next batch (counters[1] was advanced by fc1)
+            # into the other parity's buffers and fold the meters
+            conv_bwd = lambda: K.lenet_conv_bwd2(
+                self.Xb[q], self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B, self.g_c1w_rep,
+                self.g_c1b_rep, C1_NREP, C1_STRIDE, self.g_c2w_rep, self.g_c2b_rep, C2_STRIDE if self.slabs else 0,
+                self.row_loss, self.row_hit, self.loss_sum, self.correct, self.X, self.Y, self.idx,
+                self.counters[1:], self.nbatches, self.B, self.Xb[1 - q], self.Yb[1 - q], self.rowsb[1 - q],
+                self.bwd_dbg)
+        else:
+            conv_bwd = lambda: K.lenet_conv_bwd(*conv_args)
+        if fused:
             fc_route = self.comm.routes.get(self.bucket_grads[0].numel(), "peer2")
             K.lenet_conv_bwd(*conv_args, 0, self._peer_device_args(), self.bucket_grads[0], int(fc_route == "peer2"))
             conv_route = self.comm.routes.get(self.bucket_grads[1].numel(), "rccl")
@@ -203,7 +273,7 @@ class LeNetTrainStep:
             cs.wait_event(ev["fc"])
             with torch.cuda.stream(cs):
                 self.comm.all_reduce_(self.bucket_grads[0])
-        K.lenet_conv_bwd(*conv_args)
+        conv_bwd()
         if not self.comm_on:
             self._opt(0, self.params.numel(), True)
             return
@@ -251,7 +321,9 @@ class LeNetTrainStep:
     def capture(self, B: Optional[int] = None, warmup: int = 0, steps: int = 1):
         """Capture ``steps`` consecutive steps of batch size B into one hipGraph (replayed by
         ``replay``).  Every step reads its batch position / optimizer step from device counters, so
-        a multi-step graph is just the step chain repeated; it amortises the per-replay launch cost."""
+        a multi-step graph is just the step chain repeated; it amortises the per-replay launch cost.
+        The v2 step alternates its prefetch buffers by step parity: a graph is keyed by the parity it
+        starts at (capturing does not execute, so the host parity is restored afterwards)."""
         B = B or self.B
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -259,21 +331,25 @@ class LeNetTrainStep:
             for _ in range(warmup):
                 self._launch(B)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        q0 = self.q
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(steps):
                 self._launch(B)
-        self.graphs[(B, steps)] = g
+        self.q = q0
+        self.graphs[(B, steps, q0)] = g
         return g
 
     def replay(self, B: Optional[int] = None, steps: int = 1):
         """Run ``steps`` steps through the (captured on first use) graph of that many steps."""
         B = B or self.B
-        g = self.graphs.get((B, steps))
+        g = self.graphs.get((B, steps, self.q))
         if g is None:
             g = self.capture(B, steps=steps)
             # capturing does not execute: replay now so call semantics stay "steps steps"
         g.replay()
+        if self.v2 and steps % 2:
+            self.q = 1 - self.q
 
     # ------------------------------------------------------------------ epochs / meters
     def run_epoch(self, use_graph: bool = True):
@@ -313,8 +389,12 @@ class LeNetTrainStep:
         H1 = torch.empty(bs * 500, device=self.device)
         for s in range(0, n, bs):
             B = min(bs, n - s)
-            K.lenet_conv_fwd(X[s:s + B], None, None, 0, 0, None, B, p["conv1.weight"], p["conv1.bias"], self.Wt2,
-                             p["conv2.bias"], P1, A1, P2, A2, None, None, None)
+            if self.v2:
+                K.lenet_conv_fwd2(X[s:s + B], B, p["conv1.weight"], p["conv1.bias"], self.Wp, p["conv2.bias"], P1,
+                                  A1, P2, A2)
+            else:
+                K.lenet_conv_fwd(X[s:s + B], None, None, 0, 0, None, B, p["conv1.weight"], p["conv1.bias"],
+                                 self.Wt2, p["conv2.bias"], P1, A1, P2, A2, None, None, None)
             K.lenet_fc1_fwd(P2, B, p["fc1.weight"], p["fc1.bias"], H1, None)
             K.lenet_head(H1, B, p["fc2.weight"], p["fc2.bias"], Y[s:s + B], 1.0 / B, None, None, None,
                          None, None, self.eval_loss, self.eval_correct)
@@ -357,7 +437,10 @@ class LeNetTrainStep:
 
     def sync_params(self):
         """Re-derive kernel-side weight copies after parameters were changed externally."""
-        pack_conv2_weight(self.p["conv2.weight"], self.Wt2)
+        if self.v2:
+            self.K.lenet_pack_w2_v2(self.p["conv2.weight"].detach().contiguous(), self.Wp)
+        else:
+            pack_conv2_weight(self.p["conv2.weight"], self.Wt2)
 
     # ------------------------------------------------------------------ schedule autotuning (W > 1)
     def schedule_candidates(self):
@@ -397,8 +480,10 @@ class LeNetTrainStep:
         if not self.comm_on:
             return {}
         cands = candidates or self.schedule_candidates()
-        state = [self.params, self.m, self.counters] + ([self.v] if self.v is not self.m else [])
+        state = [self.params, self.m, self.counters, self.Xb, self.Yb, self.rowsb] + (
+            [self.v] if self.v is not self.m else [])
         snap = [t.clone() for t in state]
+        q_saved = self.q
         saved_idx = None if self.idx is None else (self.idx, self.nfull, self.tail, self.nbatches)
         if self.idx is None or self.nfull < 1:
             raise RuntimeError("bind a dataset and set epoch indices before autotune_schedule")
@@ -425,6 +510,7 @@ class LeNetTrainStep:
                 continue
             for t, s0 in zip(state, snap):       # every candidate starts from the same (replicated) state
                 t.copy_(s0)
+            self.q = q_saved
             self.ar_epoch.fill_(-1)              # optimizer steps repeat: no stale completion word
             self.sync_params()
             self.mode = mode
@@ -467,6 +553,7 @@ class LeNetTrainStep:
         # restore the training state the trial steps advanced
         for t, s0 in zip(state, snap):
             t.copy_(s0)
+        self.q = q_saved
         self.ar_epoch.fill_(-1)
         self.sync_params()
         self.idx, self.nfull, self.tail, self.nbatches = saved_idx

@@ -135,3 +135,56 @@ def test_graph_replay_equals_eager():
         outs.append((eng.params.clone(), eng.read_meters()))
     assert int(outs[0][1][1]) == int(outs[1][1][1])
     _mostly_close(outs[1][0], outs[0][0], 2e-6, 5 * 2e-3, "graph vs eager params")
+
+
+@pytest.mark.parametrize("B", [1, 37, 128])
+def test_conv_fwd2_matches_v1_and_torch(B):
+    """lenet_v2.hip conv forward (prefetched batch, LDS-DMA weights, 16x16x4 conv2 tiles) against the
+    first-generation kernel and against the fp64 torch conv/pool chain."""
+    from pytorch_distributed_example_amd._ext import kernels
+    from pytorch_distributed_example_amd.ops.lenet_fused import LeNetWorkspace, pack_conv2_weight
+    K = kernels()
+    net = build_net(seed=6, device=DEV)
+    x, _ = _batch(B, seed=40 + B)
+    xd = x.to(DEV).reshape(B, 784).contiguous()
+    w1, b1 = net.conv1.weight.detach().contiguous(), net.conv1.bias.detach().contiguous()
+    w2, b2 = net.conv2.weight.detach().contiguous(), net.conv2.bias.detach().contiguous()
+    ws1, ws2 = LeNetWorkspace(B, DEV), LeNetWorkspace(B, DEV)
+    pack_conv2_weight(w2, ws1.Wt2)
+    K.lenet_conv_fwd(xd, None, None, 0, 0, None, B, w1, b1, ws1.Wt2, b2, ws1.P1, ws1.A1, ws1.P2, ws1.A2, None, None,
+                     None)
+    Wp = torch.zeros(2 * 72 * 256, device=DEV)
+    K.lenet_pack_w2_v2(w2, Wp)
+    K.lenet_conv_fwd2(xd, B, w1, b1, Wp, b2, ws2.P1, ws2.A1, ws2.P2, ws2.A2)
+    torch.cuda.synchronize()
+    xr = x.double()
+    c1 = torch.nn.functional.conv2d(xr, w1.double().cpu(), b1.double().cpu()).relu()
+    p1, i1 = torch.nn.functional.max_pool2d(c1, 2, 2, return_indices=True)
+    c2 = torch.nn.functional.conv2d(p1, w2.double().cpu(), b2.double().cpu()).relu()
+    p2 = torch.nn.functional.max_pool2d(c2, 2, 2)
+    _close(ws2.P1.view(B, 20, 12, 12), p1, 1e-5, 1e-6, "P1 v2 vs torch")
+    _close(ws2.P2.view(B, 50, 4, 4), p2, 1e-5, 1e-6, "P2 v2 vs torch")
+    _close(ws2.P2, ws1.P2, 1e-5, 1e-6, "P2 v2 vs v1")
+    assert torch.equal(ws2.P1, ws1.P1) and torch.equal(ws2.A1, ws1.A1)     # same conv1 code path
+    agree = (ws2.A2 == ws1.A2).double().mean().item()
+    assert agree > 0.995, f"A2 argmax codes agree on only {agree:.4f}"     # ties broken by rounding order
+
+
+def test_engine_v2_tracks_v1():
+    """The v2 step (prefetch + new conv forward) trains like the first-generation step."""
+    B, n = 128, 6 * 128
+    x, y = _batch(n, seed=21)
+    res = []
+    for v2 in (False, True):
+        net = build_net(seed=8, device=DEV)
+        eng = LeNetTrainStep(net, batch_size=B, v2=v2)
+        eng.bind_dataset(x.to(DEV), y.to(DEV))
+        eng.set_epoch_indices(torch.randperm(n, generator=torch.Generator().manual_seed(2)).to(torch.int32))
+        for _ in range(3):
+            eng.step()
+        eng.replay(steps=2)
+        eng.replay(steps=1)
+        torch.cuda.synchronize()
+        res.append((torch.cat([p.detach().reshape(-1) for p in net.parameters()]), eng.read_meters()))
+    _mostly_close(res[1][0], res[0][0], 2e-6, 6 * 2e-3, "v2 vs v1 params after 6 steps")
+    assert abs(res[1][1][0] - res[0][1][0]) <= 1e-3 * abs(res[0][1][0]) + 1e-3
