@@ -15,8 +15,9 @@
 //    of each 32-lane half on disjoint bank sets;
 //  * bias + ReLU + 2x2 max-pool (first maximum in scan order, as ATen) on the accumulator registers with
 //    lane shuffles (pixel neighbours are lanes ^1 / ^4 / ^5 of a 4x4 tile);
-//  * P1 / A1 (conv1 pooled output + argmax codes, kept for backward) are written at the END from LDS,
-//    split between the two co-half blocks, so no store sits in the VMEM queue ahead of the LDS-DMA wait.
+//  * P1 / A1 (conv1 pooled output + argmax codes, kept for backward) are written from LDS right after
+//    the conv1 -> conv2 barrier (split between the two co-half blocks): behind the LDS-DMA wait, so no
+//    store delays it, and they drain under conv2 instead of at the kernel tail.
 //
 // Packed conv2 weight ("Wp"), written by the optimizer's repack epilogue (optim.hip, pack mode 2):
 //   Wp[ct][cotile][kq][co16][132]  (ct = co >> 5, cotile = (co >> 4) & 1, co16 = co & 15)
@@ -36,9 +37,10 @@ constexpr int kWpHalf = 72 * 256;            // floats per co-half region (72 KB
 constexpr int kL_W = 0;
 constexpr int kL_XS = kWpHalf;               // [20][144] pooled conv1 output
 constexpr int kL_CODE = kL_XS + kP1;         // [20][144] uint8 argmax codes (720 floats)
-constexpr int kL_IMG = kL_CODE + 720;        // [784]
-constexpr int kL_W1 = kL_IMG + kImg;         // conv1 weight [500] + bias [20] (+pad)
-constexpr int kL_TOT = kL_W1 + 528;          // 23344 floats = 91 KB
+constexpr int kImgRow = 48;                  // padded image row (28 -> 48 floats: rows 16 banks apart)
+constexpr int kL_IMG = kL_CODE + 720;        // [28][48]
+constexpr int kL_W1 = kL_IMG + 28 * kImgRow; // conv1 weight [500] + bias [20] (+pad)
+constexpr int kL_TOT = kL_W1 + 528;          // 23904 floats = 93 KB
 
 #define PMARK(ph)                                                                             \
   do {                                                                                        \
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   float bias2[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bias2[r] = b2[min(co_base + r, 49)];
-  if (t < kImg / 4) reinterpret_cast<float4*>(smem + kL_IMG)[t] = xv;
+  if (t < kImg / 4) reinterpret_cast<float4*>(smem + kL_IMG + (t / 7) * kImgRow)[t % 7] = xv;
   if (t < 125) reinterpret_cast<float4*>(smem + kL_W1)[t] = wv;
   if (t < 20) smem[kL_W1 + 500 + t] = bv1;
   // ---- then the conv2 weight image by LDS-DMA: 72 x 1 KB, exactly 9 per wave ----
@@ -78,13 +80,20 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
       __builtin_amdgcn_global_load_lds(wsrc + c * 256 + l * 4, smem + kL_W + c * 256, 16, 0, 0);
     }
   }
+  // gradient-buffer zeroing (atomic targets of the backward) drains while conv1 computes
+  if (zero_ptr) {
+    const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
+    for (int i = bid * 512 + t; i < zero_n; i += nb * 512) zero_ptr[i] = 0.f;
+  }
   // barrier without draining the LDS-DMA (a __syncthreads() would wait vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   PMARK(1);
   // ---- phase 1: conv1 (1->20, 5x5) + bias + ReLU + 2x2 max-pool on v_mfma_f32_32x32x2_f32 ----
   // C[m][ch] = sum_tap im2col[m][tap] * W1[ch][tap], m = 4 * pooled_pos + (dy*2+dx): accumulator rows
-  // 4g..4g+3 are the 4 sub-positions of one pooled position -> pooled in registers.
+  // 4g..4g+3 are the 4 sub-positions of one pooled position -> pooled in registers.  (Measured and
+  // rejected: the transposed C[ch][m] with the pool as a max over lanes -- its 48 lane shuffles per
+  // tile lower to LDS permutes and made this phase 6.6 us instead of 3.6.)
   {
     const float* xin = smem + kL_IMG;
     const float* w1s = smem + kL_W1;
@@ -104,12 +113,12 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
       const int tile = w + 8 * it;
       if (tile < 18) {
         const int m = tile * 32 + ch, pp = m >> 2, sub = m & 3;
-        const float* xa = xin + (2 * (pp / 12) + (sub >> 1)) * 28 + 2 * (pp % 12) + (sub & 1);
+        const float* xa = xin + (2 * (pp / 12) + (sub >> 1)) * kImgRow + 2 * (pp % 12) + (sub & 1);
         float av[13];
 #pragma unroll
         for (int s2 = 0; s2 < 13; ++s2) {
           const int t0 = 2 * s2, t1 = min(2 * s2 + 1, 24);
-          av[s2] = hi ? xa[(t1 / 5) * 28 + t1 % 5] : xa[(t0 / 5) * 28 + t0 % 5];
+          av[s2] = hi ? xa[(t1 / 5) * kImgRow + t1 % 5] : xa[(t0 / 5) * kImgRow + t0 % 5];
         }
         f32x16 acc = {0.f};
 #pragma unroll
@@ -137,6 +146,13 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   PMARK(3);
+  // ---- P1 / A1 for backward (this block's 10 channels): issued now, they drain under conv2 ----
+  if (t < 360) {
+    const int c0 = ct * 10 * 144;
+    reinterpret_cast<float4*>(P1 + (size_t)b * kP1 + c0)[t] = reinterpret_cast<const float4*>(smem + kL_XS + c0)[t];
+    reinterpret_cast<uint32_t*>(A1 + (size_t)b * kP1 + c0)[t] =
+        reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem + kL_CODE) + c0)[t];
+  }
   // ---- phase 2: conv2 (20->50, 5x5): wave = (co tile of 16, 4x4 pixel tile), K = 500 ----
   const int oh = (pxt >> 1) * 4 + (j >> 2), ow = (pxt & 1) * 4 + (j & 3);
   f32x4 acc = {0.f};
@@ -178,17 +194,6 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
         A2[o] = (uint8_t)code;
       }
     }
-  }
-  // ---- P1 / A1 for backward: this block's 10 channels, from LDS ----
-  if (t < 360) {
-    const int c0 = ct * 10 * 144;
-    reinterpret_cast<float4*>(P1 + (size_t)b * kP1 + c0)[t] = reinterpret_cast<const float4*>(smem + kL_XS + c0)[t];
-    reinterpret_cast<uint32_t*>(A1 + (size_t)b * kP1 + c0)[t] =
-        reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem + kL_CODE) + c0)[t];
-  }
-  if (zero_ptr) {
-    const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
-    for (int i = bid * 512 + t; i < zero_n; i += nb * 512) zero_ptr[i] = 0.f;
   }
   PMARK(5);
 }
