@@ -42,6 +42,22 @@ def _cap(args) -> float:
     return 25.0 if str(args.bucket_mb) == "auto" else float(args.bucket_mb)
 
 
+def _tune(ddp, step, world, args) -> dict:
+    """W > 1 with --bucket-mb auto: time whole steps per bucket cap (max over ranks), keep the fastest.
+    Reports the chosen cap, the per-cap timings and the reduction dtype in the bench JSON."""
+    if world <= 1:
+        return {"bucket_mb": None, "grad_allreduce": "none"}
+    from pytorch_distributed_example_amd.parallel import tune_bucket_cap
+    out = {"grad_reduce_dtype": str(ddp.reduce_dtype or "param dtype").replace("torch.", "")}
+    if str(args.bucket_mb) == "auto":
+        timings, best = tune_bucket_cap(ddp, step)
+        out.update(bucket_mb=best, bucket_sweep_ms_per_step=timings)
+    else:
+        out["bucket_mb"] = float(args.bucket_mb)
+    out["n_buckets"] = len(ddp.buckets)
+    return out
+
+
 def _timed(torch, dist, world, step, warmup, steps):
     for _ in range(warmup):
         step()
@@ -76,14 +92,22 @@ def bench_gpt2(args):
     model = build_gpt2(cfg, seed=args.seed, device=dev)
     ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
     opt = AdamWMaster(model.decay_groups(0.1), lr=6e-4, betas=(0.9, 0.95), max_grad_norm=1.0)
-    g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + rank)
-    data = torch.randint(0, cfg.vocab_size, (8, B, T + 1), device=dev, generator=g)
+    # a pool of 256 sequences per rank of a learnable synthetic language, sharded by the framework's
+    # DistributedSampler (disjoint per rank, reshuffled per pass): no fixed handful of batches to memorise
+    from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_tokens
+    pool = 256 * world
+    sampler = DistributedSampler(range(pool), num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
+    shard = sampler.indices_tensor().long()
+    data = synthetic_tokens(shard, T, cfg.vocab_size, seed=args.seed, device=dev)
     it = [0]
     losses = []
 
     def step():
-        batch = data[it[0] % data.shape[0]]
+        nb = data.shape[0] // B
+        j = it[0] % nb
+        if j == 0 and it[0]:
+            data.copy_(data[torch.randperm(data.shape[0], device=dev)])      # next pass over the shard
+        batch = data[j * B:(j + 1) * B]
         it[0] += 1
         opt.zero_grad()
         loss = ddp(batch[:, :-1], batch[:, 1:])
@@ -91,6 +115,7 @@ def bench_gpt2(args):
         opt.step()
         losses.append(loss.detach())
 
+    extra = _tune(ddp, step, world, args)
     elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
     tokens = args.steps * B * T * world
     tps = tokens / elapsed
@@ -101,10 +126,11 @@ def bench_gpt2(args):
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic uniform tokens, random-init weights",
+            "data": "synthetic learnable token sequences (next = 31*prev+7+U[0,4) mod V; loss floor ln 4), "
+                    "256 per rank sharded by DistributedSampler, random-init weights",
             "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
-                       "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", "bucket_mb": args.bucket_mb},
+                       "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **extra},
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),
             "last_loss": round(float(losses[-1]), 4),
         }), flush=True)

@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import json
 
-from bench_models import _cap, _setup, _timed
+from bench_models import _cap, _setup, _timed, _tune
 
 
 def bench_resnet18(args):
@@ -19,23 +19,25 @@ def bench_resnet18(args):
     model = build_resnet18(seed=args.seed, device=dev)
     ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
     opt = SGDMaster(model.decay_groups(5e-5), lr=0.1, momentum=0.9)
-    g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + rank)
-    xs = torch.randn(2, B, 3, 224, 224, device=dev, generator=g).to(torch.bfloat16)
-    xs = [x.contiguous(memory_format=torch.channels_last) for x in xs]
-    ys = torch.randint(0, 1000, (2, B), device=dev, generator=g)
+    # 8 batches per rank of class-conditional synthetic images, sharded by the DistributedSampler
+    from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_images
+    pool = 8 * B * world
+    sampler = DistributedSampler(range(pool), num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
+    X, Y = synthetic_images(sampler.indices_tensor().long(), seed=args.seed, device=dev)
+    nb = X.shape[0] // B
     it = [0]
     losses = []
 
     def step():
-        i = it[0] % 2
+        i = it[0] % nb
         it[0] += 1
         opt.zero_grad()
-        loss = ops.cross_entropy(ddp(xs[i]).float(), ys[i])
+        loss = ops.cross_entropy(ddp(X[i * B:(i + 1) * B]).float(), Y[i * B:(i + 1) * B])
         loss.backward()
         opt.step()
         losses.append(loss.detach())
 
+    extra = _tune(ddp, step, world, args)
     elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
     ips = args.steps * B * world / elapsed
     if rank == 0:
@@ -44,10 +46,11 @@ def bench_resnet18(args):
             "value": round(ips, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic 3x224x224 N(0,1) images, random labels, random-init weights",
+            "data": "synthetic class-conditional 3x224x224 images (class prototype + noise), 8 batches per rank "
+                    "sharded by DistributedSampler, random-init weights",
             "config": {"model": "ResNet-18 (11.69M params, torchvision layout)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
-                       "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", "bucket_mb": args.bucket_mb,
+                       "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", **extra,
                        "memory_format": "channels_last"},
             "last_loss": round(float(losses[-1]), 4),
         }), flush=True)

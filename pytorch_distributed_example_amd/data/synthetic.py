@@ -62,6 +62,46 @@ def synthetic_mnist(n: int, seed: int = 0, device="cpu", kind: str = "fashion", 
     return TensorDataset(images, labels, name=f"synthetic-{kind}")
 
 
+def synthetic_tokens(indices: torch.Tensor, T: int, vocab: int, seed: int = 0, device="cpu",
+                     branching: int = 4) -> torch.Tensor:
+    """Sequences ``indices`` (global sample ids) of a learnable synthetic language, [len, T+1] int64.
+
+    Sequence i starts at a token drawn from ``seed + i`` and follows next = (31 * prev + 7 + n) % vocab
+    with n uniform in [0, branching): a next-token model can reach ln(branching) nats, so the loss of
+    a benchmark run means something (uniform random tokens would sit at ln(vocab) forever, and a
+    handful of fixed batches is memorised to ~0).  Generated on ``device`` from the global ids, so a
+    DistributedSampler shard regenerates exactly its own samples whatever the world size."""
+    device = torch.device(device)
+    idx = indices.to(device=device, dtype=torch.int64)
+    h = (idx * 2654435761 + seed * 97 + 12345) % 2147483647
+    out = torch.empty(idx.numel(), T + 1, device=device, dtype=torch.int64)
+    out[:, 0] = h % vocab
+    for t in range(T):
+        h = (h * 1103515245 + 12345) % 2147483648
+        out[:, t + 1] = (31 * out[:, t] + 7 + (h >> 16) % branching) % vocab
+    return out
+
+
+def synthetic_images(indices: torch.Tensor, classes: int = 1000, res: int = 224, seed: int = 0, device="cpu",
+                     noise: float = 0.5, dtype=torch.bfloat16, chunk: int = 256):
+    """Class-conditional synthetic images for global sample ids ``indices``: (x [n,3,res,res]
+    channels-last ``dtype``, y [n] int64).  Class c = a hash of the id; the image is the class's fixed
+    8x8 prototype (upsampled) plus N(0, noise) pixel noise seeded by the id chunk -- learnable, unlike
+    pure noise."""
+    device = torch.device(device)
+    idx = indices.to(device=device, dtype=torch.int64)
+    y = (idx * 2654435761 + seed) % classes
+    g = torch.Generator(device=device).manual_seed(seed + 7)
+    proto = torch.randn(classes, 3, 8, 8, device=device, generator=g)
+    x = torch.empty(idx.numel(), 3, res, res, device=device, dtype=dtype).contiguous(memory_format=torch.channels_last)
+    for s in range(0, idx.numel(), chunk):
+        e = min(idx.numel(), s + chunk)
+        gs = torch.Generator(device=device).manual_seed(seed * 1000003 + int(idx[s]))
+        base = torch.nn.functional.interpolate(proto[y[s:e]], size=(res, res), mode="bilinear", align_corners=False)
+        x[s:e] = (base + noise * torch.randn(base.shape, device=device, generator=gs)).to(dtype)
+    return x, y
+
+
 def _read_idx(path):
     op = gzip.open if path.endswith(".gz") else open
     with op(path, "rb") as f:

@@ -7,8 +7,9 @@ Backward: dy' = dy * (y > 0); dres = dy'; dx = BN backward of dy'  -- reduce, fi
           dgamma / dbeta), one streaming apply pass that also emits dres.
 Convolutions with C_in, C_out multiples of 64 and kernels up to 3x3 (every ResNet-18 conv but the
 3-channel stem) are implicit GEMMs on bf16 MFMA (``csrc/kernels/conv.hip``): fprop, phase-split
-dgrad and split-K wgrad.  The stem runs as a library (MIOpen) convolution; CPU tensors use the
-PyTorch reference definitions.
+dgrad and split-K wgrad; the stem has its own MFMA kernels (``csrc/kernels/stem.hip``).  A GPU
+convolution outside both raises (no silent MIOpen fallback); CPU tensors use the PyTorch reference
+definitions.
 """
 from __future__ import annotations
 
@@ -143,9 +144,9 @@ class StemConvFn(torch.autograd.Function):
             return None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if ctx.needs_input_grad[0]:      # the network input never needs it; library dgrad for generality
-            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[0]:      # the network input never needs a gradient
+            raise NotImplementedError("stem conv: no input-gradient kernel (the image input of ResNet-18 "
+                                      "never requires grad)")
         if ctx.needs_input_grad[1]:
             K = kernels()
             part = torch.empty(K.stem_wgrad_blocks(x.shape[0], dy.shape[2]) * 64 * 147, device=x.device,
@@ -189,6 +190,12 @@ def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0, with_stats: bool = False):
             y, part = out
             return y, (part, kernels().conv_stats_blocks(y.shape[0] * y.shape[2] * y.shape[3], w.shape[0]))
         return out
+    if x.is_cuda:
+        # no silent library fallback on the GPU: every ResNet-18 convolution is covered above
+        raise NotImplementedError(
+            f"conv2d_nhwc: no MFMA kernel for x {tuple(x.shape)} {x.dtype}, w {tuple(w.shape)}, stride {stride}, "
+            f"pad {pad} (implicit GEMM needs C_in, C_out multiples of 64, <= 3x3 taps, stride 1/2; the stem "
+            f"kernel covers 3->64 7x7/s2/p3)")
     y = F.conv2d(x, w, None, stride, pad)
     return (y, None) if with_stats else y
 

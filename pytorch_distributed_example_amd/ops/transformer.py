@@ -359,7 +359,11 @@ class LinearFn(torch.autograd.Function):
 
 
 def linear(x, w, b=None):
-    """Projection GEMM (library GEMM on GPU; split-K weight gradients, HIP bias-gradient kernel)."""
-    if x.is_cuda and x.dtype == torch.bfloat16 and w.shape[0] % 8 == 0:
+    """Projection GEMM (split-K weight gradients, HIP bias-gradient kernel).  GPU tensors must be
+    bf16 with out_features % 8 == 0 (every GPT-2 projection): no silent fallback."""
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8 != 0:
+            raise NotImplementedError(f"linear: the GPU path is bf16 with out_features % 8 == 0 "
+                                      f"(got x {x.dtype}, w {tuple(w.shape)} {w.dtype})")
         return LinearFn.apply(x, w, b)
     return F.linear(x, w, b)

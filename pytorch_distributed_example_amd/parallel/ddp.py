@@ -20,7 +20,17 @@ for MI355X:
 
 Bucket sizing for xGMI: the default 25 MB cap gives the 1.7 MB toy CNN one bucket per dtype; for
 large models RCCL rings are per-link bound (~153 GB/s per xGMI link), so a handful of multi-MB
-buckets keeps every collective in its bandwidth regime while leaving overlap room.
+buckets keeps every collective in its bandwidth regime while leaving overlap room.  The cap can be
+changed after construction (``set_bucket_cap``: bucket boundaries only, the flat storage order is
+cap-independent) so a benchmark can time whole steps per cap on the node and keep the fastest
+(``tune_bucket_cap``).
+
+Reduction precision: bf16 parameters have bf16 gradients; ``reduce_dtype=torch.float32`` (the
+default for non-fp32 gradients) all-reduces each bucket through an fp32 staging buffer -- one
+rounding of the exact sum back to the gradient dtype instead of one rounding per ring hop (RCCL sums
+bf16 buckets in bf16 between hops: up to W-1 roundings, inherited by fp32 master weights).  It
+doubles the bytes on the wire; with buckets overlapped with backward that is mostly hidden.
+``reduce_dtype=None`` reduces in the gradient dtype (torch DDP's behaviour).
 """
 from __future__ import annotations
 
@@ -48,7 +58,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: float = 25.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 static_graph: bool = False, init_sync: bool = True):
+                 static_graph: bool = False, init_sync: bool = True, reduce_dtype="auto"):
         super().__init__()
         self.module = module
         if process_group is None and not dist.is_initialized():
@@ -70,20 +80,42 @@ class DistributedDataParallel(nn.Module):
             dist.broadcast_parameters(module, src=self.process_group.ranks[0], group=self.process_group,
                                       buffers=True)
         shapes = [(n, tuple(p.shape)) for n, p in named]
-        elem = named[0][1].element_size()
-        buckets = reverse_order_buckets(shapes, int(bucket_cap_mb * (1 << 20)), elem)
-        self.layout = FlatLayout(shapes, buckets)
+        self._shapes = shapes
+        self._elem = named[0][1].element_size()
+        # the flat storage is laid out in reverse registration order whatever the cap (one bucket):
+        # buckets are then just contiguous ranges of it, re-cut by set_bucket_cap
+        self.layout = FlatLayout(shapes, [[n for n, _ in reversed(shapes)]])
         self.flat_params, self.flat_grads = self.layout.bind(dict(named), dtype=named[0][1].dtype)
         self._params = dict(named)
-        self._bucket_of = {}
-        self.buckets = []
-        for i, names in enumerate(self.layout.bucket_names):
-            a, b = self.layout.bucket_ranges[i]
-            self.buckets.append(_Bucket(i, names, a, b))
-            for n in names:
-                self._bucket_of[n] = i
+        gdt = named[0][1].dtype
+        if reduce_dtype == "auto":
+            reduce_dtype = torch.float32 if gdt in (torch.bfloat16, torch.float16) else None
+        self.reduce_dtype = reduce_dtype if reduce_dtype != gdt else None
+        self._stage = None
+        self.set_bucket_cap(bucket_cap_mb)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(n)) for n, p in named]
         self._callback_queued = False
+
+    def set_bucket_cap(self, bucket_cap_mb: float):
+        """Re-cut the gradient buckets at ``bucket_cap_mb`` (DDP-style greedy packing in reverse
+        registration order).  Only boundaries change; parameters and gradients stay where they are.
+        Must be called identically on every rank, between iterations."""
+        self.bucket_cap_mb = float(bucket_cap_mb)
+        names = reverse_order_buckets(self._shapes, int(self.bucket_cap_mb * (1 << 20)), self._elem)
+        self._bucket_of = {}
+        self.buckets = []
+        for i, bn in enumerate(names):
+            a = self.layout.slots[bn[0]].offset
+            last = self.layout.slots[bn[-1]]
+            b = self.layout.total if i == len(names) - 1 else self.layout.slots[names[i + 1][0]].offset
+            assert b >= last.offset + last.numel
+            self.buckets.append(_Bucket(i, bn, a, b))
+            for n in bn:
+                self._bucket_of[n] = i
+        if self.reduce_dtype is not None and self._stage is None:
+            # one fp32 slot per gradient element: every bucket stages into its own range, so no
+            # bucket's fill can race another bucket's in-flight all-reduce or copy-back
+            self._stage = torch.empty(self.layout.total, device=self.device, dtype=self.reduce_dtype)
 
     # ------------------------------------------------------------------ forward
     def forward(self, *inputs, **kwargs):
@@ -126,7 +158,22 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, bk: _Bucket):
         view = self.flat_grads[bk.start:bk.end]
         with prof.range(f"ddp.bucket{bk.index}.all_reduce"):
-            bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+            if self.reduce_dtype is None:
+                bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+                return
+            # fp32 staging: one rounding of the all-reduced sum back to the gradient dtype
+            st = self._stage[bk.start:bk.end]
+            st.copy_(view)
+            work = dist.all_reduce(st, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+
+            def post(st=st, view=view):
+                view.copy_(st)
+            if work is None:
+                post()
+            else:
+                prev = work._post
+                work._post = (lambda: (prev(), post())) if prev else post
+            bk.work = work
 
     def _finalize(self):
         for bk in self.buckets:
@@ -154,6 +201,40 @@ class DistributedDataParallel(nn.Module):
 
     def bucket_sizes_bytes(self):
         return [(b.end - b.start) * self.flat_grads.element_size() for b in self.buckets]
+
+
+def tune_bucket_cap(ddp: "DistributedDataParallel", step, caps=(4, 8, 16, 25, 50, 64), warmup: int = 1,
+                    iters: int = 3):
+    """Pick the DDP bucket cap by timing WHOLE training steps on this node (the cap that
+    keeps every bucket in the xGMI bandwidth regime while leaving overlap room depends on the model and
+    the link topology, so it is measured, not assumed).  ``step()`` runs one training step.  Per cap:
+    ``warmup`` untimed steps, then ``iters`` timed ones; the MAX over ranks decides, so every rank
+    keeps the same cap.  Returns ({cap_mb: ms per step}, best cap); the DDP is left at the best cap."""
+    import time
+
+    group = ddp.process_group
+    times = []
+    for cap in caps:
+        ddp.set_bucket_cap(cap)
+        for _ in range(warmup):
+            step()
+        if ddp.device.type == "cuda":
+            torch.cuda.synchronize(ddp.device)
+        if group is not None:
+            dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            step()
+        if ddp.device.type == "cuda":
+            torch.cuda.synchronize(ddp.device)
+        times.append((time.perf_counter() - t0) / iters * 1e3)
+    t = torch.tensor(times, dtype=torch.float64)
+    if group is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    res = {float(c): round(float(x), 3) for c, x in zip(caps, t.tolist())}
+    best = min(res, key=res.get)
+    ddp.set_bucket_cap(best)
+    return res, best
 
 
 def average_gradients(model: nn.Module, group=None):

@@ -248,6 +248,37 @@ def case_ddp(backend="gloo", bucket_mb="0.05", steps="4"):
     dist.destroy_process_group()
 
 
+def case_ddp_bf16_reduce(reduce="fp32"):
+    """bf16 gradients averaged over W ranks: fp32 staging (one rounding) vs bf16 reduction, both
+    against the exact fp64 average of the ranks' gradients."""
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    _init("gloo")
+    torch.manual_seed(0)
+    net = torch.nn.Linear(64, 96).to(torch.bfloat16)
+    ddp = DistributedDataParallel(net, bucket_cap_mb=0.004,
+                                  reduce_dtype=torch.float32 if reduce == "fp32" else None)
+    g = torch.Generator().manual_seed(100 + R)
+    x = torch.randn(32, 64, generator=g).to(torch.bfloat16)
+    # every rank's local gradient, gathered to compute the exact average
+    local = {}
+    with ddp.no_sync():
+        ddp(x).float().pow(2).sum().backward()
+        for n, p in net.named_parameters():
+            local[n] = p.grad.detach().double().clone()
+    ddp.zero_grad()
+    ddp(x).float().pow(2).sum().backward()
+    errs = {}
+    for n, p in net.named_parameters():
+        allg = [torch.empty_like(local[n]) for _ in range(W)]
+        dist.all_gather(allg, local[n])
+        exact = torch.stack(allg).mean(0)
+        ulp = exact.abs().clamp_min(1e-30) * 2.0 ** -8          # one bf16 rounding of the exact average
+        errs[n] = float(((p.grad.double() - exact).abs() / ulp).max())
+    emit({"rank": R, "max_err_ulp": max(errs.values()), "n_buckets": len(ddp.buckets)})
+    dist.destroy_process_group()
+
+
 def case_manual_average(backend="gloo", steps="4"):
     """The reference's path: per-parameter all_reduce SUM / W after backward."""
     from pytorch_distributed_example_amd.models import build_net

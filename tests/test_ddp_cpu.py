@@ -37,6 +37,32 @@ def test_ddp_matches_single_process(world, bucket_mb):
         assert res[0]["n_buckets"] > 1
 
 
+def test_ddp_bf16_fp32_staged_reduction():
+    """BF16 DDP gradients all-reduced through fp32 staging are within one bf16 rounding of the
+    exact average (W=4); the bf16 reduction is allowed to be worse (it rounds per reduction step)."""
+    rc, res, logs = run_ranks("ddp_bf16_reduce", 4, "fp32")
+    assert rc == 0, logs
+    assert all(r["max_err_ulp"] <= 1.0 + 1e-6 for r in res), res
+    assert res[0]["n_buckets"] > 1
+    rc, res16, logs = run_ranks("ddp_bf16_reduce", 4, "bf16")
+    assert rc == 0, logs
+    assert max(r["max_err_ulp"] for r in res16) >= max(r["max_err_ulp"] for r in res)
+
+
+def test_ddp_set_bucket_cap_rebuckets_in_place():
+    net = build_net(seed=0)
+    ddp = DistributedDataParallel(net, bucket_cap_mb=25)
+    ptr = ddp.flat_grads.data_ptr()
+    assert len(ddp.buckets) == 1
+    ddp.set_bucket_cap(0.05)
+    assert len(ddp.buckets) > 1 and ddp.flat_grads.data_ptr() == ptr
+    cover = sorted((b.start, b.end) for b in ddp.buckets)
+    assert cover[0][0] == 0 and cover[-1][1] == ddp.layout.total
+    assert all(a[1] == b[0] for a, b in zip(cover, cover[1:]))      # contiguous, no overlap
+    names = [n for b in ddp.buckets for n in b.names]
+    assert names == [n for n, _ in reversed(list(net.named_parameters()))]
+
+
 def test_manual_average_matches_ddp():
     rc, res, logs = run_ranks("manual_average", 2, "gloo", "4")
     assert rc == 0, logs
