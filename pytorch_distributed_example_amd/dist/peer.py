@@ -13,6 +13,9 @@ and then runs a self-test of both algorithms (f32 and bf16, ragged sizes) agains
 answer.  Any failure on any rank (IPC unsupported, wrong sums, a barrier time-out) disables the
 path on every rank and the caller keeps using RCCL.
 
+``PDE_PEER_FORCE_FAIL=<rank>[,<rank>...]`` makes those ranks fail the set-up (failure-path tests:
+every rank must then agree on RCCL only).
+
 ``tune_routes`` times RCCL against the one-/two-shot peer kernels at the sizes an engine will use
 (max over ranks, so every rank takes the same decision) and returns the fastest per size.
 """
@@ -58,6 +61,8 @@ class PeerAllReduce:
         key = f"{group.prefix}/peer_ar/{_SEQ[0]}"
         err = ""
         try:
+            if str(self.rank) in os.environ.get("PDE_PEER_FORCE_FAIL", "").split(","):
+                raise RuntimeError("forced by PDE_PEER_FORCE_FAIL")      # failure-path tests
             self.native = runtime().PeerAllReduce(self.rank, self.world, self.device.index, int(capacity_bytes),
                                                   os.environ.get("PDE_PEER_UNCACHED", "0") == "1")
             self.native.set_timeout_ms(int(timeout_ms))
@@ -176,9 +181,11 @@ def tune_routes(group, peer: Optional[PeerAllReduce], rccl_fn, sizes: Iterable[i
         cands = []
         if rccl_fn is not None:
             cands.append(RCCL)
-        buf = torch.zeros(n, device=device, dtype=dtype)
-        if peer is not None and peer.ok and peer.supports(buf):
-            cands += [ONE_SHOT, TWO_SHOT]
+        buf = None
+        if peer is not None and peer.ok:
+            buf = torch.zeros(n, device=device, dtype=dtype)
+            if peer.supports(buf):
+                cands += [ONE_SHOT, TWO_SHOT]
         if forced in cands:
             out[n] = forced
             continue

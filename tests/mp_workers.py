@@ -558,6 +558,52 @@ def case_torch_backend(device="cpu"):
     tdist.destroy_process_group()
 
 
+def case_bench_peer_fail():
+    """W>1 control flow of bench.py's communication set-up with the xGMI peer path failing on one
+    rank (PDE_PEER_FORCE_FAIL): every rank must disable the peer path, route every bucket through
+    RCCL (a host-backed stand-in here), offer only RCCL-only schedules and report it in the JSON."""
+    import time
+    import types
+
+    import bench
+    from pytorch_distributed_example_amd.engine.lenet import LeNetTrainStep
+
+    t0 = time.time()
+    _init("gloo")
+    g = dist.api._group(None)
+
+    class _HostRccl:                         # the RCCL communicator's query surface, host-backed
+        device = 0
+
+        def comm_count(self):
+            return g.size()
+
+        def cu_device(self):
+            return 0
+
+    g.rccl = _HostRccl()
+    comm = dist.engine_comm()
+    calls = []
+    comm._rccl = lambda t, op=None: calls.append(t.numel())
+    sizes = [25_000, 406_080]
+    routes = comm.enable_peer(sizes, "cuda:0", tune=True)
+    assert comm.peer is None and comm.peer_reason, (comm.peer, comm.peer_reason)
+    assert set(routes.values()) == {"rccl"}, routes
+    fake = types.SimpleNamespace(comm=comm, optimizer="adam", grads=torch.zeros(sum(sizes)),
+                                 bucket_grads=[torch.zeros(sizes[0]), torch.zeros(sizes[1])])
+    cands = LeNetTrainStep.schedule_candidates(fake)
+    assert cands and all(m != "fused" and set(r.values()) == {"rccl"} for m, r in cands), cands
+    fake.comm_on, fake.mode, fake.schedule = True, cands[0][0], cands[0][0]
+    info = bench._comm_info(dist, comm, fake)
+    line = json.dumps({"metric": bench.BASELINE_METRIC, "config": info})
+    back = json.loads(line)["config"]
+    assert back["rccl_world"] == W and back["peer_ok"] is False and back["peer_reason"], back
+    assert set(back["routes"].values()) == {"rccl"}, back
+    g.rccl = None
+    dist.destroy_process_group()
+    emit({"rank": R, "ok": True, "reason": comm.peer_reason, "n_cands": len(cands), "s": time.time() - t0})
+
+
 if __name__ == "__main__":
     name = sys.argv[1]
     globals()["case_" + name](*sys.argv[2:])

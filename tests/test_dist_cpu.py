@@ -93,3 +93,35 @@ def test_torch_distributed_backend_pde(world):
     rc, res, logs = run_ranks("torch_backend", world, "cpu")
     assert rc == 0, "\n".join(logs)
     assert all(r["sums"] == res[0]["sums"] for r in res)
+
+
+def test_bench_w2_forced_peer_failure_degrades_to_rccl():
+    """Verdict r1 item 4: a peer-path failure on one rank leaves every rank on RCCL-only routes and
+    schedules, reported in the bench JSON fields, within a bounded time."""
+    t0 = time.time()
+    rc, res, logs = run_ranks("bench_peer_fail", 2, extra_env={"PDE_PEER_FORCE_FAIL": "1"})
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res), logs
+    assert "forced" in res[1]["reason"] and res[0]["reason"]          # rank 0 learns it from the vote
+    assert time.time() - t0 < 90
+
+
+def test_bench_failure_prints_one_json_line_w2():
+    """bench.py at W=2 where the step cannot run (no GPU here): rank 0 still prints exactly one JSON
+    line (value null + error), every rank exits non-zero, bounded time."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+                        "--steps", "4", "--warmup", "1"], cwd=root, capture_output=True, text=True, timeout=240,
+                       env={**os.environ, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    assert p.returncode != 0
+    assert len(lines) == 1, p.stdout + p.stderr
+    out = json.loads(lines[0])
+    assert out["value"] is None and out["n_gpus"] == 2 and out["error"]
+    assert time.time() - t0 < 240
