@@ -205,6 +205,50 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
             "attn_bwd");
 }
 
+// ---- own GEMM (gemm.hip).  Operand conventions: C[m][n] = sum_k A(m,k) B(k,n) with
+// A(m,k) = A[m*lda+k] (ta=0) or A[k*lda+m] (ta=1), B(k,n) = B[n*ldb+k] (tb=0) or B[k*ldb+n] (tb=1).
+void gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t ta, int64_t tb, int64_t epi,
+          int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t splits, int64_t cfg,
+          const OptT& C2, const OptT& bias, const OptT& aux, const OptT& colsum) {
+  check_cuda(A, "A", BF16, (ta ? K : M - 1) * lda + (ta ? 0 : K));
+  check_cuda(B, "B", BF16, (tb ? K : N - 1) * ldb + (tb ? 0 : K));
+  TORCH_CHECK(ta ? lda >= M : lda >= K, "gemm: lda too small");
+  TORCH_CHECK(tb ? ldb >= N : ldb >= K, "gemm: ldb too small");
+  TORCH_CHECK(ldc >= N, "gemm: ldc too small");
+  const int S = pde_gemm_splits((int)K, (int)splits);
+  if (epi == 3) check_cuda(C, "C", F32, (int64_t)S * M * ldc);
+  else check_cuda(C, "C", BF16, (M - 1) * ldc + N);
+  void* c2 = optr<void>(C2, "C2", BF16, (M - 1) * ldc + N);
+  const void* bp = optr<void>(bias, "bias", BF16, N);
+  const void* xp = optr<void>(aux, "aux", BF16, (M - 1) * ldc + N);
+  float* cs = optr<float>(colsum, "colsum", F32, (int64_t)S * M);
+  TORCH_CHECK(epi != 1 || c2 != nullptr, "gemm: the GELU epilogue needs C2 (activation output)");
+  TORCH_CHECK(epi != 2 || xp != nullptr, "gemm: the GELU-backward epilogue needs aux (pre-activation)");
+  hip_check(pde_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), c2, bp, xp, cs, (int)ta, (int)tb, (int)epi, (int)M,
+                     (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)splits, (int)cfg, cur_stream()),
+            "gemm");
+}
+
+// dw = sum of the S fp32 slabs of part; db = sum of the S bias-gradient partials cs (part / dw may
+// be None: db only)
+void gemm_reduce(const OptT& part, int64_t S, int64_t M, int64_t N, const OptT& dw, const OptT& cs,
+                 const OptT& db) {
+  const float* p = optr<float>(part, "part", F32, S * M * N);
+  void* w = optr<void>(dw, "dw", BF16, M * N);
+  const float* c = optr<float>(cs, "cs", F32, S * M);
+  void* d = optr<void>(db, "db", BF16, M);
+  hip_check(pde_gemm_reduce(p, (int)S, (int)M, (int)N, w, c, d, cur_stream()), "gemm_reduce");
+}
+
+std::vector<int64_t> gemm_tile(int64_t cfg) {
+  int bm = 0, bn = 0;
+  pde_gemm_tile((int)cfg, &bm, &bn);
+  return {bm, bn};
+}
+
+int64_t gemm_splits(int64_t K, int64_t splits) { return pde_gemm_splits((int)K, (int)splits); }
+int64_t gemm_num_cfgs() { return pde_gemm_num_cfgs(); }
+
 }  // namespace
 
 void register_transformer(pybind11::module& m) {
@@ -214,6 +258,15 @@ void register_transformer(pybind11::module& m) {
   m.def("ln_bwd_blocks", &ln_bwd_blocks);
   m.def("ln_bwd", &ln_bwd);
   m.def("sum_slabs_bf16", &sum_slabs_bf16);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("ta"), py::arg("tb"), py::arg("epi"),
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("splits") = 1,
+        py::arg("cfg") = 0, py::arg("C2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("colsum") = py::none());
+  m.def("gemm_reduce", &gemm_reduce, py::arg("part"), py::arg("S"), py::arg("M"), py::arg("N"), py::arg("dw"),
+        py::arg("cs") = py::none(), py::arg("db") = py::none());
+  m.def("gemm_tile", &gemm_tile);
+  m.def("gemm_splits", &gemm_splits);
+  m.def("gemm_num_cfgs", &gemm_num_cfgs);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_bf16", &xent_bf16);

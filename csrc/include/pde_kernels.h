@@ -132,6 +132,16 @@ hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hi
 hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,
                           int C, int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
 
+// ---- bf16 MFMA GEMM with fused epilogues (gemm.hip) ----
+int pde_gemm_num_cfgs();
+void pde_gemm_tile(int cfg, int* bm, int* bn);
+int pde_gemm_splits(int K, int splits);
+hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
+                    int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
+                    hipStream_t st);
+hipError_t pde_gemm_reduce(const float* part, int S, int M, int N, void* dw, const float* cs, void* db,
+                           hipStream_t st);
+
 // ---- attention (attention.hip) ----
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
                         int T, int H, float scale, hipStream_t st);

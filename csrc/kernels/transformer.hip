@@ -6,6 +6,7 @@
 // processed one wave (64 lanes) per row with 8- or 16-byte vector accesses; per-lane columns are
 // fixed (chunk c = lane + 64 j) so LayerNorm's dgamma/dbeta accumulate in registers across rows.
 #include "pde_hip.h"
+#include "pde_act.h"
 #include "pde_bf16.h"
 #include "pde_kernels.h"
 
@@ -224,14 +225,6 @@ __global__ __launch_bounds__(1024) void k_ln_reduce(const float* __restrict__ pa
 }
 
 // ---------------------------------------------------------------------------------- GELU (tanh)
-__device__ __forceinline__ float gelu_t(float x, float* dgelu) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-  if (dgelu) *dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
-  return 0.5f * x * (1.f + t);
-}
-
 __global__ __launch_bounds__(256) void k_gelu_fwd(const uint4* __restrict__ X, uint4* __restrict__ Y, int64_t n8) {
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
     float v[8];

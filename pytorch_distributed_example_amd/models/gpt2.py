@@ -71,7 +71,7 @@ class _MLP(tnn.Module):
         self.c_proj = _Linear(4 * C, C, 0.02 / math.sqrt(2 * cfg.n_layer))
 
     def forward(self, x):
-        return self.c_proj(T.gelu(self.c_fc(x)))
+        return T.mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
 
 
 class Block(tnn.Module):
@@ -125,7 +125,7 @@ class GPT(tnn.Module):
         else:   # last block's residual add fused into ln_f (the summed stream itself is not needed)
             x = T.add_layer_norm_residual(x, delta, t.ln_f.weight, t.ln_f.bias, t.ln_f.eps)[1]
         if targets is None:
-            return torch.matmul(x, t.wte.weight.t())[..., :self.config.vocab_size]
+            return T.lm_logits(x, t.wte.weight, self.config.vocab_size)
         return T.lm_head_loss(x, t.wte.weight, targets, self.config.vocab_size)
 
     def num_params(self, non_embedding: bool = False):

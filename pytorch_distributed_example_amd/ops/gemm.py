@@ -1,0 +1,151 @@
+"""The framework's own bf16 MFMA GEMM (``csrc/kernels/gemm.hip``) for the GPT-2 projections and the
+tied LM head -- the reference's ``nn.Linear`` op class (/root/reference/mnist/main.py:136-137) at
+GPT-2 shapes, with the epilogues a library GEMM cannot fuse:
+
+* ``fprop(x, w, bias, gelu)``   y = x w^T + b; with ``gelu`` the kernel writes the pre-activation
+                                AND gelu(pre) (the next projection's input) in one pass.
+* ``dgrad(dy, w, pre)``         dx = dy w; with ``pre`` the GELU backward is applied in the
+                                epilogue (dx = (dy w) * gelu'(pre)).
+* ``wgrad(dy, x, dw, db)``      dw = dy^T x (split-K over tokens, fp32 slabs, one reduction kernel
+                                that also folds the bias gradient db = sum_tokens dy, computed by
+                                the GEMM's own MFMAs against a ones fragment).
+
+All operands stay in their natural row-major layouts (the kernel reads transposed operands with
+``ds_read_b64_tr_b16``); GPU-only, bf16 in / bf16 out, fp32 accumulation.
+
+Tile configurations (``gemm_tile(cfg)``): 0 = 256x192, 1 = 256x128, 2 = 128x128, 3 = 256x256.
+``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
+``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .._ext import kernels
+
+EPI_BF16, EPI_GELU, EPI_GELU_BWD, EPI_SLAB = 0, 1, 2, 3
+N_CU = 256
+_TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256)}
+# relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
+_TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0}
+
+# GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/):
+#   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
+#   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
+_CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
+    ("fprop", 2304, 768): (0, 1), ("fprop", 768, 768): (3, 1), ("fprop", 3072, 768): (3, 1),
+    ("fprop", 768, 3072): (0, 1), ("fprop", 50304, 768): (3, 1),
+    ("dgrad", 768, 2304): (0, 1), ("dgrad", 768, 768): (0, 1), ("dgrad", 768, 3072): (0, 1),
+    ("dgrad", 3072, 768): (3, 1), ("dgrad", 768, 50304): (0, 1),
+    ("wgrad", 2304, 768): (3, 8), ("wgrad", 768, 768): (0, 16), ("wgrad", 3072, 768): (0, 4),
+    ("wgrad", 768, 3072): (0, 4), ("wgrad", 50304, 768): (3, 1),
+}
+
+_SCRATCH: Dict[Tuple, torch.Tensor] = {}
+
+
+def _scratch(device, n: int, tag: str) -> torch.Tensor:
+    key = (device, tag)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1), device=device, dtype=torch.float32)
+        _SCRATCH[key] = t
+    return t[:n]
+
+
+def pick(kind: str, M: int, N: int, K: int) -> Tuple[int, int]:
+    """(cfg, splits) for a GEMM: the measured table, else the config whose last wave of tiles
+    wastes the least of the chip (tiles / (rounds * CUs) x tile efficiency); wgrad also picks a
+    split-K factor that brings the tile count to >= 1 round with >= 1024-deep slices."""
+    if kind == "wgrad":
+        hit = _CFG.get((kind, M, N))
+        if hit is not None and K >= 2048:
+            return hit[0], max(1, min(hit[1], round(hit[1] * K / 16384)))
+    else:
+        hit = _CFG.get((kind, N, K))
+        if hit is not None and M >= 4096:
+            return hit
+    best, best_s = None, -1.0
+    for cfg, (bm, bn) in _TILES.items():
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        splits = 1
+        if kind == "wgrad":
+            while tiles * splits < N_CU and K // (64 * splits * 2) >= 16:
+                splits *= 2
+        tot = tiles * splits
+        rounds = math.ceil(tot / N_CU)
+        score = tot / (rounds * N_CU) * _TILE_EFF[cfg]
+        if kind == "wgrad" and splits > 1:
+            score *= 0.97                                # slab round trip + reduction
+        if score > best_s + 1e-9:
+            best, best_s = (cfg, splits), score
+    return best
+
+
+def _chk(t: torch.Tensor, name: str):
+    if not (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()):
+        raise ValueError(f"gemm: {name} must be a contiguous bf16 GPU tensor")
+
+
+def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
+          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+    """x2 [M, K] . w[N, K]^T (+ bias) -> y [M, N]; with ``gelu`` returns (pre, act)."""
+    _chk(x2, "x")
+    _chk(w, "w")
+    M, K = x2.shape
+    N = w.shape[0]
+    c = pick("fprop", M, N, K)[0] if cfg is None else cfg
+    y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16) if out is None else out
+    if gelu:
+        act = torch.empty_like(y)
+        kernels().gemm(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=act, bias=bias)
+        return y, act
+    kernels().gemm(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c, bias=bias)
+    return y
+
+
+def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+    """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``pre`` ([M, K]) returns dx * gelu'(pre)."""
+    _chk(dy2, "dy")
+    _chk(w, "w")
+    M, Nk = dy2.shape                  # reduction over the weight's rows
+    Kout = w.shape[1]
+    c = pick("dgrad", M, Kout, Nk)[0] if cfg is None else cfg
+    dx = torch.empty(M, Kout, device=dy2.device, dtype=torch.bfloat16)
+    if pre is not None:
+        kernels().gemm(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=pre)
+    else:
+        kernels().gemm(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c)
+    return dx
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, dw: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None,
+          want_db: bool = False, cfg: Optional[int] = None, splits: Optional[int] = None):
+    """dw [N, K] = dy2[T, N]^T . x2[T, K] (into ``dw`` when given); with ``want_db`` (or ``db``) also
+    db [N] = column sums of dy2.  Returns (dw, db or None)."""
+    _chk(dy2, "dy")
+    _chk(x2, "x")
+    T, N = dy2.shape
+    K = x2.shape[1]
+    c0, s0 = pick("wgrad", N, K, T)
+    c = c0 if cfg is None else cfg
+    S = kernels().gemm_splits(T, s0 if splits is None else splits)
+    if dw is None:
+        dw = torch.empty(N, K, device=dy2.device, dtype=torch.bfloat16)
+    want_db = want_db or db is not None
+    if want_db and db is None:
+        db = torch.empty(N, device=dy2.device, dtype=torch.bfloat16)
+    cs = _scratch(dy2.device, S * N, "cs") if want_db else None
+    if S == 1:
+        kernels().gemm(dy2, x2, dw, 1, 1, EPI_BF16, N, K, T, N, K, K, 1, c, colsum=cs)
+        if want_db:
+            kernels().gemm_reduce(None, 1, N, K, None, cs, db)     # db only
+        return dw, db
+    part = _scratch(dy2.device, S * N * K, "slab")
+    kernels().gemm(dy2, x2, part, 1, 1, EPI_SLAB, N, K, T, N, K, K, S, c, colsum=cs)
+    kernels().gemm_reduce(part, S, N, K, dw, cs, db)
+    return dw, db
+

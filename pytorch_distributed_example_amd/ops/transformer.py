@@ -4,10 +4,12 @@ GPU tensors always run the framework kernels (no silent fallback: a missing exte
 CPU tensors run the plain PyTorch definition of the same op -- used by the CPU test-suite to check
 model plumbing, and as the fp32 numerics reference of the GPU tests.
 
-Plain GEMMs (the c_attn / c_proj / c_fc projections and the tied LM head) are library GEMMs
-(``torch.matmul`` -> hipBLASLt on ROCm); everything around them is ours: LayerNorm, GELU, causal
-flash attention, the fused vocab softmax-cross-entropy that overwrites logits with dlogits in place
-(so the [N, 50304] logits tensor is written once and never re-materialised), and embeddings.
+Every GEMM is the framework's own bf16 MFMA GEMM (``ops/gemm.py`` over ``csrc/kernels/gemm.hip``):
+the c_attn / c_proj projections (bias in the epilogue, bias gradient from the wgrad GEMM's own
+MFMAs), the MLP as ONE op (c_fc with bias + GELU in its epilogue, c_proj's dgrad with the GELU
+backward in its epilogue), and the tied LM head.  Around them: LayerNorm, causal flash attention,
+the fused vocab softmax-cross-entropy that overwrites logits with dlogits in place (so the
+[N, 50304] logits tensor is written once and never re-materialised), and embeddings.
 """
 from __future__ import annotations
 
@@ -18,6 +20,7 @@ import torch.nn.functional as F
 
 from .._ext import kernels
 from ..parallel.flat import flat_grad_slot
+from . import gemm as G
 
 _BF16 = torch.bfloat16
 
@@ -267,7 +270,7 @@ class LMHeadLossFn(torch.autograd.Function):
         C = h.shape[-1]
         h2 = _c(h.reshape(-1, C))
         N = h2.shape[0]
-        logits = torch.matmul(h2, w.t())                    # [N, Vp] bf16 (hipBLASLt)
+        logits = G.fprop(h2, w)                             # [N, Vp] bf16 (own MFMA GEMM)
         rows = torch.empty(N, device=h.device, dtype=torch.float32)
         tg = _c(targets.reshape(-1).long())
         kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
@@ -282,9 +285,10 @@ class LMHeadLossFn(torch.autograd.Function):
         h2, w, dlogits = ctx.saved_tensors
         if not (isinstance(g, torch.Tensor) and g.numel() == 1):
             raise RuntimeError("LM head loss expects a scalar gradient")
-        dl = dlogits if float(g) == 1.0 else dlogits * g.to(dlogits.dtype)
-        dh = torch.matmul(dl, w)                             # [N, C]
-        dw = torch.matmul(dl.t(), h2)                        # [Vp, C]
+        if float(g) != 1.0:
+            dlogits.mul_(g.to(dlogits.dtype))
+        dh = G.dgrad(dlogits, w)                             # [N, C]
+        dw, _ = G.wgrad(dlogits, h2)                         # [Vp, C]
         return dh.reshape(ctx.hshape), dw, None, None
 
 
@@ -295,75 +299,96 @@ def lm_head_loss(h, w, targets, V: int):
     return F.cross_entropy(logits.reshape(-1, V), targets.reshape(-1))
 
 
-def _splitk(N: int, out: int, fin: int) -> int:
-    """Split-K factor of the weight-gradient GEMM dW[out, in] = dY^T X (K = tokens).
-
-    With K = 16k tokens and out*in <= a few M the library GEMM has fewer output tiles than the chip
-    has CUs; splitting K into S batched GEMMs (+ one small reduction) fills all 256 CUs.  Factors
-    measured on MI355X for GPT-2 small (tools/gemm_bench.py -> profiles/gemm_bench_gpt2.jsonl):
-    768x2304 / 768x768 best at 8, 768x3072 / 3072x768 at 4, the LM head (38.6M outputs) at 1."""
-    if out * fin >= 16 << 20:
-        return 1
-    S = 8 if out * fin <= 2 << 20 else 4
-    while S > 1 and (N % S or N // S < 512):
-        S //= 2
-    return S
+def lm_logits(h, w, V: int):
+    """Inference logits h @ w^T over the first V (real) vocabulary columns."""
+    if _gpu(h):
+        C = h.shape[-1]
+        return G.fprop(_c(h.reshape(-1, C)), w).view(*h.shape[:-1], w.shape[0])[..., :V]
+    return torch.matmul(h, w.t())[..., :V]
 
 
-def _wgrad(dy2, x2, dst=None):
-    """dW = dy2^T x2 (into ``dst`` -- the weight's flat gradient slot -- when given).  Split-K
-    partials are fp32 (``bmm(..., out_dtype=float32)``) and summed by one HIP pass straight into the
-    bf16 result (no bf16 rounding of partial sums, no extra reduction kernel)."""
-    N, out = dy2.shape
-    fin = x2.shape[1]
-    S = _splitk(N, out, fin)
-    if dst is None:
-        dst = torch.empty(out, fin, device=dy2.device, dtype=dy2.dtype)
-    if S == 1:
-        return torch.matmul(dy2.t(), x2, out=dst)
-    part = torch.bmm(dy2.view(S, N // S, out).transpose(1, 2), x2.view(S, N // S, fin), out_dtype=torch.float32)
-    kernels().sum_slabs_bf16(part, dst)
-    return dst
+def _grad_out(p):
+    slot = flat_grad_slot(p)
+    return slot if slot is not None and slot.is_contiguous() else None
 
 
 class LinearFn(torch.autograd.Function):
-    """y = x W^T + b on bf16: forward = library GEMM with the bias in its epilogue; backward =
-    dgrad GEMM, split-K wgrad GEMM, and the framework's column-sum kernel for the bias gradient."""
+    """y = x W^T + b on bf16 through the own GEMM: forward with the bias in its epilogue; backward =
+    dgrad GEMM + split-K wgrad GEMM whose extra ones-MFMA also yields the bias gradient (written
+    straight into the flat gradient slots when the parameters have them)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        fin = w.shape[1]
+        x2 = _c(x.reshape(-1, fin))
+        ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.bias = b
-        return F.linear(x, w, b)
+        ctx.xshape = x.shape
+        return G.fprop(x2, w, b).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        out, fin = w.shape
+        x2, w = ctx.saved_tensors
+        out = w.shape[0]
         dy2 = _c(dy.reshape(-1, out))
-        x2 = _c(x.reshape(-1, fin))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy2, w).view(x.shape)
-        if ctx.needs_input_grad[1]:
-            slot = flat_grad_slot(w)
-            dw = _wgrad(dy2, x2, slot if slot is not None and slot.is_contiguous() else None)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            K = kernels()
-            part = torch.empty(K.colsum_bf16_splits(out) * out, device=dy.device, dtype=torch.float32)
-            db = flat_grad_slot(ctx.bias)
-            db = torch.empty(out, device=dy.device, dtype=dy.dtype) if db is None else db
-            K.colsum_bf16(dy2, part, db)
+            dx = G.dgrad(dy2, w).view(ctx.xshape)
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_db:
+            dw, db = G.wgrad(dy2, x2, dw=_grad_out(w), db=_grad_out(ctx.bias) if want_db else None,
+                             want_db=want_db)
+            if not ctx.needs_input_grad[1]:
+                dw = None
         return dx, dw, db
 
 
-def linear(x, w, b=None):
-    """Projection GEMM (split-K weight gradients, HIP bias-gradient kernel).  GPU tensors must be
-    bf16 with out_features % 8 == 0 (every GPT-2 projection): no silent fallback."""
+class MLPFn(torch.autograd.Function):
+    """GPT-2 MLP  y = c_proj(gelu(c_fc(x)))  as two GEMMs with fused epilogues: c_fc writes the
+    pre-activation and gelu(pre) in one pass; backward runs c_proj's dgrad with the GELU backward in
+    its epilogue (no separate GELU kernels), and both wgrads with their bias gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
+        C = x.shape[-1]
+        x2 = _c(x.reshape(-1, C))
+        pre, act = G.fprop(x2, w_fc, b_fc, gelu=True)
+        y = G.fprop(act, w_proj, b_proj)
+        ctx.save_for_backward(x2, w_fc, w_proj, pre, act)
+        ctx.biases = (b_fc, b_proj)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w_proj.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w_fc, w_proj, pre, act = ctx.saved_tensors
+        b_fc, b_proj = ctx.biases
+        dy2 = _c(dy.reshape(-1, w_proj.shape[0]))
+        dw_proj, db_proj = G.wgrad(dy2, act, dw=_grad_out(w_proj), db=_grad_out(b_proj), want_db=True)
+        dpre = G.dgrad(dy2, w_proj, pre=pre)                 # (dy W_proj) * gelu'(pre)
+        dw_fc, db_fc = G.wgrad(dpre, x2, dw=_grad_out(w_fc), db=_grad_out(b_fc), want_db=True)
+        dx = G.dgrad(dpre, w_fc).view(ctx.xshape)
+        return dx, dw_fc, db_fc, dw_proj, db_proj
+
+
+def mlp(x, w_fc, b_fc, w_proj, b_proj):
+    """GPT-2 MLP block  c_proj(gelu_tanh(c_fc(x))).  GPU: two own GEMMs with fused GELU epilogues."""
     if x.is_cuda:
-        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8 != 0:
-            raise NotImplementedError(f"linear: the GPU path is bf16 with out_features % 8 == 0 "
-                                      f"(got x {x.dtype}, w {tuple(w.shape)} {w.dtype})")
+        for t in (x, w_fc, b_fc, w_proj, b_proj):
+            if t.dtype != torch.bfloat16:
+                raise NotImplementedError("mlp: the GPU path is bf16")
+        return MLPFn.apply(x, w_fc, b_fc, w_proj, b_proj)
+    return F.linear(F.gelu(F.linear(x, w_fc, b_fc), approximate="tanh"), w_proj, b_proj)
+
+
+def linear(x, w, b=None):
+    """Projection GEMM (own MFMA GEMM, split-K weight gradients, fused bias gradient).  GPU tensors
+    must be bf16 with out_features % 8 == 0 and in_features % 64 == 0 (every GPT-2 projection): no
+    silent fallback."""
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8 or w.shape[1] % 64:
+            raise NotImplementedError(f"linear: the GPU path is bf16 with out_features % 8 == 0 and "
+                                      f"in_features % 64 == 0 (got x {x.dtype}, w {tuple(w.shape)} {w.dtype})")
         return LinearFn.apply(x, w, b)
     return F.linear(x, w, b)

@@ -1,0 +1,124 @@
+"""Own bf16 MFMA GEMM (csrc/kernels/gemm.hip) vs plain PyTorch fp32 references: every tile
+configuration, ragged M / N tiles, split-K with the fused bias gradient, and the fused bias /
+GELU / GELU-backward epilogues, at small shapes and at the GPT-2 projection shapes."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_example_amd._ext import kernels
+from pytorch_distributed_example_amd.ops import gemm as G
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+CFGS = [0, 1, 2, 3]
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev, torch.bfloat16)
+
+
+def test_tiles_and_cfgs():
+    K = kernels()
+    assert K.gemm_num_cfgs() == 4
+    assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256)]
+    assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("M,N,K", [(300, 200, 192), (64, 8, 64), (513, 776, 320)])
+def test_fprop_bias(cfg, M, N, K):
+    x, w, b = _bf(M, K, seed=1), _bf(N, K, scale=0.05, seed=2), _bf(N, seed=3)
+    y = G.fprop(x, w, b, cfg=cfg)
+    ref = F.linear(x.float(), w.float(), b.float())
+    assert y.shape == (M, N)
+    assert rel_err(y, ref) < 1e-2
+    y0 = G.fprop(x, w, None, cfg=cfg)
+    assert rel_err(y0, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+def test_fprop_gelu(cfg):
+    M, N, K = 520, 392, 256
+    x, w, b = _bf(M, K, seed=4), _bf(N, K, scale=0.06, seed=5), _bf(N, scale=0.5, seed=6)
+    pre, act = G.fprop(x, w, b, gelu=True, cfg=cfg)
+    rp = F.linear(x.float(), w.float(), b.float())
+    assert rel_err(pre, rp) < 1e-2
+    # act is gelu of the bf16-rounded pre-activation (the module's semantics)
+    assert rel_err(act, F.gelu(pre.float(), approximate="tanh")) < 1e-2
+    assert rel_err(act, F.gelu(rp, approximate="tanh")) < 2e-2
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("M,N,K", [(300, 200, 192), (257, 392, 128)])
+def test_dgrad(cfg, M, N, K):
+    # dx [M, N] = dy [M, K] . w [K, N]  (w is the nn.Linear weight [out=K][in=N])
+    dy, w = _bf(M, K, seed=7), _bf(K, N, scale=0.05, seed=8)
+    dx = G.dgrad(dy, w, cfg=cfg)
+    assert rel_err(dx, dy.float() @ w.float()) < 1e-2
+    pre = _bf(M, N, seed=9)
+    dxg = G.dgrad(dy, w, pre=pre, cfg=cfg)
+    pr = pre.float().requires_grad_()
+    F.gelu(pr, approximate="tanh").backward(dx.float())
+    assert rel_err(dxg, pr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("splits", [1, 3, 8])
+def test_wgrad_split_bias(cfg, splits):
+    T, N, K = 1024, 392, 200
+    dy, x = _bf(T, N, seed=10), _bf(T, K, seed=11)
+    dw, db = G.wgrad(dy, x, want_db=True, cfg=cfg, splits=splits)
+    assert rel_err(dw, dy.float().t() @ x.float()) < 1e-2
+    assert rel_err(db, dy.float().sum(0)) < 1e-2
+    dw2, db2 = G.wgrad(dy, x, cfg=cfg, splits=splits)
+    assert db2 is None and torch.equal(dw, dw2)
+
+
+@pytest.mark.parametrize("kind,M,N,K", [
+    ("fprop", 4096, 2304, 768), ("fprop", 4096, 768, 3072), ("dgrad", 4096, 768, 3072),
+    ("wgrad", 3072, 768, 4096), ("fprop", 2048, 50304, 768), ("dgrad", 2048, 768, 50304),
+    ("wgrad", 50304, 768, 2048)])
+def test_gpt2_shapes(kind, M, N, K):
+    """GPT-2 projection / LM-head shapes (tokens reduced to 2-4k to keep the fp32 reference cheap)."""
+    if kind == "fprop":
+        x, w, b = _bf(M, K, seed=12), _bf(N, K, scale=0.03, seed=13), _bf(N, seed=14)
+        out, ref = G.fprop(x, w, b), F.linear(x.float(), w.float(), b.float())
+    elif kind == "dgrad":
+        dy, w = _bf(M, K, seed=15), _bf(K, N, scale=0.03, seed=16)
+        out, ref = G.dgrad(dy, w), dy.float() @ w.float()
+    else:
+        dy, x = _bf(K, M, scale=0.1, seed=17), _bf(K, N, seed=18)
+        out, _ = G.wgrad(dy, x)
+        ref = dy.float().t() @ x.float()
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_wgrad_into_slot_and_strided_reuse():
+    """wgrad writes into a given (flat-buffer) slot; scratch slabs are reused across shapes."""
+    flat = torch.zeros(392 * 200 + 64, device=dev, dtype=torch.bfloat16)
+    slot = flat[64:].view(392, 200)
+    dy, x = _bf(2048, 392, seed=19), _bf(2048, 200, seed=20)
+    G.wgrad(dy, x, dw=slot)
+    assert rel_err(slot, dy.float().t() @ x.float()) < 1e-2
+    assert torch.count_nonzero(flat[:64]) == 0
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+def test_k_tail(cfg):
+    """K % 64 != 0: K-contiguous operands mask the chunks past K, transposed ones end at row K (wgrad
+    over a token count that is not even a multiple of 8)."""
+    x, w, b = _bf(300, 200, seed=21), _bf(392, 200, scale=0.05, seed=22), _bf(392, seed=23)
+    assert rel_err(G.fprop(x, w, b, cfg=cfg), F.linear(x.float(), w.float(), b.float())) < 1e-2
+    dy, w2 = _bf(300, 1000, seed=24), _bf(1000, 392, scale=0.05, seed=25)
+    assert rel_err(G.dgrad(dy, w2, cfg=cfg), dy.float() @ w2.float()) < 1e-2
+    for T in (37, 300):
+        dy3, x3 = _bf(T, 392, seed=26), _bf(T, 200, seed=27)
+        dw, db = G.wgrad(dy3, x3, want_db=True, cfg=cfg, splits=2)
+        assert rel_err(dw, dy3.float().t() @ x3.float()) < 1e-2
+        assert rel_err(db, dy3.float().sum(0)) < 1e-2

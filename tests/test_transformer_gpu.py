@@ -197,7 +197,7 @@ def test_gpt2_trains():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
-@pytest.mark.parametrize("N,fin,fout", [(16384, 768, 2304), (4096, 3072, 768), (300, 64, 1000), (64, 40, 24)])
+@pytest.mark.parametrize("N,fin,fout", [(16384, 768, 2304), (4096, 3072, 768), (300, 64, 1000), (37, 128, 24)])
 def test_linear_splitk_and_bias_grad(N, fin, fout):
     torch.manual_seed(10)
     x = torch.randn(N, fin).to(dev, torch.bfloat16).requires_grad_()
@@ -213,6 +213,35 @@ def test_linear_splitk_and_bias_grad(N, fin, fout):
     assert rel_err(x.grad, xr.grad) < 2e-2
     assert rel_err(w.grad, wr.grad) < 2e-2
     assert rel_err(b.grad, br.grad) < 2e-2
+
+
+def test_linear_rejects_unsupported_shapes():
+    """No silent library fallback: in_features % 64 != 0 raises on GPU."""
+    x = torch.randn(8, 40, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(24, 40, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(NotImplementedError):
+        T.linear(x, w, None)
+
+
+def test_mlp_fused_matches_fp32():
+    """MLP as one op (c_fc + bias + GELU epilogue, GELU backward in c_proj's dgrad epilogue)."""
+    torch.manual_seed(11)
+    N, C = 1000, 256
+    x = torch.randn(N, C).to(dev, torch.bfloat16).requires_grad_()
+    ps = [(torch.randn(4 * C, C) / C ** 0.5), 0.1 * torch.randn(4 * C), (torch.randn(C, 4 * C) / (4 * C) ** 0.5),
+          0.1 * torch.randn(C)]
+    ps = [p.to(dev, torch.bfloat16).requires_grad_() for p in ps]
+    y = T.mlp(x, *ps)
+    g = torch.randn(N, C).to(dev, torch.bfloat16)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    pr = [p.detach().float().requires_grad_() for p in ps]
+    yr = F.linear(F.gelu(F.linear(xr, pr[0], pr[1]), approximate="tanh"), pr[2], pr[3])
+    yr.backward(g.float())
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(x.grad, xr.grad) < 3e-2
+    for p, q in zip(ps, pr):
+        assert rel_err(p.grad, q.grad) < 3e-2
 
 
 def test_layer_norm_residual_fused_grad():
