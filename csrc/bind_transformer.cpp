@@ -267,6 +267,7 @@ void register_transformer(pybind11::module& m) {
   m.def("gemm_tile", &gemm_tile);
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_num_cfgs", &gemm_num_cfgs);
+  m.def("gemm_set_dbg", [](int64_t d) { pde_gemm_set_dbg((int)d); });
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("xent_bf16", &xent_bf16);

@@ -136,6 +136,7 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
 int pde_gemm_num_cfgs();
 void pde_gemm_tile(int cfg, int* bm, int* bn);
 int pde_gemm_splits(int K, int splits);
+void pde_gemm_set_dbg(int d);
 hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
                     int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
                     hipStream_t st);

@@ -58,6 +58,7 @@ struct GemmArgs {
   uint32_t a_bytes, b_bytes;
   int M, N, K, lda, ldb, ldc;
   int mtiles, ntiles, kper;
+  int dbg;               // ablation (v1 loop, wrong results): 1 no DMA, 2 no waits/barriers, 4 no LDS reads
 };
 
 // Transposed-read lane bases delivering the STANDARD k order (element j of a lane in half h is
@@ -93,8 +94,107 @@ __device__ __forceinline__ uint2 row_lane_off(int r0) {
   return make_uint2(toff(row, h), toff(row, 2 + h));
 }
 
-template <int TM, int TN, int WM, int WN, int NST, bool TA, bool TB, int EPI, bool CS>
-__global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm(GemmArgs a) {
+// Shared epilogue of the GEMM kernels (called after the K loop, stage buffers free).
+//   Lane (lr, lh) of accumulator (i, j) holds C[row wm*WTM + 32i + lr][col wn*WTN + 32j + 8g + 4lh + e]
+//   in register 4g + e (the MFMAs run with swapped operands).
+template <int TM, int TN, int WM, int WN, int EPI, bool CS>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[TM][TN], f32x16* accb, char* smem,
+                                              int m0, int n0, int split, bool cs_on) {
+  constexpr int NT = 64 * WM * WN, WTM = TM * 32, WTN = TN * 32, BM = WM * WTM, BN = WN * WTN;
+  constexpr int RS = BN * 2 + 16;
+  constexpr int TILE_BYTES = EPI == kSlab ? 0 : BM * RS;
+  const int t = threadIdx.x, l = t & 63, lr = l & 31, lh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), wm = w / WN, wn = w % WN;
+  if constexpr (EPI == kSlab) {
+    float* out = reinterpret_cast<float*>(a.C) + (size_t)split * a.M * a.ldc;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + 32 * i + lr;
+      if (m < a.M) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * WTN + 32 * j + 8 * g + 4 * lh;
+            if (n < a.N)
+              *reinterpret_cast<float4*>(out + (size_t)m * a.ldc + n) =
+                  make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+          }
+      }
+    }
+  } else {
+    const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = wn * WTN + 32 * j + 8 * g + 4 * lh;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ml = wm * WTM + 32 * i + lr;
+          const float v[4] = {acc[i][j][4 * g] + bv[0], acc[i][j][4 * g + 1] + bv[1], acc[i][j][4 * g + 2] + bv[2],
+                              acc[i][j][4 * g + 3] + bv[3]};
+          *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+        }
+      }
+  }
+  if constexpr (CS) {
+    if (cs_on && lh == 0) {
+      float* csl = reinterpret_cast<float*>(smem + TILE_BYTES);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) csl[wn * BM + wm * WTM + 32 * i + lr] = accb[i][0];
+    }
+  }
+  if constexpr (EPI != kSlab || CS) __syncthreads();
+  if constexpr (CS) {
+    if (cs_on && t < BM && m0 + t < a.M) {
+      const float* csl = reinterpret_cast<const float*>(smem + TILE_BYTES);
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < WN; ++q) s += csl[q * BM + t];
+      a.colsum[(size_t)split * a.M + m0 + t] = s;
+    }
+  }
+  if constexpr (EPI != kSlab) {
+    constexpr int CPR = BN / 8;                        // 16-byte chunks per tile row
+    bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
+#pragma unroll 4
+    for (int c = t; c < BM * CPR; c += NT) {
+      const int row = c / CPR, cc = c - row * CPR;
+      const int m = m0 + row, n = n0 + 8 * cc;
+      if (m < a.M && n < a.N) {
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+        const size_t o = (size_t)m * a.ldc + n;
+        if constexpr (EPI == kBf16) {
+          *reinterpret_cast<uint4*>(C + o) = v;
+        } else if constexpr (EPI == kGelu) {
+          *reinterpret_cast<uint4*>(C + o) = v;
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = gelu_t(f[e], nullptr);
+          *reinterpret_cast<uint4*>(a.C2 + o) = pack8(f);
+        } else {                                       // kGeluBwd: dX = bf16(acc) * gelu'(pre)
+          float f[8], p[8];
+          unpack8(v, f);
+          unpack8(*reinterpret_cast<const uint4*>(a.aux + o), p);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float d;
+            gelu_t(p[e], &d);
+            f[e] *= d;
+          }
+          *reinterpret_cast<uint4*>(C + o) = pack8(f);
+        }
+      }
+    }
+  }
+}
+
+template <int TM, int TN, int WM, int WN, int NST, int OCC, int SPREAD, bool TA, bool TB, int EPI, bool CS>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm(GemmArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int WTM = TM * 32, WTN = TN * 32, BM = WM * WTM, BN = WN * WTN;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
@@ -195,24 +295,49 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm(GemmArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3f80;
 
+  // one LDS-DMA piece (1 KB wave-instruction) of stage kt into buffer buf: pieces 0..AG-1 are A's,
+  // AG..LPS-1 are B's
+  auto issue_piece = [&](auto P_, int kt, int buf) {
+    constexpr int P = decltype(P_)::value;
+    const char* As = smem + buf * STAGE;
+    const int kb = kbeg + kt * 64;
+    if constexpr (P < AG) {
+      glds16(ar, As + (NW * P + w) * 1024, (TA || kb + ach[P] < a.K) ? aoff[P] + (uint32_t)kt * astep : kOOB);
+    } else {
+      constexpr int V = P - AG;
+      glds16(br, As + ABYTES + (NW * V + w) * 1024,
+             (TB || kb + bch[V] < a.K) ? boff[V] + (uint32_t)kt * bstep : kOOB);
+    }
+  };
+
   if (KT > 0) {
+    const bool no_dma = a.dbg & 1, no_sync = a.dbg & 2, no_lds = a.dbg & 4;
 #pragma unroll
     for (int s = 0; s < NST - 1; ++s)
-      if (s < KT) issue(s, s);
+      if (s < KT && !no_dma) issue(s, s);
     int buf = 0;
+    bf16x8 fa[2][TM], fb[2][TN];
+    if (no_lds) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[0][i] = fa[1][i] = ones;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[0][j] = fb[1][j] = ones;
+    }
     for (int kt = 0; kt < KT; ++kt) {
-      if constexpr (NST >= 3) {
-        if (kt + 1 < KT) wait_vm<LPS>();
-        else wait_vm<0>();
-      } else {
-        wait_vm<0>();
+      if (!no_sync) {
+        if constexpr (NST >= 3) {
+          if (kt + 1 < KT) wait_vm<LPS>();
+          else wait_vm<0>();
+        } else {
+          wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
       }
-      __builtin_amdgcn_s_barrier();
-      if (kt + NST - 1 < KT) {
-        int nb = buf + NST - 1;
-        nb = nb >= NST ? nb - NST : nb;
-        issue(kt + NST - 1, nb);
-      }
+      // the next stage's DMA pieces are spread over the first SPREAD k-steps, between the fragment
+      // reads and the MFMAs (a burst of LDS-DMA issues right after the barrier starves the MFMA pipe)
+      const bool do_issue = kt + NST - 1 < KT && !no_dma;
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
       const uint32_t sa = lds0 + buf * STAGE, sb = sa + ABYTES;
       uint2 ab[TA ? TM : 1], bb[TB ? TN : 1];
 #pragma unroll
@@ -220,142 +345,252 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < (TB ? TN : 1); ++j) bb[j] = add2(bbase[j], sb);
 
-      bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-      auto load = [&](auto S_, bf16x8* fa, bf16x8* fb) {
+      auto load = [&](auto S_, bf16x8* fa_, bf16x8* fb_) {
         constexpr int S = decltype(S_)::value;
+        if (no_lds) return;
         static_for<0, TM>([&](auto I_) {
           constexpr int i = decltype(I_)::value;
-          if constexpr (TA) fa[i] = trpair<2048 * S>(ab[i]);
-          else fa[i] = rd128<4096 * i + 512 * (S >> 1)>((S & 1) ? ab[0].y : ab[0].x);
+          if constexpr (TA) fa_[i] = trpair<2048 * S>(ab[i]);
+          else fa_[i] = rd128<4096 * i + 512 * (S >> 1)>((S & 1) ? ab[0].y : ab[0].x);
         });
         static_for<0, TN>([&](auto J_) {
           constexpr int j = decltype(J_)::value;
-          if constexpr (TB) fb[j] = trpair<2048 * S>(bb[j]);
-          else fb[j] = rd128<4096 * j + 512 * (S >> 1)>((S & 1) ? bb[0].y : bb[0].x);
+          if constexpr (TB) fb_[j] = trpair<2048 * S>(bb[j]);
+          else fb_[j] = rd128<4096 * j + 512 * (S >> 1)>((S & 1) ? bb[0].y : bb[0].x);
         });
       };
-      auto mm = [&](auto S_, const bf16x8* fa, const bf16x8* fb) {
+      load(std::integral_constant<int, 0>{}, fa[0], fb[0]);
+      lgkm_fence();
+      static_for<0, 4>([&](auto S_) {
         constexpr int S = decltype(S_)::value;
+        if constexpr (S < 3) load(std::integral_constant<int, S + 1>{}, fa[(S + 1) & 1], fb[(S + 1) & 1]);
+        if constexpr (S < SPREAD) {
+          constexpr int P0 = S * LPS / SPREAD, P1 = (S + 1) * LPS / SPREAD;
+          if (do_issue) static_for<P0, P1>([&](auto P_) { issue_piece(P_, kt + NST - 1, nb); });
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fb[j], fa[i], acc[i][j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fb[S & 1][j], fa[S & 1][i], acc[i][j]);
         if constexpr (CS) {
           if (cs_on && (S % WN) == wn) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) accb[i] = mfma_bf16(ones, fa[i], accb[i]);
+            for (int i = 0; i < TM; ++i) accb[i] = mfma_bf16(ones, fa[S & 1][i], accb[i]);
           }
         }
-      };
-      using S0 = std::integral_constant<int, 0>;
-      using S1 = std::integral_constant<int, 1>;
-      using S2 = std::integral_constant<int, 2>;
-      using S3 = std::integral_constant<int, 3>;
-      load(S0{}, fa0, fb0);
-      lgkm_fence();
-      load(S1{}, fa1, fb1);
-      mm(S0{}, fa0, fb0);
-      lgkm_fence();
-      load(S2{}, fa0, fb0);
-      mm(S1{}, fa1, fb1);
-      lgkm_fence();
-      load(S3{}, fa1, fb1);
-      mm(S2{}, fa0, fb0);
-      lgkm_fence();
-      mm(S3{}, fa1, fb1);
+        if constexpr (S < 3) lgkm_fence();
+      });
       buf = buf + 1 == NST ? 0 : buf + 1;
     }
   }
   __syncthreads();                                     // every wave is done reading the stage buffers
+  gemm_epilogue<TM, TN, WM, WN, EPI, CS>(a, acc, accb, smem, m0, n0, split, cs_on);
+}
 
-  // ---- epilogue.  Lane (lr, lh) of accumulator (i, j) holds C[row wm*WTM + 32i + lr]
-  //      [col wn*WTN + 32j + 8g + 4lh + e] in register 4g + e ----
-  if constexpr (EPI == kSlab) {
-    float* out = reinterpret_cast<float*>(a.C) + (size_t)split * a.M * a.ldc;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + 32 * i + lr;
-      if (m < a.M) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n = n0 + wn * WTN + 32 * j + 8 * g + 4 * lh;
-            if (n < a.N)
-              *reinterpret_cast<float4*>(out + (size_t)m * a.ldc + n) =
-                  make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-          }
-      }
+
+// ============================================================================ v2 main loop
+// 32-deep sub-stages in a ring of NBUF LDS buffers, AHEAD = NBUF - 1 sub-stages of LDS-DMA in flight.
+// A sub-stage's data is certified landed one barrier EARLY (each wave waits for its own DMA of
+// sub-stage s+1 before barrier s), so the first k-step fragments of sub-stage s+1 are read during
+// sub-stage s's MFMAs: after a barrier the MFMA pipe restarts on fragments already in registers.
+//   row operand sub-image  : [rows][32 k], 64-byte rows, 8-row groups of 512 B, 16-byte chunk c of row r
+//                            at 512*(r>>3) + 64*(r&7) + 16*(c ^ ((r>>2)&3)) (the toff() bank map)
+//   transposed sub-image   : [32 k][64 cols] = toff() rows 0..31 of a 64x64 image (4 KB per image)
+// One LDS-DMA wave-instruction fills 1 KB: 16 rows x 4 chunks (row operand) or 8 k-rows x 64 cols
+// (transposed operand).  Waves issue the same number of instructions per sub-stage (counted waits);
+// when the 1 KB pieces do not divide evenly, the spare instructions load zeros into a scratch slot.
+__device__ __forceinline__ int sub_off(int row, int c) {
+  return 512 * (row >> 3) + 64 * (row & 7) + 16 * (c ^ ((row >> 2) & 3));
+}
+__host__ __device__ constexpr int colblk_off4(int x) { return (x >> 1) * 4096 + (x & 1) * 512; }
+
+// vmcnt(n * LPS) for a wave-uniform n in [0, K] (steady state: the first compare)
+template <int K, int LPS>
+__device__ __forceinline__ void wait_sub(int n) {
+  if constexpr (K > 0) {
+    if (n >= K) {
+      wait_vm<K * LPS>();
+      return;
     }
+    wait_sub<K - 1, LPS>(n);
   } else {
-    const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+    wait_vm<0>();
+  }
+}
+
+template <int TM, int TN, int WM, int WN, int NBUF, int OCC, bool TA, bool TB, int EPI, bool CS>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm2(GemmArgs a) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int WTM = TM * 32, WTN = TN * 32, BM = WM * WTM, BN = WN * WTN;
+  constexpr int ASUB = BM * 64, BSUB = BN * 64, SUB = ASUB + BSUB + 1024;   // + scratch slot
+  constexpr int GA = ASUB / 1024, GB = BSUB / 1024;           // 1 KB pieces per sub-stage
+  constexpr int AG = (GA + NW - 1) / NW, BG = (GB + NW - 1) / NW;
+  constexpr int LPS = AG + BG, AHEAD = NBUF - 1;
+  static_assert(AHEAD >= 2, "the early-certify pipeline needs >= 3 sub-stage buffers");
+  static_assert((!TA || BM % 64 == 0) && (!TB || BN % 64 == 0), "transposed operands come in 64-wide images");
+  static_assert(BM % 16 == 0 && BN % 16 == 0, "row operands fill 16-row pieces");
+  constexpr int RS = BN * 2 + 16;
+  constexpr int EPI_BYTES = (EPI == kSlab ? 0 : BM * RS) + (CS ? WN * BM * 4 : 0);
+  constexpr int SMEM = NBUF * SUB > EPI_BYTES ? NBUF * SUB : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int t = threadIdx.x, l = t & 63, lr = l & 31, lh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.mtiles * a.ntiles;
+  const int split = id / ntile, rem = id - split * ntile;
+  constexpr int G = 8;
+  const int grp = rem / (G * a.ntiles), r2 = rem - grp * (G * a.ntiles);
+  const int gsz = min(G, a.mtiles - grp * G);
+  const int mt = grp * G + r2 % gsz, nt = r2 / gsz;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = split * a.kper;
+  const int NS = (min(a.K, kbeg + a.kper) - kbeg + 31) >> 5;   // 32-deep sub-stages
+  const int wm = w / WN, wn = w % WN;
+
+  // ---- per-lane LDS-DMA sources (bytes, sub-stage 0), LDS destinations (relative to a buffer) ----
+  uint32_t aoff[AG], boff[BG], adst[AG], bdst[BG];
+  int ak[AG], bk[BG];                                  // k offset of this lane's chunk (row operands)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+  for (int u = 0; u < AG; ++u) {
+    const int P = w + NW * u;                          // piece index
+    adst[u] = P < GA ? 1024 * P : ASUB + BSUB;         // spare instruction -> scratch slot
+    if constexpr (!TA) {
+      const int gg = l >> 5, rig = (l >> 2) & 7, row = 16 * P + 8 * gg + rig;
+      const int c = (l & 3) ^ ((2 * gg + (rig >> 2)) & 3), m = m0 + row;
+      ak[u] = 8 * c;
+      aoff[u] = (P < GA && m < a.M) ? (uint32_t)(((size_t)m * a.lda + kbeg + 8 * c) * 2) : kOOB;
+    } else {
+      const int kg = P & 3, img = P >> 2;
+      const int k = kbeg + 8 * kg + glds_row(l), m = m0 + 64 * img + 8 * glds_chunk(l, kg & 1);
+      ak[u] = 0;
+      aoff[u] = (P < GA && m < a.M) ? (uint32_t)(((size_t)k * a.lda + m) * 2) : kOOB;
+    }
+  }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = wn * WTN + 32 * j + 8 * g + 4 * lh;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+  for (int v = 0; v < BG; ++v) {
+    const int P = w + NW * v;
+    bdst[v] = P < GB ? ASUB + 1024 * P : ASUB + BSUB;
+    if constexpr (!TB) {
+      const int gg = l >> 5, rig = (l >> 2) & 7, row = 16 * P + 8 * gg + rig;
+      const int c = (l & 3) ^ ((2 * gg + (rig >> 2)) & 3), n = n0 + row;
+      bk[v] = 8 * c;
+      boff[v] = (P < GB && n < a.N) ? (uint32_t)(((size_t)n * a.ldb + kbeg + 8 * c) * 2) : kOOB;
+    } else {
+      const int kg = P & 3, img = P >> 2;
+      const int k = kbeg + 8 * kg + glds_row(l), n = n0 + 64 * img + 8 * glds_chunk(l, kg & 1);
+      bk[v] = 0;
+      boff[v] = (P < GB && n < a.N) ? (uint32_t)(((size_t)k * a.ldb + n) * 2) : kOOB;
+    }
+  }
+  const uint32_t astep = TA ? (uint32_t)a.lda * 64u : 64u, bstep = TB ? (uint32_t)a.ldb * 64u : 64u;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  auto issue = [&](int ss, int buf) {
+    const char* base = smem + buf * SUB;
+    const int kb = kbeg + ss * 32;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int ml = wm * WTM + 32 * i + lr;
-          const float v[4] = {acc[i][j][4 * g] + bv[0], acc[i][j][4 * g + 1] + bv[1], acc[i][j][4 * g + 2] + bv[2],
-                              acc[i][j][4 * g + 3] + bv[3]};
-          *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
-        }
+    for (int u = 0; u < AG; ++u)
+      glds16(ar, base + adst[u], (TA || kb + ak[u] < a.K) ? aoff[u] + (uint32_t)ss * astep : kOOB);
+#pragma unroll
+    for (int v = 0; v < BG; ++v)
+      glds16(br, base + bdst[v], (TB || kb + bk[v] < a.K) ? boff[v] + (uint32_t)ss * bstep : kOOB);
+  };
+
+  // ---- fragment lane bases relative to a sub-buffer ----
+  uint2 abase[TA ? TM : 1], bbase[TB ? TN : 1];
+  if constexpr (TA) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) abase[i] = add2(tr_lane_off_k8(), colblk_off4(wm * TM + i));
+  } else {
+    const int row = wm * WTM + lr;
+    abase[0] = make_uint2(sub_off(row, lh), sub_off(row, 2 + lh));
+  }
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bbase[j] = add2(tr_lane_off_k8(), ASUB + colblk_off4(wn * TN + j));
+  } else {
+    const int row = wn * WTN + lr;
+    bbase[0] = make_uint2(ASUB + sub_off(row, lh), ASUB + sub_off(row, 2 + lh));
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
+  f32x16 accb[CS ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < (CS ? TM : 1); ++i) accb[i] = f32x16{0.f};
+  const bool cs_on = CS && a.colsum != nullptr && nt == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3f80;
+
+  // k-step S (0/1) fragments of the sub-buffer at LDS address sb
+  auto load = [&](auto S_, uint32_t sb, bf16x8* fa, bf16x8* fb) {
+    constexpr int S = decltype(S_)::value;
+    static_for<0, TM>([&](auto I_) {
+      constexpr int i = decltype(I_)::value;
+      if constexpr (TA) fa[i] = trpair<2048 * S>(add2(abase[i], sb));
+      else fa[i] = rd128<2048 * i>((S ? abase[0].y : abase[0].x) + sb);
+    });
+    static_for<0, TN>([&](auto J_) {
+      constexpr int j = decltype(J_)::value;
+      if constexpr (TB) fb[j] = trpair<2048 * S>(add2(bbase[j], sb));
+      else fb[j] = rd128<2048 * j>((S ? bbase[0].y : bbase[0].x) + sb);
+    });
+  };
+  auto mm = [&](int S, const bf16x8* fa, const bf16x8* fb) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fb[j], fa[i], acc[i][j]);
+    if constexpr (CS) {
+      if (cs_on && (S % WN) == wn) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accb[i] = mfma_bf16(ones, fa[i], accb[i]);
       }
-  }
-  if constexpr (CS) {
-    if (cs_on && lh == 0) {
-      float* csl = reinterpret_cast<float*>(smem + TILE_BYTES);
+    }
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+
+  if (NS > 0) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) csl[wn * BM + wm * WTM + 32 * i + lr] = accb[i][0];
+    for (int q = 0; q < AHEAD; ++q)
+      if (q < NS) issue(q, q);
+    wait_sub<AHEAD - 1, LPS>(min(AHEAD - 1, NS - 1));   // own sub-stage 0 landed
+    __builtin_amdgcn_s_barrier();                        // everyone's sub-stage 0 landed
+    bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    load(S0{}, lds0, fa0, fb0);
+    lgkm_fence();
+    int buf = 0;
+    for (int ss = 0; ss < NS; ++ss) {
+      // own DMA of sub-stage ss+1 landed (younger sub-stages stay in flight), then the barrier
+      // certifies it for every wave and frees the buffer of sub-stage ss-1 for refilling
+      const int younger = min(AHEAD - 2, NS - 2 - ss);
+      if (younger >= 0) wait_sub<AHEAD - 2, LPS>(younger);
+      __builtin_amdgcn_s_barrier();
+      int nb = buf + AHEAD;
+      nb = nb >= NBUF ? nb - NBUF : nb;
+      if (ss + AHEAD < NS) issue(ss + AHEAD, nb);
+      const uint32_t sb = lds0 + buf * SUB;
+      int b1 = buf + 1;
+      b1 = b1 == NBUF ? 0 : b1;
+      load(S1{}, sb, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);               // the reads go out before the MFMAs
+      mm(0, fa0, fb0);
+      lgkm_fence();
+      if (ss + 1 < NS) load(S0{}, lds0 + b1 * SUB, fa0, fb0);
+      mm(1, fa1, fb1);
+      lgkm_fence();
+      buf = b1;
     }
   }
-  if constexpr (EPI != kSlab || CS) __syncthreads();
-  if constexpr (CS) {
-    if (cs_on && t < BM && m0 + t < a.M) {
-      const float* csl = reinterpret_cast<const float*>(smem + TILE_BYTES);
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < WN; ++q) s += csl[q * BM + t];
-      a.colsum[(size_t)split * a.M + m0 + t] = s;
-    }
-  }
-  if constexpr (EPI != kSlab) {
-    constexpr int CPR = BN / 8;                        // 16-byte chunks per tile row
-    bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
-#pragma unroll 4
-    for (int c = t; c < BM * CPR; c += NT) {
-      const int row = c / CPR, cc = c - row * CPR;
-      const int m = m0 + row, n = n0 + 8 * cc;
-      if (m < a.M && n < a.N) {
-        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
-        const size_t o = (size_t)m * a.ldc + n;
-        if constexpr (EPI == kBf16) {
-          *reinterpret_cast<uint4*>(C + o) = v;
-        } else if constexpr (EPI == kGelu) {
-          *reinterpret_cast<uint4*>(C + o) = v;
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = gelu_t(f[e], nullptr);
-          *reinterpret_cast<uint4*>(a.C2 + o) = pack8(f);
-        } else {                                       // kGeluBwd: dX = bf16(acc) * gelu'(pre)
-          float f[8], p[8];
-          unpack8(v, f);
-          unpack8(*reinterpret_cast<const uint4*>(a.aux + o), p);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float d;
-            gelu_t(p[e], &d);
-            f[e] *= d;
-          }
-          *reinterpret_cast<uint4*>(C + o) = pack8(f);
-        }
-      }
-    }
-  }
+  __syncthreads();                                     // every wave is done reading the sub-buffers
+  gemm_epilogue<TM, TN, WM, WN, EPI, CS>(a, acc, accb, smem, m0, n0, split, cs_on);
 }
 
 // dW (bf16 [M][N] contiguous) = sum of the fp32 slabs [S][M][N]; blocks past the dW range fold the
@@ -387,12 +622,28 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ p
 //   1: 256 x 128, 8 waves (4 x 2) of 64 x 64, 3 stages (144 KB)
 //   2: 128 x 128, 4 waves (2 x 2) of 64 x 64, 3 stages (96 KB)
 //   3: 256 x 256, 8 waves (4 x 2) of 64 x 128, 2 stages (128 KB)
+//   4: 128 x 128, 4 waves (2 x 2) of 64 x 64, 2 stages (64 KB): TWO blocks per CU, so one block's
+//      barrier stalls and epilogue overlap the other block's MFMAs
+//   5-8: the v2 main loop (k_gemm2: 32-deep sub-stages, NST = sub-stage buffers) at 256x256 (4),
+//        256x192 (5), 256x128 (6) and 128x128 at two blocks per CU (4)
+//   9-13: v1 with the next stage's DMA spread over the first 2 / 4 k-steps: 256x192 (9, 10),
+//        256x256 (11, 12), 256x128 x3 stages (13)
 template <int CFG> struct Cfg;
-template <> struct Cfg<0> { static constexpr int TM = 2, TN = 3, WM = 4, WN = 2, NST = 2; };
-template <> struct Cfg<1> { static constexpr int TM = 2, TN = 2, WM = 4, WN = 2, NST = 3; };
-template <> struct Cfg<2> { static constexpr int TM = 2, TN = 2, WM = 2, WN = 2, NST = 3; };
-template <> struct Cfg<3> { static constexpr int TM = 2, TN = 4, WM = 4, WN = 2, NST = 2; };
-constexpr int kNumCfg = 4;
+template <> struct Cfg<0> { static constexpr int V = 1, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 1; };
+template <> struct Cfg<1> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4, WN = 2, NST = 3, OCC = 1, SP = 1; };
+template <> struct Cfg<2> { static constexpr int V = 1, TM = 2, TN = 2, WM = 2, WN = 2, NST = 3, OCC = 1, SP = 1; };
+template <> struct Cfg<3> { static constexpr int V = 1, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 1; };
+template <> struct Cfg<4> { static constexpr int V = 1, TM = 2, TN = 2, WM = 2, WN = 2, NST = 2, OCC = 2, SP = 1; };
+template <> struct Cfg<5> { static constexpr int V = 2, TM = 2, TN = 4, WM = 4, WN = 2, NST = 4, OCC = 1, SP = 1; };
+template <> struct Cfg<6> { static constexpr int V = 2, TM = 2, TN = 3, WM = 4, WN = 2, NST = 5, OCC = 1, SP = 1; };
+template <> struct Cfg<7> { static constexpr int V = 2, TM = 2, TN = 2, WM = 4, WN = 2, NST = 6, OCC = 1, SP = 1; };
+template <> struct Cfg<8> { static constexpr int V = 2, TM = 2, TN = 2, WM = 2, WN = 2, NST = 4, OCC = 2, SP = 1; };
+template <> struct Cfg<9> { static constexpr int V = 1, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+template <> struct Cfg<10> { static constexpr int V = 1, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 4; };
+template <> struct Cfg<11> { static constexpr int V = 1, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+template <> struct Cfg<12> { static constexpr int V = 1, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 4; };
+template <> struct Cfg<13> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4, WN = 2, NST = 3, OCC = 1, SP = 4; };
+constexpr int kNumCfg = 14;
 
 template <int CFG, bool TA, bool TB, int EPI, bool CS>
 hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
@@ -401,8 +652,12 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  hipLaunchKernelGGL((k_gemm<C::TM, C::TN, C::WM, C::WN, C::NST, TA, TB, EPI, CS>), dim3(grid),
-                     dim3(64 * C::WM * C::WN), 0, st, a);
+  if constexpr (C::V == 1)
+    hipLaunchKernelGGL((k_gemm<C::TM, C::TN, C::WM, C::WN, C::NST, C::OCC, C::SP, TA, TB, EPI, CS>), dim3(grid),
+                       dim3(64 * C::WM * C::WN), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_gemm2<C::TM, C::TN, C::WM, C::WN, C::NST, C::OCC, TA, TB, EPI, CS>), dim3(grid),
+                       dim3(64 * C::WM * C::WN), 0, st, a);
   return hipGetLastError();
 }
 
@@ -412,7 +667,17 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 0: return launch_cfg<0, TA, TB, EPI, CS>(a, splits, st);
     case 1: return launch_cfg<1, TA, TB, EPI, CS>(a, splits, st);
     case 2: return launch_cfg<2, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<3, TA, TB, EPI, CS>(a, splits, st);
+    case 3: return launch_cfg<3, TA, TB, EPI, CS>(a, splits, st);
+    case 4: return launch_cfg<4, TA, TB, EPI, CS>(a, splits, st);
+    case 5: return launch_cfg<5, TA, TB, EPI, CS>(a, splits, st);
+    case 6: return launch_cfg<6, TA, TB, EPI, CS>(a, splits, st);
+    case 7: return launch_cfg<7, TA, TB, EPI, CS>(a, splits, st);
+    case 8: return launch_cfg<8, TA, TB, EPI, CS>(a, splits, st);
+    case 9: return launch_cfg<9, TA, TB, EPI, CS>(a, splits, st);
+    case 10: return launch_cfg<10, TA, TB, EPI, CS>(a, splits, st);
+    case 11: return launch_cfg<11, TA, TB, EPI, CS>(a, splits, st);
+    case 12: return launch_cfg<12, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<13, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -423,7 +688,9 @@ extern "C" {
 int pde_gemm_num_cfgs() { return kNumCfg; }
 
 void pde_gemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}};
+  static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
+                                     {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
+                                     {256, 192}, {256, 256}, {256, 256}, {256, 128}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
@@ -433,6 +700,10 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
 // C2 = act), 2 GELU backward (aux = pre), 3 fp32 split-K slabs (C = float [splits][M][ldc]).
 // colsum (wgrad only): fp32 [splits][M] bias-gradient partials.  Supported combinations:
 // (ta, tb) = (0, 0) with epi 0/1, (0, 1) with epi 0/2, (1, 1) with epi 0/3 (+colsum).
+int g_gemm_dbg = 0;   // pde_gemm_set_dbg: ablation flags of the v1 main loop (benchmarks only)
+
+void pde_gemm_set_dbg(int d) { g_gemm_dbg = d; }
+
 hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
                     int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
                     hipStream_t st) {
@@ -456,6 +727,7 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   a.a_bytes = (uint32_t)a_bytes;
   a.b_bytes = (uint32_t)b_bytes;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.dbg = g_gemm_dbg;
   a.kper = (((K + 63) / 64 + splits - 1) / splits) * 64;
   splits = (K + a.kper - 1) / a.kper;
   if (!ta && !tb) {

@@ -13,7 +13,10 @@ GPT-2 shapes, with the epilogues a library GEMM cannot fuse:
 All operands stay in their natural row-major layouts (the kernel reads transposed operands with
 ``ds_read_b64_tr_b16``); GPU-only, bf16 in / bf16 out, fp32 accumulation.
 
-Tile configurations (``gemm_tile(cfg)``): 0 = 256x192, 1 = 256x128, 2 = 128x128, 3 = 256x256.
+Tile configurations (``gemm_tile(cfg)``): 0 = 256x192, 1 = 256x128, 2 = 128x128, 3 = 256x256,
+4 = 128x128 at two blocks per CU; 5-8 = the same tiles (256x256, 256x192, 256x128, 128x128 x2)
+on the v2 main loop (32-deep sub-stages, fragments of the next sub-stage read across the barrier);
+9-13 = v1 tiles with the next stage's LDS-DMA spread over 2 or 4 k-steps.
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -28,20 +31,23 @@ from .._ext import kernels
 
 EPI_BF16, EPI_GELU, EPI_GELU_BWD, EPI_SLAB = 0, 1, 2, 3
 N_CU = 256
-_TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256)}
+_TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (128, 128),
+          5: (256, 256), 6: (256, 192), 7: (256, 128), 8: (128, 128), 9: (256, 192), 10: (256, 192),
+          11: (256, 256), 12: (256, 256), 13: (256, 128)}
 # relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
-_TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0}
+_TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 8: 0.8, 9: 1.0, 10: 1.0, 11: 1.0,
+             12: 1.0, 13: 0.93}
 
 # GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/):
 #   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
 #   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
 _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
-    ("fprop", 2304, 768): (0, 1), ("fprop", 768, 768): (3, 1), ("fprop", 3072, 768): (3, 1),
-    ("fprop", 768, 3072): (0, 1), ("fprop", 50304, 768): (3, 1),
-    ("dgrad", 768, 2304): (0, 1), ("dgrad", 768, 768): (0, 1), ("dgrad", 768, 3072): (0, 1),
-    ("dgrad", 3072, 768): (3, 1), ("dgrad", 768, 50304): (0, 1),
-    ("wgrad", 2304, 768): (3, 8), ("wgrad", 768, 768): (0, 16), ("wgrad", 3072, 768): (0, 4),
-    ("wgrad", 768, 3072): (0, 4), ("wgrad", 50304, 768): (3, 1),
+    ("fprop", 2304, 768): (9, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (11, 1),
+    ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (11, 1),
+    ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
+    ("dgrad", 3072, 768): (11, 1), ("dgrad", 768, 50304): (9, 1),
+    ("wgrad", 2304, 768): (11, 8), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (9, 4),
+    ("wgrad", 768, 3072): (9, 4), ("wgrad", 50304, 768): (11, 1),
 }
 
 _SCRATCH: Dict[Tuple, torch.Tensor] = {}

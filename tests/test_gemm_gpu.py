@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = [0, 1, 2, 3]
+CFGS = list(range(14))
 
 
 def rel_err(a, b):
@@ -25,8 +25,10 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 4
-    assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256)]
+    assert K.gemm_num_cfgs() == 14
+    assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
+                                                     (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
+                                                     (256, 192), (256, 256), (256, 256), (256, 128)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 

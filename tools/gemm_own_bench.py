@@ -37,8 +37,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fprop,dgrad,wgrad")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cfgs", default="0,3,4,6,9,10,11,12,13")
     a = ap.parse_args()
     T = a.tokens
+    CFGS = [int(c) for c in a.cfgs.split(",")]
     dev = torch.device("cuda", 0)
     kinds = a.only.split(",")
     r = lambda *s: (torch.randn(*s, device=dev) * 0.05).to(torch.bfloat16)
@@ -53,7 +55,7 @@ def main():
         if "fprop" in kinds:
             lib = timeit(lambda: torch.nn.functional.linear(x, w, None if name == "lm_head" else b), a.iters)
             res = {}
-            for cfg in range(4):
+            for cfg in CFGS:
                 res[cfg] = timeit(lambda: G.fprop(x, w, None if name == "lm_head" else b, gelu=gelu, cfg=cfg), a.iters)
             best = min(res, key=res.get)
             lines.append({"gemm": f"{name}.fprop", "M": T, "N": out, "K": fin, "epilogue": "bias+gelu" if gelu else "bias",
@@ -66,7 +68,7 @@ def main():
             pre = r(T, fin) if name == "mlp_proj" else None
             lib = timeit(lambda: torch.matmul(dy, w), a.iters)
             res = {}
-            for cfg in range(4):
+            for cfg in CFGS:
                 res[cfg] = timeit(lambda: G.dgrad(dy, w, pre=pre, cfg=cfg), a.iters)
             best = min(res, key=res.get)
             lines.append({"gemm": f"{name}.dgrad", "M": T, "N": fin, "K": out,
@@ -79,7 +81,7 @@ def main():
             dw = torch.empty(out, fin, device=dev, dtype=torch.bfloat16)
             lib = timeit(lambda: torch.matmul(dy.t(), x, out=dw), a.iters)
             res = {}
-            for cfg in range(4):
+            for cfg in CFGS:
                 for s in (1, 2, 4, 8, 16):
                     if name == "lm_head" and s > 2:
                         continue
