@@ -93,22 +93,28 @@ def bench_gpt2(args):
     ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
     opt = AdamWMaster(model.decay_groups(0.1), lr=6e-4, betas=(0.9, 0.95), max_grad_norm=1.0)
     # a pool of 256 sequences per rank of a learnable synthetic language, sharded by the framework's
-    # DistributedSampler (disjoint per rank, reshuffled per pass): no fixed handful of batches to memorise
+    # DistributedSampler and reshuffled every epoch (set_epoch): no fixed handful of batches to
+    # memorise.  The whole pool and the per-epoch shard orders of every epoch the run can reach are
+    # built before timing, so a step only gathers its B rows on the device (no host sync, no randperm
+    # inside the timed region).
     from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_tokens
     pool = 256 * world
+    data = synthetic_tokens(torch.arange(pool), T, cfg.vocab_size, seed=args.seed, device=dev)   # [pool, T+1]
     sampler = DistributedSampler(range(pool), num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
-    shard = sampler.indices_tensor().long()
-    data = synthetic_tokens(shard, T, cfg.vocab_size, seed=args.seed, device=dev)
+    nb = sampler.num_samples // B
+    n_epochs = (args.warmup + args.steps + 64 * (world > 1)) // nb + 2
+    orders = []
+    for e in range(n_epochs):
+        sampler.set_epoch(e)
+        orders.append(sampler.indices_tensor().long())
+    orders = torch.stack(orders).to(dev)                 # [epochs, pool / world]
     it = [0]
     losses = []
 
     def step():
-        nb = data.shape[0] // B
-        j = it[0] % nb
-        if j == 0 and it[0]:
-            data.copy_(data[torch.randperm(data.shape[0], device=dev)])      # next pass over the shard
-        batch = data[j * B:(j + 1) * B]
+        e, j = divmod(it[0], nb)
         it[0] += 1
+        batch = data.index_select(0, orders[e % n_epochs, j * B:(j + 1) * B])
         opt.zero_grad()
         loss = ddp(batch[:, :-1], batch[:, 1:])
         loss.backward()
@@ -127,7 +133,7 @@ def bench_gpt2(args):
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic learnable token sequences (next = 31*prev+7+U[0,4) mod V; loss floor ln 4), "
-                    "256 per rank sharded by DistributedSampler, random-init weights",
+                    "256 per rank sharded by DistributedSampler, reshuffled per epoch, random-init weights",
             "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
                        "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **extra},

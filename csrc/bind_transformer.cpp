@@ -284,6 +284,7 @@ void register_transformer(pybind11::module& m) {
   m.def("colsum_bf16", &colsum_bf16);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_set_variant", [](int64_t v) { pde_attn_set_variant((int)v); });
 }
 
 }  // namespace pde

@@ -144,6 +144,7 @@ hipError_t pde_gemm_reduce(const float* part, int S, int M, int N, void* dw, con
                            hipStream_t st);
 
 // ---- attention (attention.hip) ----
+void pde_attn_set_variant(int v);
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
                         int T, int H, float scale, hipStream_t st);
 hipError_t pde_attn_bwd(const void* q, const void* k, const void* v, int ldq, const void* o, const void* dout,

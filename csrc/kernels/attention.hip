@@ -38,7 +38,7 @@ using namespace pde_lds;
 
 constexpr int HD = 64;        // head dim
 constexpr int TILE = 8192;    // bytes of one 64 x 64 bf16 tile image
-constexpr int NST = 4;        // LDS stage ring depth
+constexpr int kNstDefault = 4;   // LDS stage ring depth (template parameter NST of the kernels)
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -94,7 +94,8 @@ __device__ __forceinline__ void store_dimrows(bf16_t* dst, const f32x16& a0, con
 
 // ------------------------------------------------------------------------------------ forward
 // grid (T/128, B*H), 256 threads: wave w owns queries qt*128 + 32w + (0..31)
-__global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+template <int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_fwd(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                      const bf16_t* __restrict__ V, int ldq, bf16_t* __restrict__ O,
                                                      int ldo, float* __restrict__ LSE, int T, int H, float sl2,
                                                      float scale) {
@@ -215,7 +216,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_pre(const bf16_t* __restrict__
 
 // dQ: grid (T/128, B*H); transposed-score structure of the forward; K, V tiles staged in LDS
 // (K rows for S^T, V rows for dP^T, K^T via transposed reads for dQ^T += K^T dS^T).
-__global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+template <int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                         const bf16_t* __restrict__ V, int ldq,
                                                         const bf16_t* __restrict__ dO, int ldo,
                                                         const float* __restrict__ LSE, const float* __restrict__ Dd,
@@ -303,7 +305,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
 // dK, dV: grid (T/128, B*H); wave w owns keys kb*128 + 32w + (0..31); loops over 64-query tiles
 // with Q / dO / LSE / D staged in LDS (rows for S / dP, transposed reads for dK / dV).
 constexpr int kDkdvStage = 2 * TILE + 512;           // Q | dO | LSE[64] | D[64]
-__global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+template <int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkdv(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, int ldq,
                                                           const bf16_t* __restrict__ dO, int ldo,
                                                           const float* __restrict__ LSE,
@@ -413,15 +416,46 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   }
 }
 
+int g_attn_variant = 5;   // pde_attn_set_variant: LDS ring depth / occupancy (default: measured best)
+
+template <int NST, int OCC>
+void launch_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B, int T,
+                int H, float scale, hipStream_t st) {
+  hipLaunchKernelGGL((k_attn_fwd<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, ldq, (bf16_t*)o, ldo, lse, T, H, scale * 1.4426950408889634f,
+                     scale);
+}
+
+template <int NST, int OCC>
+void launch_dq(const void* q, const void* k, const void* v, int ldq, const void* dout, int ldo, const float* lse,
+               const float* Dd, void* dq, int B, int T, int H, float sl2, float scale, hipStream_t st) {
+  hipLaunchKernelGGL((k_attn_bwd_dq<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dq, T, H,
+                     sl2, scale);
+}
+
+template <int NST, int OCC>
+void launch_dkdv(const void* q, const void* k, const void* v, int ldq, const void* dout, int ldo, const float* lse,
+                 const float* Dd, void* dk, void* dv, int B, int T, int H, float sl2, float scale, hipStream_t st) {
+  hipLaunchKernelGGL((k_attn_bwd_dkdv<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dk,
+                     (bf16_t*)dv, T, H, sl2, scale);
+}
+
 }  // namespace
 
 extern "C" {
 
+// variant bits: 1 = forward with a 3-deep ring at 3 blocks per CU, 2 = dQ likewise (spills: slower),
+//               4 = dK/dV with a 3-deep ring (2 blocks per CU).  Default 5, measured on MI355X at the
+//               GPT-2 shape (tools/attn_bench.py, profiles/r2_attn/): fwd 85.3 -> 71.3 us, bwd 263.8 -> 241.0 us
+void pde_attn_set_variant(int v) { g_attn_variant = v; }
+
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
                         int T, int H, float scale, hipStream_t st) {
   if (T % 128 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_attn_fwd, dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, ldq, (bf16_t*)o, ldo, lse, T, H, scale * 1.4426950408889634f, scale);
+  if (g_attn_variant & 1) launch_fwd<3, 3>(q, k, v, ldq, o, ldo, lse, B, T, H, scale, st);
+  else launch_fwd<kNstDefault, 2>(q, k, v, ldq, o, ldo, lse, B, T, H, scale, st);
   return hipGetLastError();
 }
 
@@ -433,11 +467,10 @@ hipError_t pde_attn_bwd(const void* q, const void* k, const void* v, int ldq, co
   hipLaunchKernelGGL(k_attn_bwd_pre, dim3((N * H + 255) / 256), dim3(256), 0, st, (const bf16_t*)o,
                      (const bf16_t*)dout, ldo, Dd, N, T, H);
   const float sl2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dk, (bf16_t*)dv, T, H, sl2,
-                     scale);
-  hipLaunchKernelGGL(k_attn_bwd_dq, dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q, (const bf16_t*)k,
-                     (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dq, T, H, sl2, scale);
+  if (g_attn_variant & 4) launch_dkdv<3, 2>(q, k, v, ldq, dout, ldo, lse, Dd, dk, dv, B, T, H, sl2, scale, st);
+  else launch_dkdv<kNstDefault, 2>(q, k, v, ldq, dout, ldo, lse, Dd, dk, dv, B, T, H, sl2, scale, st);
+  if (g_attn_variant & 2) launch_dq<3, 3>(q, k, v, ldq, dout, ldo, lse, Dd, dq, B, T, H, sl2, scale, st);
+  else launch_dq<kNstDefault, 2>(q, k, v, ldq, dout, ldo, lse, Dd, dq, B, T, H, sl2, scale, st);
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--B", type=int, default=16)
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--variants", default="0", help="attention variant bits (pde_attn_set_variant), comma list")
     a = ap.parse_args()
     K = kernels()
     B, T, H, D = a.B, a.T, a.H, 64
@@ -49,10 +50,14 @@ def main():
     Dd = torch.empty(B * H * T, device="cuda")
     scale = 1.0 / math.sqrt(D)
     fwd_flops = 4.0 * B * H * T * T * D / 2          # QK^T + PV, causal half
-    t_f = timeit(lambda: K.attn_fwd(q, k, v, o, lse, H, scale), a.iters)
-    t_b = timeit(lambda: K.attn_bwd(q, k, v, o, do, lse, Dd, dq, dk, dv, H, scale), a.iters)
-    print(json.dumps({"shape": [B, T, H, D], "fwd_us": round(t_f, 1), "fwd_tflops": round(fwd_flops / t_f / 1e6, 1),
-                      "bwd_us": round(t_b, 1), "bwd_tflops": round(2.5 * fwd_flops / t_b / 1e6, 1)}), flush=True)
+    for var in [int(x) for x in a.variants.split(",")]:
+        K.attn_set_variant(var)
+        t_f = timeit(lambda: K.attn_fwd(q, k, v, o, lse, H, scale), a.iters)
+        t_b = timeit(lambda: K.attn_bwd(q, k, v, o, do, lse, Dd, dq, dk, dv, H, scale), a.iters)
+        print(json.dumps({"variant": var, "shape": [B, T, H, D], "fwd_us": round(t_f, 1),
+                          "fwd_tflops": round(fwd_flops / t_f / 1e6, 1), "bwd_us": round(t_b, 1),
+                          "bwd_tflops": round(2.5 * fwd_flops / t_b / 1e6, 1)}), flush=True)
+    K.attn_set_variant(5)
 
 
 if __name__ == "__main__":
