@@ -79,6 +79,23 @@ void bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& x, cons
             "bn_bwd");
 }
 
+// global average pool: x channels-last [N, C, H, W] -> out [N, C] (and back)
+void avgpool_fwd(const at::Tensor& x, const at::Tensor& out) {
+  nhwc_rows(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  check_cuda(out, "out", BF16, N * C);
+  TORCH_CHECK(C % 8 == 0, "avgpool: C % 8 == 0");
+  hip_check(pde_avgpool_fwd(x.data_ptr(), out.data_ptr(), (int)N, (int)HW, (int)C, cur_stream()), "avgpool_fwd");
+}
+
+void avgpool_bwd(const at::Tensor& dout, const at::Tensor& dx) {
+  nhwc_rows(dx, "dx");
+  const int64_t N = dx.size(0), C = dx.size(1), HW = dx.size(2) * dx.size(3);
+  check_cuda(dout, "dout", BF16, N * C);
+  TORCH_CHECK(C % 8 == 0, "avgpool: C % 8 == 0");
+  hip_check(pde_avgpool_bwd(dout.data_ptr(), dx.data_ptr(), (int)N, (int)HW, (int)C, cur_stream()), "avgpool_bwd");
+}
+
 void maxpool3s2_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& arg) {
   nhwc_rows(x, "x");
   nhwc_rows(y, "y");
@@ -163,7 +180,7 @@ void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 }
 
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt, const at::Tensor& dx,
-                int64_t stride, int64_t pad) {
+                int64_t stride, int64_t pad, const OptT& res) {
   const ConvGeom g = conv_geom(dx, w, stride, pad);
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
@@ -171,7 +188,14 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
   check_cuda(wt, "wt", BF16, g.N * g.C * g.R * g.S);
   hip_check(pde_conv_wtrans(w.data_ptr(), wt.data_ptr(), (int)g.N, (int)(g.R * g.S), (int)g.C, cur_stream()),
             "conv_wtrans");
-  hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    TORCH_CHECK(res->is_cuda() && res->scalar_type() == BF16 && res->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    res->sizes() == dx.sizes(),
+                "conv dgrad: res must be a channels-last bf16 tensor shaped like dx");
+    rp = res->data_ptr();
+  }
+  hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), rp, (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
                            (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, cur_stream()),
             "conv_dgrad");
 }
@@ -252,6 +276,8 @@ void register_resnet(pybind11::module& m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("sgd_master", &sgd_master);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv_stats_blocks", &conv_stats_blocks);
   m.def("stem_stats_blocks", &stem_stats_blocks);
@@ -261,7 +287,8 @@ void register_resnet(pybind11::module& m) {
   m.def("bn_part_rows", &bn_part_rows);
   m.def("conv_set_stages", [](int64_t n) { pde_conv_set_stages((int)n); });
   m.def("conv_fprop", &conv_fprop);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt"), py::arg("dx"), py::arg("stride"),
+        py::arg("pad"), py::arg("res") = py::none());
   m.def("conv_wgrad_splits", &conv_wgrad_splits);
   m.def("conv_wgrad", &conv_wgrad);
 }

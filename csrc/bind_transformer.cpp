@@ -258,7 +258,7 @@ void register_transformer(pybind11::module& m) {
   m.def("ln_bwd_blocks", &ln_bwd_blocks);
   m.def("ln_bwd", &ln_bwd);
   m.def("sum_slabs_bf16", &sum_slabs_bf16);
-  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("ta"), py::arg("tb"), py::arg("epi"),
+  m.def("gemm_bf16", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("ta"), py::arg("tb"), py::arg("epi"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("splits") = 1,
         py::arg("cfg") = 0, py::arg("C2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("colsum") = py::none());

@@ -70,6 +70,7 @@ struct IgemmArgs {
   const bf16_t* A;      // gather source NHWC [Bn][IH][IW][CA]
   const bf16_t* W;      // [NC][T][CA]
   bf16_t* Y;            // NHWC [Bn][OH][OW][NC]
+  const bf16_t* R;      // optional, same layout as Y: Y = bf16(acc) + R (residual-gradient accumulate)
   float* stats;         // optional [mtiles][2][NC] (single-phase launches)
   uint32_t a_bytes, w_bytes;
   int Bn, IH, IW, CA;
@@ -245,8 +246,17 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
       const int b = fdiv(m, P.Hq * P.Wq, P.inv_hw), r2 = m - b * (P.Hq * P.Wq);
       const int hq = fdiv(r2, P.Wq, P.inv_w);
       const int oh = hq * a.sO + P.ph, ow = (r2 - hq * P.Wq) * a.sO + P.pw;
-      const uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
-      *reinterpret_cast<uint4*>(a.Y + (((size_t)b * a.OH + oh) * a.OW + ow) * a.NC + n0 + cc * 8) = v;
+      uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
+      const size_t o = (((size_t)b * a.OH + oh) * a.OW + ow) * a.NC + n0 + cc * 8;
+      if (a.R) {                                       // the other consumer's gradient, added once
+        float f[8], r[8];
+        unpack8(v, f);
+        unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(a.Y + o) = v;
     }
   }
   if (a.stats && t < 2 * BN) {
@@ -489,14 +499,17 @@ hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStre
   return hipGetLastError();
 }
 
-// dX (NHWC [Bn][H][W][C]) from dY ([Bn][OH][OW][N]) and Wt = [C][R*S][N] (pde_conv_wtrans)
-hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, int Bn, int H, int W, int C, int N, int R, int S,
-                          int stride, int pad, int OH, int OW, hipStream_t st) {
+// dX (NHWC [Bn][H][W][C]) from dY ([Bn][OH][OW][N]) and Wt = [C][R*S][N] (pde_conv_wtrans);
+// res (optional, NHWC like dX): dX = dgrad + res -- the residual / second-consumer gradient of the
+// conv input accumulated in the epilogue instead of a separate add pass
+hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, int Bn, int H, int W, int C,
+                          int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st) {
   if (C % 64 || N % 64 || R * S > 9 || stride < 1 || stride > 2) return hipErrorInvalidValue;
   IgemmArgs a{};
   a.A = (const bf16_t*)dy;
   a.W = (const bf16_t*)wt;
   a.Y = (bf16_t*)dx;
+  a.R = (const bf16_t*)res;
   a.stats = nullptr;
   a.a_bytes = (uint32_t)((size_t)Bn * OH * OW * N * 2);
   a.w_bytes = (uint32_t)((size_t)N * R * S * C * 2);

@@ -378,6 +378,38 @@ inline int grid_cap(int64_t n, int cap) {
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+// ---- global average pool over NHWC (the ResNet head before the FC GEMM) ----
+// fwd: out[n][c] = mean_hw x[n][hw][c]; one thread per (n, 8-channel chunk), fp32 sum
+__global__ __launch_bounds__(256) void k_avgpool_fwd(const uint4* __restrict__ x, uint4* __restrict__ out, int N,
+                                                     int HW, int C8, float inv) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C8) return;
+  const int n = i / C8, c = i - n * C8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < HW; ++p) {
+    float v[8];
+    unpack8(x[((size_t)n * HW + p) * C8 + c], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] *= inv;
+  out[i] = pack8(s);
+}
+// bwd: dx[n][hw][c] = dout[n][c] / HW
+__global__ __launch_bounds__(256) void k_avgpool_bwd(const uint4* __restrict__ dout, uint4* __restrict__ dx, int N,
+                                                     int HW, int C8, float inv) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)N * HW * C8) return;
+  const int c = (int)(i % C8);
+  const int n = (int)(i / ((int64_t)HW * C8));
+  float v[8];
+  unpack8(dout[(size_t)n * C8 + c], v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= inv;
+  dx[i] = pack8(v);
+}
+
 }  // namespace
 
 extern "C" {
@@ -468,6 +500,22 @@ hipError_t pde_sgd_master(float* master, void* p16, const void* g16, float* buf,
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(k_sgd_master, dim3(grid_cap(n4, 2048)), dim3(256), 0, st, master, (uint2*)p16,
                      (const uint2*)g16, (float4*)buf, n4, lr, momentum, wd, nesterov, grad_scale, decay_blk);
+  return hipGetLastError();
+}
+
+hipError_t pde_avgpool_fwd(const void* x, void* out, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int total = N * (C / 8);
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3((total + 255) / 256), dim3(256), 0, st, (const uint4*)x, (uint4*)out, N, HW,
+                     C / 8, 1.f / (float)HW);
+  return hipGetLastError();
+}
+
+hipError_t pde_avgpool_bwd(const void* dout, void* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const uint4*)dout,
+                     (uint4*)dx, N, HW, C / 8, 1.f / (float)HW);
   return hipGetLastError();
 }
 

@@ -2,7 +2,9 @@
 synthetic 3x224x224, DDP 8xMI355X").  Same architecture / parameter names as torchvision's
 ``resnet18`` (conv1/bn1, layer1..layer4 of BasicBlocks with downsample, fc), so state_dicts
 interchange; BatchNorm+residual+ReLU run as fused HIP kernels (``ops.resnet``); every convolution except the 3-channel
-stem is an implicit GEMM on bf16 MFMA (``csrc/kernels/conv.hip``), the stem a MIOpen convolution.
+stem is an implicit GEMM on bf16 MFMA (``csrc/kernels/conv.hip``), the stem has its own MFMA kernels
+(``csrc/kernels/stem.hip``); a training BasicBlock is one autograd node (``ops.resnet.BasicBlockFn``:
+residual-gradient add inside conv1's dgrad epilogue); the head is an own pool kernel + the own GEMM.
 """
 from __future__ import annotations
 
@@ -10,9 +12,9 @@ import math
 
 import torch
 import torch.nn as tnn
-import torch.nn.functional as F
 
-from ..ops.resnet import batch_norm_act, conv2d_nhwc, max_pool3s2
+from ..ops.resnet import (basic_block_eligible, basic_block_train, batch_norm_act, conv2d_nhwc, max_pool3s2,
+                          resnet_head)
 
 
 class BN(tnn.Module):
@@ -72,6 +74,11 @@ class BasicBlock(tnn.Module):
 
     def forward(self, x):
         st = self.training and x.is_cuda
+        if st and basic_block_eligible(x, self.conv1.weight, self.conv2.weight, None):
+            # one autograd node: residual-gradient add fused into conv1's dgrad epilogue
+            ds = self.downsample
+            return basic_block_train(x, self.conv1, self.bn1, self.conv2, self.bn2,
+                                     ds[0] if ds is not None else None, ds[1] if ds is not None else None)
         if self.downsample is not None:
             idt = self.downsample[1](self.downsample[0](x, st), relu=False)
         else:
@@ -120,8 +127,7 @@ class ResNet(tnn.Module):
         x = max_pool3s2(x)
         for i in range(1, 5):
             x = getattr(self, f"layer{i}")(x)
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
-        return self.fc(x)
+        return resnet_head(x, self.fc.weight, self.fc.bias)
 
     def decay_groups(self, weight_decay: float):
         """SGD groups: conv / fc weights decay; BN parameters and biases do not."""

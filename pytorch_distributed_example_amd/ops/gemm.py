@@ -107,9 +107,9 @@ def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16) if out is None else out
     if gelu:
         act = torch.empty_like(y)
-        kernels().gemm(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=act, bias=bias)
+        kernels().gemm_bf16(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=act, bias=bias)
         return y, act
-    kernels().gemm(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c, bias=bias)
+    kernels().gemm_bf16(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c, bias=bias)
     return y
 
 
@@ -122,9 +122,9 @@ def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None
     c = pick("dgrad", M, Kout, Nk)[0] if cfg is None else cfg
     dx = torch.empty(M, Kout, device=dy2.device, dtype=torch.bfloat16)
     if pre is not None:
-        kernels().gemm(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=pre)
+        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=pre)
     else:
-        kernels().gemm(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c)
+        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c)
     return dx
 
 
@@ -146,12 +146,12 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, dw: Optional[torch.Tensor] = None
         db = torch.empty(N, device=dy2.device, dtype=torch.bfloat16)
     cs = _scratch(dy2.device, S * N, "cs") if want_db else None
     if S == 1:
-        kernels().gemm(dy2, x2, dw, 1, 1, EPI_BF16, N, K, T, N, K, K, 1, c, colsum=cs)
+        kernels().gemm_bf16(dy2, x2, dw, 1, 1, EPI_BF16, N, K, T, N, K, K, 1, c, colsum=cs)
         if want_db:
             kernels().gemm_reduce(None, 1, N, K, None, cs, db)     # db only
         return dw, db
     part = _scratch(dy2.device, S * N * K, "slab")
-    kernels().gemm(dy2, x2, part, 1, 1, EPI_SLAB, N, K, T, N, K, K, S, c, colsum=cs)
+    kernels().gemm_bf16(dy2, x2, part, 1, 1, EPI_SLAB, N, K, T, N, K, K, S, c, colsum=cs)
     kernels().gemm_reduce(part, S, N, K, dw, cs, db)
     return dw, db
 

@@ -13,6 +13,8 @@ definitions.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -158,6 +160,129 @@ class StemConvFn(torch.autograd.Function):
         return dx, dw, None
 
 
+# ----------------------------------------------------------------------------- fused BasicBlock
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _conv_fwd(x, w, stride, pad):
+    """conv (MFMA implicit GEMM) with the following BN's partial statistics: (y, part, nblk)."""
+    K = kernels()
+    N, C, H, W = x.shape
+    O, _, R, S = w.shape
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    y = torch.empty(N, O, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    nblk = K.conv_stats_blocks(N * OH * OW, O)
+    part = torch.empty(K.bn_part_rows(nblk) * 2 * O, device=x.device, dtype=torch.float32)
+    K.conv_fprop(x, w, y, part, stride, pad)
+    return y, part, nblk
+
+
+def _bn_fwd(x, part, nblk, gamma, beta, rm, rv, momentum, eps, res, relu):
+    C = x.shape[1]
+    dev = x.device
+    y = torch.empty_like(x)
+    mean, rstd, scale, shift = (torch.empty(C, device=dev, dtype=torch.float32) for _ in range(4))
+    kernels().bn_fwd(x, res, y, gamma, beta, eps, momentum, rm, rv, part, mean, rstd, scale, shift, relu, True, nblk)
+    return y, mean, rstd
+
+
+def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres):
+    K = kernels()
+    C = x.shape[1]
+    M = x.numel() // C
+    dev = x.device
+    part = torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev, dtype=torch.float32)
+    coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
+    dgamma = flat_grad_slot(gamma)
+    dgamma = torch.empty(C, device=dev, dtype=gamma.dtype) if dgamma is None else dgamma
+    dbeta = flat_grad_slot(beta)
+    dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if want_dres else None
+    K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, relu)
+    return dx, dgamma, dbeta, dres
+
+
+def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None):
+    """(dx [+ res, fused into the dgrad epilogue], dw)."""
+    K = kernels()
+    dx = None
+    if need_dx:
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        wt = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
+        K.conv_dgrad(dy, w, wt, dx, stride, pad, res)
+    splits = K.conv_wgrad_splits(x, w, stride, pad)
+    part = torch.empty(splits * w.numel(), device=w.device, dtype=torch.float32)
+    dw = flat_grad_slot(w)
+    if dw is None or not dw.is_contiguous(memory_format=torch.channels_last):
+        dw = torch.empty_like(w, memory_format=torch.channels_last)
+    K.conv_wgrad(dy, x, w, part, splits, dw, stride, pad)
+    return dx, dw
+
+
+class BasicBlockFn(torch.autograd.Function):
+    """Training-mode ResNet BasicBlock  out = relu(bn2(conv2(relu(bn1(conv1(x))))) + idt), idt = x or
+    bn_d(conv_d(x)), as ONE autograd node.  Forward is the usual kernel chain (every conv emits its
+    BN's batch statistics in the epilogue).  Backward runs the chain in reverse and adds the two
+    gradients of x -- the residual (or downsample) path and conv1's input gradient -- inside conv1's
+    dgrad epilogue, instead of autograd summing two separately materialised tensors (an extra read
+    of both and a write per block)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, wd, gd, bd, rm1, rv1, rm2, rv2, rmd, rvd, stride, momentum, eps):
+        y1, p1, n1 = _conv_fwd(x, w1, stride, 1)
+        a1, m1, s1 = _bn_fwd(y1, p1, n1, g1, b1, rm1, rv1, momentum, eps, None, True)
+        y2, p2, n2 = _conv_fwd(a1, w2, 1, 1)
+        if wd is not None:
+            yd, pd, nd = _conv_fwd(x, wd, stride, 0)
+            idt, md, sd = _bn_fwd(yd, pd, nd, gd, bd, rmd, rvd, momentum, eps, None, False)
+        else:
+            yd = md = sd = None
+            idt = x                                      # identity shortcut
+        out, m2, s2 = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, idt, True)
+        ctx.save_for_backward(x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd,
+                              idt if wd is not None else None, m1, s1, m2, s2, md, sd)
+        ctx.stride = stride
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd, idt, m1, s1, m2, s2, md,
+         sd) = ctx.saved_tensors
+        dout = _cl(dout)
+        dy2, dg2, db2, dres = _bn_bwd(dout, out, y2, g2, b2, m2, s2, True, True)
+        da1, dw2 = _conv_bwd(dy2, a1, w2, 1, 1)
+        dy1, dg1, db1, _ = _bn_bwd(da1, a1, y1, g1, b1, m1, s1, True, False)
+        dwd = dgd = dbd = None
+        if wd is not None:
+            dyd, dgd, dbd, _ = _bn_bwd(dres, idt, yd, gd, bd, md, sd, False, False)
+            dxd, dwd = _conv_bwd(dyd, x, wd, ctx.stride, 0, need_dx=ctx.needs_input_grad[0])
+            other = dxd
+        else:
+            other = dres
+        dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=other)
+        return (dx, dw1, dg1, db1, dw2, dg2, db2, dwd, dgd, dbd) + (None,) * 9
+
+
+def basic_block_eligible(x, w1, w2, wd) -> bool:
+    """GPU training blocks take the fused single-node path (PDE_RESNET_FUSED_BLOCK=0 disables it)."""
+    return (os.environ.get("PDE_RESNET_FUSED_BLOCK", "1") != "0" and x.is_cuda and x.dim() == 4 and igemm_eligible(x, w1, 1, 1) and w2.shape[1] % 64 == 0
+            and w2.shape[0] % 64 == 0)
+
+
+def basic_block_train(x, conv1, bn1, conv2, bn2, ds_conv=None, ds_bn=None):
+    """Training forward of a BasicBlock through BasicBlockFn (modules supply weights and BN state)."""
+    x = _cl(x)
+    wd = gd = bd = rmd = rvd = None
+    if ds_conv is not None:
+        wd, gd, bd, rmd, rvd = (_cl(ds_conv.weight), ds_bn.weight, ds_bn.bias, ds_bn.running_mean,
+                                ds_bn.running_var)
+    return BasicBlockFn.apply(x, _cl(conv1.weight), bn1.weight, bn1.bias, _cl(conv2.weight), bn2.weight, bn2.bias,
+                              wd, gd, bd, bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
+                              rmd, rvd, conv1.stride[0], bn1.momentum, bn1.eps)
+
+
 def stem_eligible(x, w, stride: int, pad: int) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
             and x.shape[1] == 3 and tuple(w.shape) == (64, 3, 7, 7) and stride == 2 and pad == 3
@@ -244,3 +369,38 @@ def max_pool3s2(x):
     if x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0:
         return MaxPool3s2Fn.apply(x.contiguous(memory_format=torch.channels_last))
     return F.max_pool2d(x, 3, 2, 1)
+
+
+class HeadFn(torch.autograd.Function):
+    """ResNet head: global average pool (HIP kernel) + FC on the framework's bf16 MFMA GEMM (bias in
+    the epilogue; backward = dgrad GEMM + wgrad GEMM with the bias gradient from its ones-MFMA)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from . import gemm as G
+        N, C = x.shape[0], x.shape[1]
+        pooled = torch.empty(N, C, device=x.device, dtype=x.dtype)
+        kernels().avgpool_fwd(x, pooled)
+        ctx.save_for_backward(pooled, w)
+        ctx.xshape = x.shape
+        ctx.bias = b
+        return G.fprop(pooled, w, b)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        from . import gemm as G
+        pooled, w = ctx.saved_tensors
+        dl = dlogits.contiguous()
+        dpooled = G.dgrad(dl, w)
+        dw, db = G.wgrad(dl, pooled, dw=flat_grad_slot(w), db=flat_grad_slot(ctx.bias), want_db=True)
+        dx = torch.empty(ctx.xshape, device=dl.device, dtype=dl.dtype, memory_format=torch.channels_last)
+        kernels().avgpool_bwd(dpooled, dx)
+        return dx, dw, db
+
+
+def resnet_head(x, w, b):
+    """logits = fc(flatten(adaptive_avg_pool2d(x, 1)))."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0
+            and w.shape[0] % 8 == 0):
+        return HeadFn.apply(_cl(x), w.contiguous(), b)
+    return F.linear(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1), w, b)
