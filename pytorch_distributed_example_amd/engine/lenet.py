@@ -217,7 +217,12 @@ class LeNetTrainStep:
         rejected: folding the head into fc1, the last column block of each 16-row tile running the
         head -- with __threadfence() in every block (L2 write-back/invalidate per block) 99 us/step,
         with write-through H1 stores + agent-scope loads 83 us, against 69 us for two launches: one
-        wave doing 4 latency-bound rows serially costs more than the kernel boundary it saves.)"""
+        wave doing 4 latency-bound rows serially costs more than the kernel boundary it saves.  Round 2:
+        the head without its launch -- fc1 blocks atomically accumulating H1 W2^T into a logits buffer,
+        every fc_bwd block finishing log_softmax / CE / dz and building its dZ1 / dZ2 operand in LDS --
+        measured 74.3 us/step against 57.7: fc1 + 2 us (cross-XCD float atomics drain 8.8 us before the
+        next launch), fc_bwd 5.8 -> 19 us (per-block head + operand build, and 37 KB of LDS halving the
+        resident blocks); profiles/r2_lenet_v3/rejected_fused_head/.)"""
         K, p, g = self.K, self.p, self.g
         q = self.q
         if self.v2:
