@@ -222,7 +222,11 @@ class LeNetTrainStep:
         every fc_bwd block finishing log_softmax / CE / dz and building its dZ1 / dZ2 operand in LDS --
         measured 74.3 us/step against 57.7: fc1 + 2 us (cross-XCD float atomics drain 8.8 us before the
         next launch), fc_bwd 5.8 -> 19 us (per-block head + operand build, and 37 KB of LDS halving the
-        resident blocks); profiles/r2_lenet_v3/rejected_fused_head/.)"""
+        resident blocks); profiles/r2_lenet_v3/rejected_fused_head/.  Also rejected in round 2: the fc
+        parameters' Adam as extra blocks of the conv backward launch -- they dispatch only as W blocks
+        retire and end after the D chain (conv_bwd 18.5 -> 21.4 us), while the remaining conv-range
+        Adam is latency-bound on the slab folds (6.3 -> 5.6 us): 61.1 vs 57.7 us/step;
+        profiles/r2_lenet_v3/rejected_fc_adam_in_bwd/.)"""
         K, p, g = self.K, self.p, self.g
         q = self.q
         if self.v2:
