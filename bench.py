@@ -14,8 +14,9 @@ Adam update, loss/accuracy meters.  Each rank trains on its DistributedSampler s
   python bench.py --gpus N --steps K --warmup W
   (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...)
 
-Every captured hipGraph is replayed once before the W untimed warm-up steps (a graph's first launch
-pays its instantiation/upload, never inside the timed window); then exactly K steps are timed,
+Every captured hipGraph -- at both step parities of the prefetching engine, so no warm-up / step count
+can leave a capture or first launch for the timed window -- is replayed (``--prime-replays``, default
+3) before the W untimed warm-up steps; then exactly K steps are timed,
 bracketed by barrier + device synchronize on both sides; the elapsed time is the MAX over ranks;
 rank 0 prints one JSON line.  A failure still prints one JSON line (``value`` null, ``error``) and
 exits non-zero, and so does a communication-health failure (peer barrier time-out, RCCL error):
@@ -56,6 +57,8 @@ def build_parser():
     ap.add_argument("--no-autotune", action="store_true", help="W>1: skip the whole-step schedule autotuning")
     ap.add_argument("--autotune-budget-s", type=float, default=60.0,
                     help="wall-clock budget of the schedule autotuner (candidates left untimed past it)")
+    ap.add_argument("--prime-replays", type=int, default=3,
+                    help="untimed replays of each captured graph before the warm-up steps")
     ap.add_argument("--comm-figure", choices=["auto", "on", "off"], default="auto",
                     help="W=1: also time the step with RCCL initialised + the comm path on (auto = on at W=1)")
     ap.add_argument("--train-size", type=int, default=60000)
@@ -168,10 +171,9 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
         if health:
             raise RuntimeError(f"communication failure during schedule autotuning: {health}")
     if args.mode == "graph":
-        eng.capture(steps=S)
-        eng.capture(steps=1)
-        eng.replay(steps=S)                     # first launch of each graph: untimed
-        eng.replay(steps=1)
+        # both step parities of both graphs are captured and launched once before the warm-up, so no
+        # warm-up / step count can make the timed window capture or first-launch a graph
+        eng.prime_graphs((S, 1), replays=max(1, args.prime_replays))
     run(warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only

@@ -349,6 +349,36 @@ class LeNetTrainStep:
         self.graphs[(B, steps, q0)] = g
         return g
 
+    def prime_graphs(self, step_counts=(1,), B: Optional[int] = None, replays: int = 1):
+        """Capture the graphs of every step count at BOTH step parities (v2 prefetch buffers) and
+        launch each ``replays`` times (untimed first launches), leaving the parity as it was."""
+        B = B or self.B
+        q0 = self.q
+        parities = (0, 1) if self.v2 else (q0,)
+        for S in step_counts:
+            for par in parities:
+                self.q = par
+                if (B, S, par) not in self.graphs:
+                    self.capture(B, steps=S)
+        self.q = q0
+        if self.v2 and (B, 1, 0) not in self.graphs:
+            for par in (0, 1):
+                self.q = par
+                self.capture(B, steps=1)
+            self.q = q0
+        for _ in range(replays):
+            for S in step_counts:
+                if not self.v2:
+                    self.replay(B, steps=S)
+                elif S % 2:                           # odd: two replays visit both parities
+                    self.replay(B, steps=S)
+                    self.replay(B, steps=S)
+                else:                                 # even: a 1-step replay moves to the other parity
+                    self.replay(B, steps=S)
+                    self.replay(B, steps=1)
+                    self.replay(B, steps=S)
+                    self.replay(B, steps=1)
+
     def replay(self, B: Optional[int] = None, steps: int = 1):
         """Run ``steps`` steps through the (captured on first use) graph of that many steps."""
         B = B or self.B
