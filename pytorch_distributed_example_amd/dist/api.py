@@ -158,9 +158,12 @@ class _DeferredP2P(Work):
 
 
 class _Completed(Work):
+    """Handle of a collective that already completed synchronously (host-staged GPU tensors).
+    Not pre-marked done: a post-completion hook attached by the caller (e.g. DDP's copy-back of an
+    fp32-staged bucket) still runs at wait()."""
+
     def __init__(self):
         super().__init__()
-        self._done = True
 
 
 class ProcessGroup:

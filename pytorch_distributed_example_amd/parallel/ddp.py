@@ -35,6 +35,7 @@ doubles the bytes on the wire; with buckets overlapped with backward that is mos
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List
 
 import torch
@@ -89,7 +90,11 @@ class DistributedDataParallel(nn.Module):
         self._params = dict(named)
         gdt = named[0][1].dtype
         if reduce_dtype == "auto":
-            reduce_dtype = torch.float32 if gdt in (torch.bfloat16, torch.float16) else None
+            # PDE_DDP_REDUCE_DTYPE=param: reduce in the gradient dtype (torch DDP's behaviour)
+            if os.environ.get("PDE_DDP_REDUCE_DTYPE", "auto") == "param":
+                reduce_dtype = None
+            else:
+                reduce_dtype = torch.float32 if gdt in (torch.bfloat16, torch.float16) else None
         self.reduce_dtype = reduce_dtype if reduce_dtype != gdt else None
         self._stage = None
         self.set_bucket_cap(bucket_cap_mb)
