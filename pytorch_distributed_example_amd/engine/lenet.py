@@ -226,7 +226,10 @@ class LeNetTrainStep:
         parameters' Adam as extra blocks of the conv backward launch -- they dispatch only as W blocks
         retire and end after the D chain (conv_bwd 18.5 -> 21.4 us), while the remaining conv-range
         Adam is latency-bound on the slab folds (6.3 -> 5.6 us): 61.1 vs 57.7 us/step;
-        profiles/r2_lenet_v3/rejected_fc_adam_in_bwd/.)"""
+        profiles/r2_lenet_v3/rejected_fc_adam_in_bwd/.  A persistent single-launch step was not built: a
+        grid-wide barrier (one agent-scope atomic counter, co-resident blocks) measures 3.6 us at 128
+        blocks and 10.4 us at 256 against 1.5-1.6 us for a kernel boundary in a stream or hipGraph
+        (tools/native/grid_barrier_bench.hip, profiles/r2_lenet_v3/grid_barrier_vs_kernel_boundary.jsonl).)"""
         K, p, g = self.K, self.p, self.g
         q = self.q
         if self.v2:
