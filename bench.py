@@ -29,6 +29,7 @@ communicator initialised and the full W>1 communication path running (config 2 o
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import socket
@@ -65,6 +66,8 @@ def build_parser():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--model", choices=["lenet", "gpt2", "resnet18"], default="lenet",
                     help="lenet = the BASELINE headline (default); gpt2 / resnet18 = the driver-added configs")
+    ap.add_argument("--no-spin-wait", action="store_true",
+                    help="leave HIP's default host wait policy (default: hipDeviceScheduleSpin, utils/hipsched.py)")
     ap.add_argument("--seq-len", type=int, default=1024, help="gpt2: sequence length")
     ap.add_argument("--bucket-mb", type=str, default="auto",
                     help="gpt2/resnet18: DDP gradient bucket cap in MB, or 'auto' (timed sweep at W>1)")
@@ -93,6 +96,7 @@ class _Job:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = 0 if args.shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+        self.spin_wait = False
 
 
 def _comm_info(dist, comm, eng):
@@ -177,16 +181,32 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     run(warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only
+    gc_off = os.environ.get("PDE_BENCH_GC") != "1"
+    if gc_off:       # as timeit does: no Python GC pause between graph launches inside the window
+        gc.collect()
+        gc.disable()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    trace = os.environ.get("PDE_BENCH_TRACE") == "1"
+    if trace:       # diagnostics only: GPU-clocked window and host launch time, to stderr
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
     t0 = time.perf_counter()
     run(steps)
+    t_launch = time.perf_counter() - t0
+    if trace:
+        ev1.record()
     torch.cuda.synchronize()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if gc_off:
+        gc.enable()
+    if trace:
+        print(json.dumps({"trace_host_us": round(elapsed * 1e6, 1), "trace_launch_us": round(t_launch * 1e6, 1),
+                          "trace_gpu_us": round(ev0.elapsed_time(ev1) * 1e3, 1)}), file=sys.stderr)
     if comm is not None and world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -235,6 +255,7 @@ def lenet_main(job: _Job):
             "optimizer": "Adam(lr=1e-3)",
             "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
             "grad_allreduce": "none" if not eng.comm_on else eng.mode,
+            "host_wait": "spin" if job.spin_wait else "runtime default",
             **_comm_info(dist, comm, eng),
             **extra,
         },
@@ -262,6 +283,10 @@ def lenet_main(job: _Job):
 def main():
     args = build_parser().parse_args()
     job = _Job(args)
+    if not args.no_spin_wait:
+        # before any HIP context exists: spinning host waits keep the graph-launch path fast
+        from pytorch_distributed_example_amd.utils.hipsched import set_schedule
+        job.spin_wait = set_schedule(job.local_rank)
     try:
         if args.model != "lenet":
             from bench_models import run_model_bench
