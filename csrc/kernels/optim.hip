@@ -42,50 +42,27 @@ struct Fold {      // up to two replicated gradient ranges (LeNet: conv1 atomic 
   Fold1 f[2];
 };
 
-// Returns false for float4 groups that are replica storage (r >= 1): they are not parameters.
-// For canonical groups, sums the replicas into g4 (written back so p.grad holds the true gradient).
+// Folded ranges (whole replica sets [off, off + nrep*stride)) are holes of the main index space;
+// appended fold blocks own them.  Each canonical float4 gets kLS lanes: lane l sums replicas
+// l, l+kLS, ... (all loads in flight at once), a 2-step xor shuffle combines the lanes, and lane l
+// then updates element l of the float4 (the old one-thread-per-float4 fold issued 19 loads per
+// thread on the last ~27 blocks and ended the kernel 2 us after every other block).
 constexpr int kMaxFold = 16;
+constexpr int kLS = 4;
 
-__device__ __forceinline__ bool fold_grad1(const Fold1& fd, float4* g4, long long i, float4& gg) {
-  if (fd.off < 0 || fd.nrep <= 1) return true;
-  const long long e64 = 4 * i - fd.off;
-  if (e64 < 0 || e64 >= (long long)fd.stride * fd.nrep) return true;
-  const int e = (int)e64;                        // in range: 32-bit math (64-bit division is a call)
-  const int r = e / fd.stride, o = e - r * fd.stride;
-  if (r > 0) return false;
-  if (o < fd.len) {
-    // all replica loads in flight at once (a dependent-looking loop here cost ~1 us per replica)
-    const int s4 = fd.stride / 4, last = fd.nrep - 1;
-    float4 x[kMaxFold - 1];
-#pragma unroll
-    for (int k = 1; k < kMaxFold; ++k) x[k - 1] = g4[i + (long long)min(k, last) * s4];
-#pragma unroll
-    for (int k = 1; k < kMaxFold; ++k) {
-      const float w = k <= last ? 1.f : 0.f;
-      gg.x += w * x[k - 1].x; gg.y += w * x[k - 1].y; gg.z += w * x[k - 1].z; gg.w += w * x[k - 1].w;
-    }
-    g4[i] = gg;
-  }
-  return true;
-}
-
-__device__ __forceinline__ bool fold_grad(const Fold& fd, float4* g4, long long i, float4& gg) {
-  return fold_grad1(fd.f[0], g4, i, gg) && fold_grad1(fd.f[1], g4, i, gg);
-}
-
-// Replica storage (r >= 1) of the folded ranges is not parameters: the optimizer's index space skips
-// it without loading anything (the LeNet v2 conv2 slabs are 94 K float4, 46 % of the flat buffer).
 struct Holes {
   long long lo[2], len[2];   // in float4 units, sorted, lo = huge when unused
 };
+
+__host__ __device__ __forceinline__ bool fold_on(const Fold1& f) { return f.off >= 0 && f.nrep > 1; }
 
 __host__ __device__ __forceinline__ Holes make_holes(const Fold& fd) {
   Holes h{{(long long)1 << 60, (long long)1 << 60}, {0, 0}};
   for (int k = 0; k < 2; ++k) {
     const Fold1& f = fd.f[k];
-    if (f.off >= 0 && f.nrep > 1) {
-      h.lo[k] = (f.off + f.stride) / 4;
-      h.len[k] = (long long)(f.nrep - 1) * f.stride / 4;
+    if (fold_on(f)) {
+      h.lo[k] = f.off / 4;
+      h.len[k] = (long long)f.nrep * f.stride / 4;
     }
   }
   if (h.lo[1] < h.lo[0]) {
@@ -100,6 +77,44 @@ __device__ __forceinline__ long long hole_map(const Holes& h, long long c) {   /
   if (c >= h.lo[0]) c += h.len[0];
   if (c >= h.lo[1]) c += h.len[1];
   return c;
+}
+
+// fold blocks per range: kLS lanes for each float4 of the canonical slot (stride / 4 float4s)
+__host__ __device__ __forceinline__ int fold_blocks(const Fold1& f) {
+  return fold_on(f) ? (int)(((long long)f.stride / 4 * kLS + 255) / 256) : 0;
+}
+
+struct FoldLane {
+  long long e;   // flat element this lane updates (-1: none)
+  float g;       // its folded gradient (before grad_scale)
+};
+
+// fb = fold-block index (0-based over both ranges).  All lanes of the wave take part in the shuffles.
+__device__ __forceinline__ FoldLane fold_lane(const Fold& fd, float* __restrict__ g, int fb) {
+  const int nb0 = fold_blocks(fd.f[0]);
+  const int k = fb < nb0 ? 0 : 1;
+  const Fold1& f = fd.f[k];
+  const long long j = ((long long)(k ? fb - nb0 : fb) * 256 + threadIdx.x) / kLS;   // float4 in the slot
+  const int lane = threadIdx.x % kLS;
+  const bool valid = j < f.stride / 4;
+  const int nrep = (valid && 4 * j < f.len) ? f.nrep : 1;            // past len: no replicas to add
+  const float4* g4 = reinterpret_cast<const float4*>(g) + f.off / 4 + (valid ? j : 0);
+  const int s4 = f.stride / 4;
+  float4 x[kMaxFold / kLS];
+#pragma unroll
+  for (int q = 0; q < kMaxFold / kLS; ++q) {
+    const int r = lane + q * kLS;
+    x[q] = (valid && r < nrep) ? g4[(long long)r * s4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 a = x[0];
+#pragma unroll
+  for (int q = 1; q < kMaxFold / kLS; ++q) { a.x += x[q].x; a.y += x[q].y; a.z += x[q].z; a.w += x[q].w; }
+#pragma unroll
+  for (int o = 1; o < kLS; o <<= 1) {
+    a.x += __shfl_xor(a.x, o); a.y += __shfl_xor(a.y, o); a.z += __shfl_xor(a.z, o); a.w += __shfl_xor(a.w, o);
+  }
+  const float mine = lane == 0 ? a.x : lane == 1 ? a.y : lane == 2 ? a.z : a.w;
+  return FoldLane{valid ? f.off + 4 * j + lane : -1, mine};
 }
 
 __device__ __forceinline__ void pack_store(const Pack& pk, long long i, float v) {
@@ -151,6 +166,18 @@ __device__ __forceinline__ void wait_epoch(const long long* epoch, long long t, 
   __syncthreads();
 }
 
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr, float lr, float wd, int decoupled,
+                                          float omb1, float omb2, float b2, float step_size, float bc2s, float eps) {
+  if (wd != 0.f) {
+    if (decoupled) p = p * (1.f - lr * wd);
+    else gr = gr + wd * p;
+  }
+  m = m + omb1 * (gr - m);
+  v = v * b2 + omb2 * gr * gr;
+  const float denom = sqrtf(v) / bc2s + eps;
+  p = p - step_size * (m / denom);
+}
+
 template <bool PROF>
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, long long n4,
@@ -165,7 +192,8 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   __shared__ uint32_t lds2[2];
   const Holes holes = make_holes(fd);
   const long long n4c = n4 - holes.len[0] - holes.len[1];   // compressed index space (replicas skipped)
-  long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, istride = (long long)gridDim.x * blockDim.x;
+  const int nmain = (int)gridDim.x - fold_blocks(fd.f[0]) - fold_blocks(fd.f[1]);
+  long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, istride = (long long)nmain * blockDim.x;
   long long lo = 0, hi = n4c;                         // pass 1 range; pass 2 = [ar.lo4, n4c) after the wait
   if (ar.nvb > 0) {
     if ((int)blockIdx.x < ar.nvb) {
@@ -175,7 +203,7 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
       i0 = n4;                                        // no parameter work in side blocks
     } else {
       i0 = (long long)(blockIdx.x - ar.nvb) * blockDim.x + threadIdx.x;
-      istride = (long long)(gridDim.x - ar.nvb) * blockDim.x;
+      istride = (long long)(nmain - ar.nvb) * blockDim.x;
       hi = ar.lo4;
     }
   }
@@ -188,29 +216,35 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   float4* g4 = reinterpret_cast<float4*>(g);
   float4* m4 = reinterpret_cast<float4*>(m);
   float4* v4 = reinterpret_cast<float4*>(v);
+  const int nfb = fold_blocks(fd.f[0]) + fold_blocks(fd.f[1]);
+  const int fb = (int)blockIdx.x - ((int)gridDim.x - nfb);   // >= 0: fold block
   for (int pass = 0; pass < 2; ++pass) {
-  if (pass == 1) {
+  if (pass == 1 && fb < 0) {
     if (ar.nvb == 0 || (int)blockIdx.x < ar.nvb) break;   // block-uniform: wait_epoch has barriers
     wait_epoch(ar.epoch, t, ar.pd);                   // the all-reduced range is ready
     lo = ar.lo4;
     hi = n4c;
   }
+  if (fb >= 0) {                                     // fold block: its own range, one pass
+    if (pass == 1) break;
+    if (ar.nvb > 0) wait_epoch(ar.epoch, t, ar.pd);   // the reduced replicas must be complete
+    const FoldLane fl = fold_lane(fd, g, fb);
+    if (fl.e >= 0) {
+      float pa = p[fl.e], ma = m[fl.e], va = v[fl.e];
+      adam_elem(pa, ma, va, fl.g * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
+      p[fl.e] = pa; m[fl.e] = ma; v[fl.e] = va;
+      g[fl.e] = fl.g;                                  // p.grad holds the true (folded) gradient
+      pack_store(pk, fl.e, pa);
+    }
+    continue;
+  }
   for (long long ic = lo + i0; ic < hi; ic += istride) {
     const long long i = hole_map(holes, ic);
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
-    if (!fold_grad(fd, g4, i, gg)) continue;
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float gr = ga[j] * grad_scale;
-      if (wd != 0.f) {
-        if (decoupled) pa[j] = pa[j] * (1.f - lr * wd);
-        else gr = gr + wd * pa[j];
-      }
-      ma[j] = ma[j] + omb1 * (gr - ma[j]);
-      va[j] = va[j] * b2 + omb2 * gr * gr;
-      const float denom = sqrtf(va[j]) / bc2s + eps;
-      pa[j] = pa[j] - step_size * (ma[j] / denom);
+      adam_elem(pa[j], ma[j], va[j], ga[j] * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
       pack_store(pk, 4 * i + j, pa[j]);
     }
     p4[i] = pp; m4[i] = mm; v4[i] = vv;
@@ -226,6 +260,16 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   }
 }
 
+__device__ __forceinline__ void sgd_elem(float& p, float& b, float d, float lr, float momentum, float dampening,
+                                         float wd, int nesterov, long long t) {
+  if (wd != 0.f) d = d + wd * p;
+  if (momentum != 0.f) {
+    b = (t == 1) ? d : momentum * b + (1.f - dampening) * d;
+    d = nesterov ? d + momentum * b : b;
+  }
+  p = p - lr * d;
+}
+
 // torch.optim.SGD semantics (torch/optim/sgd.py): d_p = g + wd*p; buf = momentum*buf + (1-dampening)*d_p
 // (buf = d_p on the first step); d_p = nesterov ? d_p + momentum*buf : buf; p -= lr*d_p.
 __global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
@@ -238,25 +282,33 @@ __global__ __launch_bounds__(256) void k_sgd(float* __restrict__ p, float* __res
   float4* b4 = reinterpret_cast<float4*>(buf);
   const Holes holes = make_holes(fd);
   const long long n4c = n4 - holes.len[0] - holes.len[1];
-  for (long long ic = (long long)blockIdx.x * blockDim.x + threadIdx.x; ic < n4c; ic += (long long)gridDim.x * blockDim.x) {
-    const long long i = hole_map(holes, ic);
-    float4 pp = p4[i], gg = g4[i];
-    if (!fold_grad(fd, g4, i, gg)) continue;
-    float4 bb = momentum != 0.f ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float* pa = &pp.x; float* ga = &gg.x; float* ba = &bb.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = ga[j] * grad_scale;
-      if (wd != 0.f) d = d + wd * pa[j];
-      if (momentum != 0.f) {
-        ba[j] = (t == 1) ? d : momentum * ba[j] + (1.f - dampening) * d;
-        d = nesterov ? d + momentum * ba[j] : ba[j];
-      }
-      pa[j] = pa[j] - lr * d;
-      pack_store(pk, 4 * i + j, pa[j]);
+  const int nfb = fold_blocks(fd.f[0]) + fold_blocks(fd.f[1]);
+  const int fb = (int)blockIdx.x - ((int)gridDim.x - nfb);
+  if (fb >= 0) {                                       // fold block (see fold_lane)
+    const FoldLane fl = fold_lane(fd, g, fb);
+    if (fl.e >= 0) {
+      float pa = p[fl.e], ba = momentum != 0.f ? buf[fl.e] : 0.f;
+      sgd_elem(pa, ba, fl.g * grad_scale, lr, momentum, dampening, wd, nesterov, t);
+      p[fl.e] = pa;
+      if (momentum != 0.f) buf[fl.e] = ba;
+      g[fl.e] = fl.g;
+      pack_store(pk, fl.e, pa);
     }
-    p4[i] = pp;
-    if (momentum != 0.f) b4[i] = bb;
+  } else {
+    const long long istride = (long long)(gridDim.x - nfb) * blockDim.x;
+    for (long long ic = (long long)blockIdx.x * blockDim.x + threadIdx.x; ic < n4c; ic += istride) {
+      const long long i = hole_map(holes, ic);
+      float4 pp = p4[i], gg = g4[i];
+      float4 bb = momentum != 0.f ? b4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float* pa = &pp.x; float* ga = &gg.x; float* ba = &bb.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sgd_elem(pa[j], ba[j], ga[j] * grad_scale, lr, momentum, dampening, wd, nesterov, t);
+        pack_store(pk, 4 * i + j, pa[j]);
+      }
+      p4[i] = pp;
+      if (momentum != 0.f) b4[i] = bb;
+    }
   }
   if (bump > 0 && last_block(arrive, t) && threadIdx.x == 0) {
     step[0] = t;
@@ -311,13 +363,18 @@ hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, fl
   const Holes hh = make_holes(fdh);
   const long long n4c = n4 - hh.len[0] - hh.len[1];
   if (ar.nvb > 0 && (hh.len[0] || hh.len[1]) && hh.lo[0] < ar.lo4) return hipErrorInvalidValue;   // holes above ar range start
+  for (int k = 0; k < 2; ++k)
+    if (fold_on(fdh.f[k]) && (fdh.f[k].off % 4 || fdh.f[k].stride % 4 || fdh.f[k].nrep > kMaxFold ||
+                              fdh.f[k].off + (long long)fdh.f[k].nrep * fdh.f[k].stride > n))
+      return hipErrorInvalidValue;
+  const int nfb = fold_blocks(fdh.f[0]) + fold_blocks(fdh.f[1]);
   unsigned long long* prof = pde_lenet_prof_slot(5);
   if (prof)
-    hipLaunchKernelGGL(k_adam<true>, dim3(grid_for(n4c) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
+    hipLaunchKernelGGL(k_adam<true>, dim3(grid_for(n4c) + ar.nvb + nfb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
                        wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
                        Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, prof);
   else
-    hipLaunchKernelGGL(k_adam<false>, dim3(grid_for(n4c) + ar.nvb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
+    hipLaunchKernelGGL(k_adam<false>, dim3(grid_for(n4c) + ar.nvb + nfb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
                        wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
                        Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, nullptr);
   return hipGetLastError();
@@ -330,9 +387,14 @@ hipError_t pde_sgd_flat(float* p, float* g, float* buf, long long n, float lr, f
                         int fold2_stride, hipStream_t st) {
   if (n % 4) return hipErrorInvalidValue;
   const long long n4 = n / 4;
-  const Holes hh = make_holes(Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride},
-                                    Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}});
-  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4 - hh.len[0] - hh.len[1])), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
+  const Fold fdh{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}};
+  const Holes hh = make_holes(fdh);
+  for (int k = 0; k < 2; ++k)
+    if (fold_on(fdh.f[k]) && (fdh.f[k].off % 4 || fdh.f[k].stride % 4 || fdh.f[k].nrep > kMaxFold ||
+                              fdh.f[k].off + (long long)fdh.f[k].nrep * fdh.f[k].stride > n))
+      return hipErrorInvalidValue;
+  const int nfb = fold_blocks(fdh.f[0]) + fold_blocks(fdh.f[1]);
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n4 - hh.len[0] - hh.len[1]) + nfb), dim3(256), 0, st, p, g, buf, n4, lr, momentum, dampening, wd,
                      nesterov, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
                      Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}});
   return hipGetLastError();

@@ -99,6 +99,57 @@ def test_adam_kernel_matches_torch_adam():
     _close(p, pref.detach(), 0, 2e-6, "adam params")
 
 
+@pytest.mark.parametrize("opt_kind", ["adam", "sgd"])
+def test_flat_optimizer_folds_replicas(opt_kind):
+    """Two folded ranges (replica sets summed by the optimizer's fold blocks, one with a tail past
+    ``len`` that has no replicas) plus plain elements on both sides: parameters match torch's
+    optimizer fed the summed gradient, the canonical gradient slot holds that sum, and the replica
+    storage is left alone."""
+    from pytorch_distributed_example_amd._ext import kernels
+    K = kernels()
+    torch.manual_seed(1)
+    # [plain 1000][fold A: 3 reps x 64 (len 48)][plain 36][fold B: 16 reps x 1024][plain 200]
+    a_off, a_nrep, a_stride, a_len = 1000, 3, 64, 48
+    b_off, b_nrep, b_stride = a_off + a_nrep * a_stride + 36, 16, 1024
+    n = b_off + b_nrep * b_stride + 200
+    p = torch.randn(n, device=DEV)
+    p0 = p.cpu()
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    canon = torch.zeros(n, dtype=torch.bool)
+    canon[:a_off] = True
+    canon[a_off:a_off + a_stride] = True
+    canon[a_off + a_nrep * a_stride:b_off] = True
+    canon[b_off:b_off + b_stride] = True
+    canon[b_off + b_nrep * b_stride:] = True
+    pref = p.detach().cpu()[canon].clone().requires_grad_(True)
+    opt = (torch.optim.Adam([pref], lr=1e-3) if opt_kind == "adam"
+           else torch.optim.SGD([pref], lr=1e-2, momentum=0.9))
+    step = torch.zeros(1, device=DEV, dtype=torch.int64)
+    arrive = torch.zeros(1, device=DEV, dtype=torch.int32)
+    for it in range(4):
+        g = torch.randn(n)
+        gs = g.clone()
+        for off, nrep, stride, ln in ((a_off, a_nrep, a_stride, a_len), (b_off, b_nrep, b_stride, b_stride)):
+            for r in range(1, nrep):
+                gs[off:off + ln] += g[off + r * stride:off + r * stride + ln]
+        pref.grad = gs[canon].clone()
+        opt.step()
+        gd = g.to(DEV)
+        fold = dict(fold_off=b_off, fold_len=b_stride, fold_nrep=b_nrep, fold_stride=b_stride,
+                    fold2_off=a_off, fold2_len=a_len, fold2_nrep=a_nrep, fold2_stride=a_stride)
+        if opt_kind == "adam":
+            K.adam_flat(p, gd, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1.0, step, arrive, 1, **fold)
+        else:
+            K.sgd_flat(p, gd, m, 1e-2, 0.9, 0.0, 0.0, False, 1.0, step, arrive, 1, **fold)
+        torch.cuda.synchronize()
+        _close(gd.cpu()[canon], gs[canon], 1e-6, 1e-6, f"folded grad step {it}")
+        _close(gd.cpu()[~canon], g[~canon], 0, 0, f"replica storage step {it}")
+    assert int(step.item()) == 4
+    _close(p.cpu()[canon], pref.detach(), 0, 3e-6, f"{opt_kind} params")
+    _close(p.cpu()[~canon], p0[~canon], 0, 0, "replica params untouched")
+
+
 def test_engine_multi_step_tracks_torch_adam():
     B = 64
     net = build_net(seed=4, device=DEV)

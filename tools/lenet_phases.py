@@ -49,6 +49,14 @@ def analyse(buf):
                "block_start_max": round((st.max() - st.min()) * tick, 2),
                "block_dur_p50": round(float(np.median(ends - st)) * tick, 2),
                "block_dur_max": round(float((ends - st).max()) * tick, 2)}
+        if k == 5:      # optimizer: which block ranges are slow (fold / pack ranges are contiguous)
+            d = (ends - st) * tick
+            idx = np.nonzero(live)[0]
+            edges = np.linspace(0, idx.max() + 1, 17).astype(int)
+            rec["dur_by_block_range"] = {f"{edges[i]}-{edges[i + 1]}": [
+                round(float(np.median(d[(idx >= edges[i]) & (idx < edges[i + 1])])), 2),
+                round(float(d[(idx >= edges[i]) & (idx < edges[i + 1])].max()), 2)]
+                for i in range(16) if ((idx >= edges[i]) & (idx < edges[i + 1])).any()}
         if k == 0:
             rec["phases_p50"] = [round(float(np.median(rows[:, p] - st)) * tick, 2) for p in range(1, 8)
                                  if (rows[:, p] > 0).all()]
