@@ -178,13 +178,13 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
         # both step parities of both graphs are captured and launched once before the warm-up, so no
         # warm-up / step count can make the timed window capture or first-launch a graph
         eng.prime_graphs((S, 1), replays=max(1, args.prime_replays))
+    gc_off = os.environ.get("PDE_BENCH_GC") != "1"
+    if gc_off:       # as timeit does: no Python GC pause between graph launches inside the window;
+        gc.collect()     # collected BEFORE the warm-up, so the GPU does not idle (and clock down) for the
+        gc.disable()     # collection between the last warm-up step and the timed window
     run(warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only
-    gc_off = os.environ.get("PDE_BENCH_GC") != "1"
-    if gc_off:       # as timeit does: no Python GC pause between graph launches inside the window
-        gc.collect()
-        gc.disable()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()

@@ -41,18 +41,37 @@ class _FlatGroup:
         return self.layout.view(self.bufs[key], p._pde_flat[3])
 
     def sync_grads(self, params):
-        """Make every p.grad the flat view (autograd may have replaced it after zero_grad(set_to_none))."""
-        missing = False
+        """Make every p.grad the flat view (autograd may have replaced it after zero_grad(set_to_none)).
+
+        Returns the parameters whose grad was None: torch.optim skips those, so the caller saves their
+        value and state around the fused launch (``_Frozen``) instead of letting the flat kernel move them."""
+        missing = []
         for p in params:
             v = self.layout.view(self.grads, p._pde_flat[3])
             if p.grad is None:
-                missing = True
+                missing.append(p)
                 v.zero_()
-                p.grad = v
             elif p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)
                 p.grad = v
         return missing
+
+
+class _Frozen:
+    """Parameters without a gradient this step keep their value and optimizer state, as in torch.optim
+    (the flat kernel updates every element; the rare grad-None case restores the saved slices after it).
+    The device step counter is shared by the group, so such a parameter's later bias correction uses the
+    group's step count rather than a private one."""
+
+    def __init__(self, fg, params):
+        self.saved = [(p, p.detach().clone(), {k: fg.view(k, p).clone() for k in fg.bufs}) for p in params]
+        self.fg = fg
+
+    def restore(self):
+        for p, val, st in self.saved:
+            p.data.copy_(val)
+            for k, v in st.items():
+                self.fg.view(k, p).copy_(v)
 
 
 class _FusedBase(torch.optim.Optimizer):
@@ -87,6 +106,9 @@ class _FusedBase(torch.optim.Optimizer):
         for gi, group in enumerate(self.param_groups):
             if gi in self._flat:
                 self._flat[gi].grads.zero_()
+                if set_to_none:     # torch semantics: grad None until backward writes one (re-bound in step)
+                    for p in group["params"]:
+                        p.grad = None
                 continue
             for p in group["params"]:
                 if p.grad is None:
@@ -143,10 +165,12 @@ class Adam(_FusedBase):
             b1, b2 = group["betas"]
             if self._gpu_group(group):
                 fg = self._prepare(gi, group)
-                fg.sync_grads(group["params"])
+                frozen = _Frozen(fg, missing) if (missing := fg.sync_grads(group["params"])) else None
                 kernels().adam_flat(fg.params, fg.grads, fg.bufs["exp_avg"], fg.bufs["exp_avg_sq"], group["lr"], b1,
                                     b2, group["eps"], group["weight_decay"], group["decoupled_weight_decay"],
                                     self.grad_scale, fg.step_ctr, fg.arrive, 1)
+                if frozen is not None:
+                    frozen.restore()
                 self._after_step(gi, group)
             else:
                 _adam_cpu(self, group, b1, b2)
@@ -177,10 +201,12 @@ class SGD(_FusedBase):
         for gi, group in enumerate(self.param_groups):
             if self._gpu_group(group):
                 fg = self._prepare(gi, group)
-                fg.sync_grads(group["params"])
+                frozen = _Frozen(fg, missing) if (missing := fg.sync_grads(group["params"])) else None
                 kernels().sgd_flat(fg.params, fg.grads, fg.bufs["momentum_buffer"], group["lr"], group["momentum"],
                                    group["dampening"], group["weight_decay"], group["nesterov"], self.grad_scale,
                                    fg.step_ctr, fg.arrive, 1)
+                if frozen is not None:
+                    frozen.restore()
                 self._after_step(gi, group)
             else:
                 _sgd_cpu(self, group)

@@ -100,6 +100,42 @@ def test_adam_kernel_matches_torch_adam():
 
 
 @pytest.mark.parametrize("opt_kind", ["adam", "sgd"])
+def test_fused_optimizer_skips_params_without_grad(opt_kind):
+    """torch.optim leaves a parameter whose grad is None (and its state) untouched; so must the fused
+    flat-buffer optimizer, although its kernel sweeps the whole buffer."""
+    from pytorch_distributed_example_amd.optim import SGD, Adam
+    torch.manual_seed(5)
+    ps = [torch.randn(300, device=DEV, requires_grad=True), torch.randn(64, 5, device=DEV, requires_grad=True)]
+    ref = [p.detach().clone().requires_grad_() for p in ps]
+    kw = dict(lr=1e-2) if opt_kind == "adam" else dict(lr=0.1, momentum=0.9)
+    ours = (Adam if opt_kind == "adam" else SGD)(ps, **kw)
+    theirs = (torch.optim.Adam if opt_kind == "adam" else torch.optim.SGD)(ref, foreach=False, **kw)
+    for it in range(4):
+        used = [0, 1] if it % 2 == 0 else [0]       # parameter 1 gets no gradient on odd steps
+        for o in (ours, theirs):
+            o.zero_grad(set_to_none=True)
+        for i in used:
+            g = torch.randn_like(ps[i])
+            ps[i].grad = g.clone()
+            ref[i].grad = g.clone()
+        ours.step()
+        theirs.step()
+    torch.cuda.synchronize()
+    # Adam's bias correction uses the group's shared device step counter, so only the step at which the
+    # parameter was last skipped differs (it3 skipped param 1): compare param 0 tightly, param 1 after
+    # its last skip has not moved, as torch's has not.
+    _close(ps[0], ref[0], 1e-5, 1e-6, f"{opt_kind} used param")
+    if opt_kind == "sgd":
+        _close(ps[1], ref[1], 1e-5, 1e-6, "sgd skipped param")
+    before = ps[1].detach().clone()
+    ours.zero_grad(set_to_none=True)
+    ps[0].grad = torch.randn_like(ps[0])
+    ours.step()
+    torch.cuda.synchronize()
+    assert torch.equal(ps[1].detach(), before), "a parameter without grad was updated"
+
+
+@pytest.mark.parametrize("opt_kind", ["adam", "sgd"])
 def test_flat_optimizer_folds_replicas(opt_kind):
     """Two folded ranges (replica sets summed by the optimizer's fold blocks, one with a tail past
     ``len`` that has no replicas) plus plain elements on both sides: parameters match torch's
