@@ -123,6 +123,67 @@ void maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, const at::Tenso
             "maxpool3s2_bwd");
 }
 
+// ---- stem BN + ReLU + max-pool as one pass (k_bnpool_*): the post-BN map is never materialised ----
+void check_pool_shapes(const at::Tensor& y, const at::Tensor& p, const at::Tensor& arg) {
+  nhwc_rows(y, "y");
+  nhwc_rows(p, "pooled");
+  TORCH_CHECK(y.dim() == 4 && p.dim() == 4, "bnpool: 4-D channels-last tensors");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  TORCH_CHECK(C % 8 == 0 && ((C / 8) & (C / 8 - 1)) == 0 && C / 8 <= 64, "bnpool: C must be 8 * a power of two <= 512");
+  TORCH_CHECK(p.size(0) == N && p.size(1) == C && p.size(2) == (H - 1) / 2 + 1 && p.size(3) == (W - 1) / 2 + 1,
+              "bnpool: pooled must be [N, C, (H-1)/2+1, (W-1)/2+1]");
+  TORCH_CHECK(arg.is_cuda() && arg.scalar_type() == U8 && arg.numel() == p.numel() && arg.is_contiguous(),
+              "bnpool: arg must be a uint8 buffer of pooled.numel()");
+  TORCH_CHECK(y.numel() * 2 < (int64_t(1) << 31), "bnpool: y must be < 2 GiB");
+}
+
+int64_t bnpool_part_floats(int64_t N, int64_t H, int64_t C) { return pde_bnpool_part_floats((int)N, (int)H, (int)C); }
+
+// training forward: batch statistics from the conv-epilogue partials (part, pre_nblk), running-stat
+// update, then the fused BN-apply + ReLU + max-pool pass writing pooled + argmax
+void bnpool_fwd(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta, double eps, double momentum,
+                const at::Tensor& run_mean, const at::Tensor& run_var, const at::Tensor& part, int64_t pre_nblk,
+                const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift,
+                const at::Tensor& pooled, const at::Tensor& arg) {
+  check_pool_shapes(y, pooled, arg);
+  const int64_t M = nhwc_rows(y, "y"), C = y.size(1);
+  check_cuda(gamma, "gamma", BF16, C);
+  check_cuda(beta, "beta", BF16, C);
+  check_cuda(run_mean, "running_mean", F32, C);
+  check_cuda(run_var, "running_var", F32, C);
+  TORCH_CHECK(pre_nblk > 0, "bnpool_fwd: needs the producing convolution's statistics partials");
+  check_cuda(part, "part", F32, pde_bn_part_rows((int)pre_nblk) * 2 * C);
+  for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
+  hip_check(pde_bn_fwd(y.data_ptr(), nullptr, nullptr, (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
+                       (float)momentum, ptr<float>(run_mean), ptr<float>(run_var), ptr<float>(part), ptr<float>(mean),
+                       ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), 1, 1, (int)pre_nblk, cur_stream()),
+            "bnpool_fwd (finalize)");
+  hip_check(pde_bnpool_fwd(y.data_ptr(), ptr<float>(scale), ptr<float>(shift), pooled.data_ptr(), arg.data_ptr(),
+                           (int)y.size(0), (int)C, (int)y.size(2), (int)y.size(3), (int)pooled.size(2),
+                           (int)pooled.size(3), cur_stream()),
+            "bnpool_fwd");
+}
+
+void bnpool_bwd(const at::Tensor& dp, const at::Tensor& arg, const at::Tensor& y, const at::Tensor& gamma,
+                const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift,
+                const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dgamma, const at::Tensor& dbeta,
+                const at::Tensor& dy) {
+  check_pool_shapes(y, dp, arg);
+  check_same(y, dy, "dy");
+  const int64_t C = y.size(1);
+  check_cuda(gamma, "gamma", BF16, C);
+  for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
+  check_cuda(part, "part", F32, bnpool_part_floats(y.size(0), y.size(2), C));
+  check_cuda(coef, "coef", F32, 3 * C);
+  check_cuda(dgamma, "dgamma", BF16, C);
+  check_cuda(dbeta, "dbeta", BF16, C);
+  hip_check(pde_bnpool_bwd(dp.data_ptr(), arg.data_ptr(), y.data_ptr(), ptr<float>(scale), ptr<float>(shift),
+                           gamma.data_ptr(), ptr<float>(mean), ptr<float>(rstd), ptr<float>(part), ptr<float>(coef),
+                           dgamma.data_ptr(), dbeta.data_ptr(), dy.data_ptr(), (int)y.size(0), (int)C, (int)y.size(2),
+                           (int)y.size(3), (int)dp.size(2), (int)dp.size(3), cur_stream()),
+            "bnpool_bwd");
+}
+
 void sgd_master(const at::Tensor& master, const at::Tensor& p16, const at::Tensor& g16, const at::Tensor& buf,
                 double lr, double momentum, double wd, bool nesterov, double grad_scale, const OptT& decay_blk) {
   const int64_t n = master.numel();
@@ -279,6 +340,9 @@ void register_resnet(pybind11::module& m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("bnpool_part_floats", &bnpool_part_floats);
+  m.def("bnpool_fwd", &bnpool_fwd);
+  m.def("bnpool_bwd", &bnpool_bwd);
   m.def("conv_stats_blocks", &conv_stats_blocks);
   m.def("stem_stats_blocks", &stem_stats_blocks);
   m.def("stem_fwd", &stem_fwd);

@@ -346,6 +346,152 @@ __global__ __launch_bounds__(256) void k_maxpool3s2_bwd(const uint4* __restrict_
   }
 }
 
+// ------------------------------------------------------------------------------- stem BN + ReLU + max-pool
+// The stem's BatchNorm apply, ReLU and 3x3/s2/p1 max-pool as ONE pass over the conv output y: the
+// post-BN map a = relu(y*scale + shift) (411 MB at B=256) is never materialised.  Forward writes only
+// the pooled map and its window argmax; backward recomputes a's sign from y and runs two passes over y:
+//   REDUCE: d = pooling gather of dP (each input element sums the <= 2x2 windows that chose it) masked
+//           by a > 0, then the BN partials (sum d, sum d*xhat) -> part[blk][2][C]
+//   APPLY:  the same d, dy = A*d + B*y + Cc (coefficients of k_bn_bwd_finalize)
+// replacing bn_apply + maxpool fwd and maxpool bwd + bn_bwd_reduce + bn_bwd_apply (5 full passes, 2 of
+// them writing 411 MB).  One block per pooled row (fwd) / per rows_per_block input rows (bwd) of one
+// image, so the row index needs no division; blockDim is a multiple of CP (a thread's channel chunk is
+// fixed) and a thread walks the row's (column, chunk) pairs.
+__global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, uint4* __restrict__ P,
+                                                    uint2* __restrict__ Arg, int H, int W, int OH, int OW, int CP,
+                                                    int lgcp) {
+  const int oh = blockIdx.x, n = blockIdx.y, c8 = threadIdx.x & (CP - 1);
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c8 * 8 + e];
+    sf[e] = shift[c8 * 8 + e];
+  }
+  const uint4* yimg = Y + (size_t)n * H * W * CP;
+  for (int idx = threadIdx.x; idx < OW * CP; idx += blockDim.x) {
+    const int ow = idx >> lgcp;
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      arg[e] = 0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if (ih < 0 || ih >= H) continue;  // uniform over the block
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        const bool ok = iw >= 0 && iw < W;
+        float v[8];
+        unpack8(yimg[(ih * W + min(max(iw, 0), W - 1)) * CP + c8], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // the value the unfused path pooled: relu(bn(y)) rounded to bf16 (same ties, same argmax)
+          const float a = bf2f(f2bf(fmaxf(v[e] * sc[e] + sf[e], 0.f)));
+          const bool better = ok && a > best[e];
+          best[e] = better ? a : best[e];
+          arg[e] = better ? (uint32_t)(kh * 3 + kw) : arg[e];
+        }
+      }
+    }
+    const size_t o = ((size_t)(n * OH + oh) * OW + ow) * CP + c8;
+    P[o] = pack8(best);
+    Arg[o] = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
+                        arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
+  }
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(512) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
+                                                    const uint4* __restrict__ Y, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, const float* __restrict__ coef,
+                                                    float* __restrict__ part, uint4* __restrict__ dY, int H, int W,
+                                                    int OH, int OW, int CP, int lgcp, int rows_per_block) {
+  extern __shared__ float sh[];  // REDUCE: [blockDim / CP][2][C]
+  const int n = blockIdx.y, c8 = threadIdx.x & (CP - 1), C = CP * 8;
+  float sc[8], sf[8], k0[8], k1[8], k2[8], s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c8 * 8 + e;
+    sc[e] = scale[c];
+    sf[e] = shift[c];
+    if (APPLY) {
+      k0[e] = coef[c];
+      k1[e] = coef[C + c];
+      k2[e] = coef[2 * C + c];
+    } else {
+      k0[e] = mean[c];
+      k1[e] = rstd[c];
+    }
+    s[e] = q[e] = 0.f;
+  }
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(H, r0 + rows_per_block);
+  const uint4* dimg = dP + (size_t)n * OH * OW * CP;
+  const uint2* aimg = Arg + (size_t)n * OH * OW * CP;
+  for (int ih = r0; ih < r1; ++ih) {
+    const int oh0 = ih >> 1;
+    const bool oh1ok = (ih & 1) && oh0 + 1 < OH;
+    for (int idx = threadIdx.x; idx < W * CP; idx += blockDim.x) {
+      const int iw = idx >> lgcp, ow0 = iw >> 1;
+      const bool ow1ok = (iw & 1) && ow0 + 1 < OW;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const bool ok = (a == 0 || oh1ok) && (b == 0 || ow1ok);
+          const int oh = a ? min(oh0 + 1, OH - 1) : oh0, ow = b ? min(ow0 + 1, OW - 1) : ow0;
+          const int o = (oh * OW + ow) * CP + c8;
+          float g[8];
+          unpack8(dimg[o], g);
+          const uint2 ar = aimg[o];
+          const uint32_t want = (uint32_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t ae = ((e < 4 ? ar.x : ar.y) >> (8 * (e & 3))) & 0xffu;
+            acc[e] += (ok && ae == want) ? g[e] : 0.f;
+          }
+        }
+      }
+      const size_t yi = ((size_t)(n * H + ih) * W + iw) * CP + c8;
+      float y[8];
+      unpack8(Y[yi], y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
+        if (APPLY) {
+          acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
+        } else {
+          s[e] += d;
+          q[e] += d * (y[e] - k0[e]) * k1[e];
+        }
+      }
+      if (APPLY) dY[yi] = pack8(acc);
+    }
+  }
+  if (!APPLY) {
+    const int rl = threadIdx.x >> lgcp, RL = blockDim.x >> lgcp;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sh[(rl * 2 + 0) * C + c8 * 8 + e] = s[e];
+      sh[(rl * 2 + 1) * C + c8 * 8 + e] = q[e];
+    }
+    __syncthreads();
+    const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    for (int k = threadIdx.x; k < 2 * C; k += blockDim.x) {
+      const int which = k / C, c = k % C;
+      float t = 0.f;
+      for (int j = 0; j < RL; ++j) t += sh[(j * 2 + which) * C + c];
+      part[blk * 2 * C + k] = t;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------- SGD (master)
 // torch.optim.SGD semantics (coupled weight decay, dampening 0): g' = g*s + wd*p; buf = mom*buf + g'
 // (buf starts at 0, which equals torch's buf = g' on the first step); p -= lr * (nesterov ? g' + mom*buf : buf)
@@ -455,8 +601,64 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
                        shift);
   }
   const int64_t n8 = (int64_t)M * CP;
-  hipLaunchKernelGGL(k_bn_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)x, (const uint4*)res,
-                     scale, shift, (uint4*)y, n8, CP, relu);
+  if (y)   // y == nullptr: statistics / finalize only (the apply is fused into a consumer, e.g. k_bnpool_fwd)
+    hipLaunchKernelGGL(k_bn_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)x, (const uint4*)res,
+                       scale, shift, (uint4*)y, n8, CP, relu);
+  return hipGetLastError();
+}
+
+// fused stem BN + ReLU + max-pool (k_bnpool_*): launch geometry shared by the host functions below
+static int bnpool_threads(int cols_cp) {
+  const int iters = (cols_cp + 511) / 512;
+  return ((cols_cp + iters - 1) / iters + 63) / 64 * 64;
+}
+constexpr int kBnpoolRows = 4;
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+int pde_bnpool_part_floats(int N, int H, int C) {
+  const int nblk = N * ((H + kBnpoolRows - 1) / kBnpoolRows);
+  return pde_bn_part_rows(nblk) * 2 * C;
+}
+
+hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, int N, int C,
+                          int H, int W, int OH, int OW, hipStream_t st) {
+  const int CP = C / 8;
+  if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bnpool_fwd, dim3(OH, N), dim3(bnpool_threads(OW * CP)), 0, st, (const uint4*)y, scale, shift,
+                     (uint4*)p, (uint2*)arg, H, W, OH, OW, CP, ilog2(CP));
+  return hipGetLastError();
+}
+
+// part: pde_bnpool_part_floats(N, H, C) floats; coef: 3C floats
+hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const float* scale, const float* shift,
+                          const void* gamma, const float* mean, const float* rstd, float* part, float* coef,
+                          void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
+                          hipStream_t st) {
+  const int CP = C / 8;
+  if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
+  const int lg = ilog2(CP), nt = bnpool_threads(W * CP), gx = (H + kBnpoolRows - 1) / kBnpoolRows;
+  const size_t lds = (size_t)(nt / CP) * 2 * C * sizeof(float);
+  hipLaunchKernelGGL(k_bnpool_bwd<false>, dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp, (const uint2*)arg,
+                     (const uint4*)y, scale, shift, mean, rstd, (const float*)nullptr, part, (uint4*)nullptr, H, W, OH,
+                     OW, CP, lg, kBnpoolRows);
+  int nblk = gx * N;
+  float* pp = part;
+  if (nblk > kFoldThreshold) {
+    float* folded = part + (size_t)nblk * 2 * C;
+    hipLaunchKernelGGL(k_fold_rows, dim3((2 * C + 255) / 256, kFoldRows), dim3(256), 0, st, part, nblk, 2 * C,
+                       (nblk + kFoldRows - 1) / kFoldRows, folded);
+    pp = folded;
+    nblk = kFoldRows;
+  }
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, pp, nblk, C, N * H * W,
+                     (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
+  hipLaunchKernelGGL(k_bnpool_bwd<true>, dim3(gx, N), dim3(nt), 0, st, (const uint4*)dp, (const uint2*)arg,
+                     (const uint4*)y, scale, shift, mean, rstd, (const float*)coef, (float*)nullptr, (uint4*)dy, H, W,
+                     OH, OW, CP, lg, kBnpoolRows);
   return hipGetLastError();
 }
 

@@ -13,8 +13,8 @@ import math
 import torch
 import torch.nn as tnn
 
-from ..ops.resnet import (basic_block_eligible, basic_block_train, batch_norm_act, conv2d_nhwc, max_pool3s2,
-                          resnet_head)
+from ..ops.resnet import (basic_block_eligible, basic_block_train, batch_norm_act, bn_relu_maxpool, conv2d_nhwc,
+                          max_pool3s2, resnet_head)
 
 
 class BN(tnn.Module):
@@ -123,8 +123,12 @@ class ResNet(tnn.Module):
     def forward(self, x):
         if self.training:
             self._bn_counters().add_(1)
-        x = self.bn1(self.conv1(x, self.training and x.is_cuda))
-        x = max_pool3s2(x)
+        if self.training and x.is_cuda:
+            # stem BN + ReLU + max-pool as one fused node: the 64x112x112 post-BN map is never stored
+            y, stats = self.conv1(x, True)
+            x = bn_relu_maxpool(y, stats, self.bn1)
+        else:
+            x = max_pool3s2(self.bn1(self.conv1(x, False)))
         for i in range(1, 5):
             x = getattr(self, f"layer{i}")(x)
         return resnet_head(x, self.fc.weight, self.fc.bias)

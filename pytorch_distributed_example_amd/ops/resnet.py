@@ -365,6 +365,57 @@ class MaxPool3s2Fn(torch.autograd.Function):
         return dx
 
 
+class BNReluMaxPoolFn(torch.autograd.Function):
+    """Training-mode stem tail ``maxpool3x3s2(relu(bn(y)))`` as one autograd node over the stem conv's
+    output ``y`` and its fused batch-statistics partials (``k_bnpool_*`` in csrc/kernels/resnet.hip):
+    the post-BN map (the largest tensor of ResNet-18) is never written; backward recomputes the ReLU
+    mask from ``y``.  Same math, ties and argmax as BatchNormActFn followed by MaxPool3s2Fn."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, run_mean, run_var, momentum, eps, part, pre_nblk):
+        K = kernels()
+        N, C, H, W = y.shape
+        dev = y.device
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        mean, rstd, scale, shift = (torch.empty(C, device=dev, dtype=torch.float32) for _ in range(4))
+        pooled = torch.empty(N, C, OH, OW, device=dev, dtype=y.dtype, memory_format=torch.channels_last)
+        arg = torch.empty(pooled.numel(), device=dev, dtype=torch.uint8)
+        K.bnpool_fwd(y, gamma, beta, eps, momentum, run_mean, run_var, part, pre_nblk, mean, rstd, scale, shift,
+                     pooled, arg)
+        ctx.save_for_backward(y, gamma, mean, rstd, scale, shift, arg)
+        ctx.beta = beta
+        return pooled
+
+    @staticmethod
+    def backward(ctx, dp):
+        y, gamma, mean, rstd, scale, shift, arg = ctx.saved_tensors
+        K = kernels()
+        N, C, H, _ = y.shape
+        dev = y.device
+        part = torch.empty(K.bnpool_part_floats(N, H, C), device=dev, dtype=torch.float32)
+        coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
+        dgamma = flat_grad_slot(gamma)
+        dgamma = torch.empty(C, device=dev, dtype=gamma.dtype) if dgamma is None else dgamma
+        dbeta = flat_grad_slot(ctx.beta)
+        dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
+        dy = torch.empty_like(y)
+        K.bnpool_bwd(dp.contiguous(memory_format=torch.channels_last), arg, y, gamma, mean, rstd, scale, shift, part,
+                     coef, dgamma, dbeta, dy)
+        return dy, dgamma, dbeta, None, None, None, None, None, None
+
+
+def bn_relu_maxpool(y, stats, bn):
+    """``max_pool3s2(relu(bn(y)))`` for a training-mode ``BN`` module whose batch statistics ``stats``
+    (``(partials, nblk)``) came from the convolution that produced ``y``: one fused node on the GPU."""
+    C = y.shape[1]
+    if (y.is_cuda and bn.training and stats is not None and y.dim() == 4 and C % 8 == 0
+            and (C // 8) & (C // 8 - 1) == 0 and C // 8 <= 64):
+        part, nblk = stats
+        return BNReluMaxPoolFn.apply(_cl(y), bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
+                                     bn.eps, part, nblk)
+    return max_pool3s2(bn(y, stats=stats))
+
+
 def max_pool3s2(x):
     if x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0:
         return MaxPool3s2Fn.apply(x.contiguous(memory_format=torch.channels_last))

@@ -166,6 +166,56 @@ def test_maxpool3s2(shape):
     assert rel_err(x.grad, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 64, 9, 7), (3, 16, 6, 6)])
+def test_bn_relu_maxpool_fused(shape):
+    """Fused stem tail (BN apply + ReLU + max-pool forward, pooling gather + ReLU mask + BN backward in
+    two passes over y) vs the unfused kernels and an fp32 PyTorch reference."""
+    from pytorch_distributed_example_amd.models.resnet import BN
+    from pytorch_distributed_example_amd.ops.resnet import bn_relu_maxpool, max_pool3s2
+    torch.manual_seed(10)
+    N, C, H, W = shape
+    y0 = (torch.randn(N, C, H, W) * 1.3 + 0.2).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g0 = (1 + 0.2 * torch.randn(C)).to(torch.bfloat16)
+    b0 = (0.1 * torch.randn(C)).to(torch.bfloat16)
+
+    def stats_of(y):      # the conv-epilogue partials: one row of (sum, sum of squares) per channel
+        yf = y.detach().float().permute(0, 2, 3, 1).reshape(-1, C)
+        return torch.cat([yf.sum(0), (yf * yf).sum(0)]).contiguous(), 1
+
+    outs = []
+    for fused in (True, False):
+        bn = BN(C).to(dev)
+        with torch.no_grad():
+            bn.weight.copy_(g0.to(dev))
+            bn.bias.copy_(b0.to(dev))
+        bn = bn.to(torch.bfloat16)
+        y = y0.clone().requires_grad_()
+        if fused:
+            p = bn_relu_maxpool(y, stats_of(y), bn)
+            assert type(p.grad_fn).__name__ == "BNReluMaxPoolFnBackward"
+        else:
+            p = max_pool3s2(bn(y, stats=stats_of(y)))
+        torch.manual_seed(11)
+        dp = torch.randn(p.shape).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        p.backward(dp)
+        outs.append((p.detach(), y.grad, bn.weight.grad, bn.bias.grad, bn.running_mean.clone(), bn.running_var.clone()))
+    (pf, dyf, dgf, dbf, rmf, rvf), (pu, dyu, dgu, dbu, rmu, rvu) = outs
+    assert torch.equal(pf, pu)
+    assert rel_err(dyf, dyu) < 1e-2 and rel_err(dgf, dgu) < 1e-2 and rel_err(dbf, dbu) < 1e-2
+    assert torch.allclose(rmf, rmu) and torch.allclose(rvf, rvu)
+    # fp32 reference
+    yr = y0.detach().float().requires_grad_()
+    gr, br = g0.float().to(dev).requires_grad_(), b0.float().to(dev).requires_grad_()
+    pr = F.max_pool2d(F.relu(F.batch_norm(yr, torch.zeros(C, device=dev), torch.ones(C, device=dev), gr, br, True,
+                                          0.1, 1e-5)), 3, 2, 1)
+    pr.backward(dp.float())
+    assert rel_err(pf, pr) < 1e-2
+    # bf16-rounded activations tie inside pooling windows where fp32 ones do not, so a few input
+    # elements receive their window's gradient in one path and not the other: compare dy by cosine
+    assert F.cosine_similarity(dyf.float().flatten(), yr.grad.flatten(), dim=0).item() > 0.995
+    assert rel_err(dgf, gr.grad) < 3e-2 and rel_err(dbf, br.grad) < 3e-2
+
+
 def test_resnet18_grads_land_in_flat_buffer():
     """After the optimizer binds the flat buffers, conv weights stay channels-last and every
     gradient of a step is written in place into the flat gradient buffer (no per-parameter copy)."""
