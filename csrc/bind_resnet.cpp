@@ -53,14 +53,24 @@ void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at:
             "bn_fwd");
 }
 
-void bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& x, const at::Tensor& gamma,
-            const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& part, const at::Tensor& coef,
-            const at::Tensor& dgamma, const at::Tensor& dbeta, const at::Tensor& dx, const OptT& dres, bool relu) {
+// y: the forward output (ReLU mask y > 0), or None with scale / shift of the forward: the mask is
+// recomputed from x (only valid without a residual), one tensor less to read
+void bn_bwd(const at::Tensor& dy, const OptT& y, const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& mean,
+            const at::Tensor& rstd, const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dgamma,
+            const at::Tensor& dbeta, const at::Tensor& dx, const OptT& dres, bool relu, const OptT& scale,
+            const OptT& shift) {
   const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
   check_c(C);
   check_same(x, dy, "dy");
-  check_same(x, y, "y");
   check_same(x, dx, "dx");
+  const void* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_same(x, *y, "y");
+    yp = y->data_ptr();
+  }
+  const float* sc = optr<float>(scale, "scale", F32, C);
+  const float* sf = optr<float>(shift, "shift", F32, C);
+  TORCH_CHECK(!relu || yp || (sc && sf), "bn_bwd: a ReLU needs y or the forward's scale / shift");
   void* dr = nullptr;
   if (dres.has_value() && dres->defined()) {
     check_same(x, *dres, "dres");
@@ -73,9 +83,9 @@ void bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& x, cons
   check_cuda(coef, "coef", F32, 3 * C);
   check_cuda(dgamma, "dgamma", BF16, C);
   check_cuda(dbeta, "dbeta", BF16, C);
-  hip_check(pde_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), (int)M, (int)C, gamma.data_ptr(), ptr<float>(mean),
-                       ptr<float>(rstd), ptr<float>(part), ptr<float>(coef), dgamma.data_ptr(), dbeta.data_ptr(),
-                       dx.data_ptr(), dr, relu, cur_stream()),
+  hip_check(pde_bn_bwd(dy.data_ptr(), yp, x.data_ptr(), (int)M, (int)C, gamma.data_ptr(), ptr<float>(mean),
+                       ptr<float>(rstd), sc, sf, ptr<float>(part), ptr<float>(coef), dgamma.data_ptr(),
+                       dbeta.data_ptr(), dx.data_ptr(), dr, relu, cur_stream()),
             "bn_bwd");
 }
 
@@ -334,7 +344,9 @@ void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& par
 void register_resnet(pybind11::module& m) {
   m.def("bn_blocks", &bn_blocks);
   m.def("bn_fwd", &bn_fwd);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("part"), py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dx"),
+        py::arg("dres"), py::arg("relu"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("sgd_master", &sgd_master);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -159,8 +159,8 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
                       float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
                       float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk, hipStream_t st);
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
-                      const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
-                      int relu, hipStream_t st);
+                      const float* rstd, const float* scale, const float* shift, float* part, float* coef,
+                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, hipStream_t st);
 int pde_bnpool_part_floats(int N, int H, int C);
 hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, int N, int C,
                           int H, int W, int OH, int OW, hipStream_t st);

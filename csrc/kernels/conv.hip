@@ -427,18 +427,54 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
     }
 }
 
-// dW (bf16) = sum over splits of the fp32 slabs; 4 elements per thread
+// dW (bf16) = sum over splits of the fp32 slabs [splits][n].  A 256-thread block = SL split lanes x
+// 256/SL output lanes of 4 elements: the split range is walked by SL lanes in parallel (two slabs in
+// flight each) and folded through LDS, so a small weight with hundreds of splits (1x1 downsample:
+// 8192 outputs x ~200 slabs) is not one serial 200-load chain per thread on a handful of blocks.
+template <int SL>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int splits, int64_t n,
                                                       bf16_t* __restrict__ dw) {
-  const int64_t i = (blockIdx.x * 256ll + threadIdx.x) * 4;
-  if (i >= n) return;
-  float4 s = *reinterpret_cast<const float4*>(part + i);
-  for (int k = 1; k < splits; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  constexpr int OL = 256 / SL;
+  __shared__ float4 sh[SL][OL];
+  const int ol = threadIdx.x % OL, sl = threadIdx.x / OL;
+  const int64_t i = (blockIdx.x * (int64_t)OL + ol) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n) {
+    int k = sl;
+    for (; k + SL < splits; k += 2 * SL) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
+      const float4 w = *reinterpret_cast<const float4*>(part + (size_t)(k + SL) * n + i);
+      s.x += v.x + w.x; s.y += v.y + w.y; s.z += v.z + w.z; s.w += v.w + w.w;
+    }
+    if (k < splits) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
   }
+  if constexpr (SL > 1) {
+    sh[sl][ol] = s;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int j = 1; j < SL; ++j) {
+      const float4 v = sh[j][ol];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  if (i >= n) return;
   const float f[4] = {s.x, s.y, s.z, s.w};
   *reinterpret_cast<uint2*>(dw + i) = pack4(f);
+}
+
+hipError_t launch_wgrad_reduce(const float* part, int splits, int64_t n, bf16_t* dw, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  if (splits >= 32)
+    hipLaunchKernelGGL(k_wgrad_reduce<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st, part, splits, n, dw);
+  else if (splits >= 4)
+    hipLaunchKernelGGL(k_wgrad_reduce<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, part, splits, n, dw);
+  else
+    hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, part, splits, n, dw);
+  return hipGetLastError();
 }
 
 int g_conv_nst = 2;    // LDS pipeline depth of the conv kernels (2 or 3), pde_conv_set_stages
@@ -554,9 +590,7 @@ int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C) {
 // out (bf16) = sum over S fp32 slabs [S][n] (split-K partial products), n % 4 == 0
 hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hipStream_t st) {
   if (n % 4 || S < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n,
-                     (bf16_t*)out);
-  return hipGetLastError();
+  return launch_wgrad_reduce(part, S, n, (bf16_t*)out, st);
 }
 
 // part: fp32 [splits][N][T*C] scratch; dw: bf16 [N][T*C]
@@ -592,9 +626,7 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   }
   PDE_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)N * TC;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, splits, n,
-                     (bf16_t*)dw);
-  return hipGetLastError();
+  return launch_wgrad_reduce(part, splits, n, (bf16_t*)dw, st);
 }
 
 }  // extern "C"

@@ -168,20 +168,33 @@ __global__ __launch_bounds__(256) void k_bn_apply(const uint4* __restrict__ X, c
 
 // ------------------------------------------------------------------------------- backward
 // part[blk] = (sum dy', sum dy' * xhat) per channel, dy' = dy * (y > 0) when relu
+// relu: 0 none, 1 mask from the saved output Y (y > 0), 2 mask recomputed from the input X with the
+// forward's per-channel scale / shift (x*scale + shift > 0; no residual): one tensor less to read
+// (a template parameter: a runtime mode made the per-thread prologue heavy enough to slow the small
+// layer4 passes 4x)
+__device__ __forceinline__ void load8f(const float* __restrict__ p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <int RELU>
 __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__ dY, const uint4* __restrict__ Y,
                                                        const uint4* __restrict__ X, const float* __restrict__ mean,
-                                                       const float* __restrict__ rstd, int M, int C,
-                                                       int rows_per_block, int relu, float* __restrict__ part) {
+                                                       const float* __restrict__ rstd, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int M, int C,
+                                                       int rows_per_block, float* __restrict__ part) {
   extern __shared__ float sh[];
   int CP, RP;
   bn_geom(C, CP, RP);
   const int tid = threadIdx.x, c8 = tid % CP, rl = tid / CP;
-  float s[8], q[8], mu[8], rs[8];
+  float s[8], q[8], mu[8], rs[8], sc[8], sf[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    s[e] = q[e] = 0.f;
-    mu[e] = mean[c8 * 8 + e];
-    rs[e] = rstd[c8 * 8 + e];
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  load8f(mean + c8 * 8, mu);
+  load8f(rstd + c8 * 8, rs);
+  if constexpr (RELU == 2) {
+    load8f(scale + c8 * 8, sc);
+    load8f(shift + c8 * 8, sf);
   }
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rl < RP) {
@@ -190,10 +203,12 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__
       float g[8], x[8], y[8];
       unpack8(dY[i], g);
       unpack8(X[i], x);
-      if (relu) unpack8(Y[i], y);
+      if constexpr (RELU == 1) unpack8(Y[i], y);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float d = relu ? (y[e] > 0.f ? g[e] : 0.f) : g[e];
+        float d = g[e];
+        if constexpr (RELU == 1) d = y[e] > 0.f ? d : 0.f;
+        if constexpr (RELU == 2) d = x[e] * sc[e] + sf[e] > 0.f ? d : 0.f;
         s[e] += d;
         q[e] += d * (x[e] - mu[e]) * rs[e];
       }
@@ -234,28 +249,33 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restric
   coef[2 * C + c] = -A * (s / M) - Bc * mean[c];
 }
 
+template <int RELU>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint4* __restrict__ dY, const uint4* __restrict__ Y,
                                                       const uint4* __restrict__ X, const float* __restrict__ coef,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
                                                       uint4* __restrict__ dX, uint4* __restrict__ dR, int64_t n8,
-                                                      int C, int relu) {
+                                                      int C) {
   const int CP = C >> 3;
   const int64_t i0 = blockIdx.x * 256ll + threadIdx.x;
   const int c0 = (int)(i0 & (CP - 1)) * 8;
-  float ca[8], cb[8], cc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    ca[e] = coef[c0 + e];
-    cb[e] = coef[C + c0 + e];
-    cc[e] = coef[2 * C + c0 + e];
+  float ca[8], cb[8], cc[8], sc[8], sf[8];
+  load8f(coef + c0, ca);
+  load8f(coef + C + c0, cb);
+  load8f(coef + 2 * C + c0, cc);
+  if constexpr (RELU == 2) {
+    load8f(scale + c0, sc);
+    load8f(shift + c0, sf);
   }
   for (int64_t i = i0; i < n8; i += (int64_t)gridDim.x * 256) {
     float g[8], x[8], y[8], o[8];
     unpack8(dY[i], g);
     unpack8(X[i], x);
-    if (relu) unpack8(Y[i], y);
+    if constexpr (RELU == 1) unpack8(Y[i], y);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float d = relu ? (y[e] > 0.f ? g[e] : 0.f) : g[e];
+      float d = g[e];
+      if constexpr (RELU == 1) d = y[e] > 0.f ? d : 0.f;
+      if constexpr (RELU == 2) d = x[e] * sc[e] + sf[e] > 0.f ? d : 0.f;
       g[e] = d;
       o[e] = ca[e] * d + cb[e] * x[e] + cc[e];
     }
@@ -662,20 +682,26 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
   return hipGetLastError();
 }
 
+// relu with y == nullptr: the ReLU mask is recomputed from x with the forward's scale / shift (no
+// residual in the forward), so y is not read
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
-                      const float* rstd, float* part, float* coef, void* dgamma, void* dbeta, void* dx, void* dres,
-                      int relu, hipStream_t st) {
+                      const float* rstd, const float* scale, const float* shift, float* part, float* coef,
+                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, hipStream_t st) {
   if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
+  if (relu && !y && (!scale || !shift)) return hipErrorInvalidValue;
+  relu = !relu ? 0 : (y ? 1 : 2);
   const int CP = C / 8, RP = 256 / CP;
   const int nblk = pde_bn_blocks(M, C);
   const int rpb = (M + nblk - 1) / nblk;
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
-                     (const uint4*)dy, (const uint4*)y, (const uint4*)x, mean, rstd, M, C, rpb, relu, part);
+  auto red = relu == 0 ? k_bn_bwd_reduce<0> : relu == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>;
+  hipLaunchKernelGGL(red, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)dy,
+                     (const uint4*)y, (const uint4*)x, mean, rstd, scale, shift, M, C, rpb, part);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
   const int64_t n8 = (int64_t)M * CP;
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dy, (const uint4*)y,
-                     (const uint4*)x, coef, (uint4*)dx, (uint4*)dres, n8, C, relu);
+  auto app = relu == 0 ? k_bn_bwd_apply<0> : relu == 1 ? k_bn_bwd_apply<1> : k_bn_bwd_apply<2>;
+  hipLaunchKernelGGL(app, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dy, (const uint4*)y,
+                     (const uint4*)x, coef, scale, shift, (uint4*)dx, (uint4*)dres, n8, C);
   return hipGetLastError();
 }
 

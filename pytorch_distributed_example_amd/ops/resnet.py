@@ -184,10 +184,12 @@ def _bn_fwd(x, part, nblk, gamma, beta, rm, rv, momentum, eps, res, relu):
     y = torch.empty_like(x)
     mean, rstd, scale, shift = (torch.empty(C, device=dev, dtype=torch.float32) for _ in range(4))
     kernels().bn_fwd(x, res, y, gamma, beta, eps, momentum, rm, rv, part, mean, rstd, scale, shift, relu, True, nblk)
-    return y, mean, rstd
+    return y, mean, rstd, scale, shift
 
 
-def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres):
+def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shift=None):
+    """``y=None`` with the forward's ``scale`` / ``shift``: the ReLU mask is recomputed from ``x`` (BN
+    without residual), so the backward passes read two tensors instead of three."""
     K = kernels()
     C = x.shape[1]
     M = x.numel() // C
@@ -200,7 +202,7 @@ def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres):
     dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if want_dres else None
-    K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, relu)
+    K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, relu, scale, shift)
     return dx, dgamma, dbeta, dres
 
 
@@ -232,28 +234,29 @@ class BasicBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, g1, b1, w2, g2, b2, wd, gd, bd, rm1, rv1, rm2, rv2, rmd, rvd, stride, momentum, eps):
         y1, p1, n1 = _conv_fwd(x, w1, stride, 1)
-        a1, m1, s1 = _bn_fwd(y1, p1, n1, g1, b1, rm1, rv1, momentum, eps, None, True)
+        a1, m1, s1, sc1, sh1 = _bn_fwd(y1, p1, n1, g1, b1, rm1, rv1, momentum, eps, None, True)
         y2, p2, n2 = _conv_fwd(a1, w2, 1, 1)
         if wd is not None:
             yd, pd, nd = _conv_fwd(x, wd, stride, 0)
-            idt, md, sd = _bn_fwd(yd, pd, nd, gd, bd, rmd, rvd, momentum, eps, None, False)
+            idt, md, sd, _, _ = _bn_fwd(yd, pd, nd, gd, bd, rmd, rvd, momentum, eps, None, False)
         else:
             yd = md = sd = None
             idt = x                                      # identity shortcut
-        out, m2, s2 = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, idt, True)
+        out, m2, s2, _, _ = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, idt, True)
         ctx.save_for_backward(x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd,
-                              idt if wd is not None else None, m1, s1, m2, s2, md, sd)
+                              idt if wd is not None else None, m1, s1, m2, s2, md, sd, sc1, sh1)
         ctx.stride = stride
         return out
 
     @staticmethod
     def backward(ctx, dout):
         (x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd, idt, m1, s1, m2, s2, md,
-         sd) = ctx.saved_tensors
+         sd, sc1, sh1) = ctx.saved_tensors
         dout = _cl(dout)
         dy2, dg2, db2, dres = _bn_bwd(dout, out, y2, g2, b2, m2, s2, True, True)
         da1, dw2 = _conv_bwd(dy2, a1, w2, 1, 1)
-        dy1, dg1, db1, _ = _bn_bwd(da1, a1, y1, g1, b1, m1, s1, True, False)
+        # bn1 has no residual: its ReLU mask comes from y1 with the forward's scale / shift (a1 not read)
+        dy1, dg1, db1, _ = _bn_bwd(da1, None, y1, g1, b1, m1, s1, True, False, sc1, sh1)
         dwd = dgd = dbd = None
         if wd is not None:
             dyd, dgd, dbd, _ = _bn_bwd(dres, idt, yd, gd, bd, md, sd, False, False)
