@@ -259,3 +259,50 @@ def test_resnet_head_matches_fp32():
     assert rel_err(x.grad, xr.grad) < 2e-2
     assert rel_err(w.grad, wr.grad) < 2e-2
     assert rel_err(b.grad, br.grad) < 2e-2
+
+
+def test_resnet18_step_replays_as_hipgraph():
+    """The whole ResNet-18 training step (forward, loss, backward, SGDMaster) captured once into a
+    hipGraph and replayed on new batches gives the same parameters as the eager steps (bench_resnet's
+    graph mode)."""
+    from pytorch_distributed_example_amd import ops
+    torch.manual_seed(12)
+    xs = torch.randn(4, 8, 3, 64, 64).to(dev, torch.bfloat16)
+    ys = torch.randint(0, 10, (4, 8), device=dev)
+    models = []
+    for use_graph in (False, True):
+        m = build_resnet18(num_classes=10, seed=3, device=dev)
+        opt = SGDMaster(m.decay_groups(5e-5), lr=0.05, momentum=0.9)
+
+        def step(x, y):
+            opt.zero_grad()
+            loss = ops.cross_entropy(m(x).float(), y)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        sx = xs[0].contiguous(memory_format=torch.channels_last).clone()
+        sy = ys[0].clone()
+        step(sx, sy)                              # step 0 eager in both runs
+        if use_graph:
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                sx.copy_(xs[1].contiguous(memory_format=torch.channels_last))
+                sy.copy_(ys[1])
+                step(sx, sy)                      # step 1 eager (allocator warm-up)
+            torch.cuda.current_stream().wait_stream(side)
+            with torch.cuda.graph(g):
+                step(sx, sy)                      # captured, not executed
+            for i in (2, 3):
+                sx.copy_(xs[i].contiguous(memory_format=torch.channels_last))
+                sy.copy_(ys[i])
+                g.replay()
+        else:
+            for i in (1, 2, 3):
+                step(xs[i].contiguous(memory_format=torch.channels_last), ys[i])
+        torch.cuda.synchronize()
+        models.append(m)
+    for (n, a), b in zip(models[0].named_parameters(), models[1].parameters()):
+        assert torch.equal(a, b), n
