@@ -250,8 +250,11 @@ void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
             "conv_fprop");
 }
 
+// ds_dy / ds_w / ds_wt (optional): the gradient of a 1x1 / stride-2 / pad-0 downsample conv of the same
+// input (dy [B, Cout, OH, OW], weight [Cout, C, 1, 1], bf16 scratch for its transpose) accumulated into dx
+// in the same pass (extra K stages of the even-pixel phase) instead of a second dgrad + residual add
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt, const at::Tensor& dx,
-                int64_t stride, int64_t pad, const OptT& res) {
+                int64_t stride, int64_t pad, const OptT& res, const OptT& ds_dy, const OptT& ds_w, const OptT& ds_wt) {
   const ConvGeom g = conv_geom(dx, w, stride, pad);
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
@@ -266,8 +269,29 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
                 "conv dgrad: res must be a channels-last bf16 tensor shaped like dx");
     rp = res->data_ptr();
   }
-  hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), rp, (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
-                           (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, cur_stream()),
+  const void* dy2 = nullptr;
+  const void* wt2 = nullptr;
+  if (ds_dy.has_value() && ds_dy->defined()) {
+    TORCH_CHECK(ds_w.has_value() && ds_wt.has_value(), "conv dgrad: ds_dy needs ds_w and ds_wt");
+    TORCH_CHECK(stride == 2, "conv dgrad: the downsample source needs a stride-2 convolution");
+    TORCH_CHECK(ds_dy->is_cuda() && ds_dy->scalar_type() == BF16 &&
+                    ds_dy->is_contiguous(at::MemoryFormat::ChannelsLast) && ds_dy->sizes() == dy.sizes(),
+                "conv dgrad: ds_dy must be a channels-last bf16 tensor shaped like dy");
+    TORCH_CHECK(g.OH == (g.H - 1) / 2 + 1 && g.OW == (g.W - 1) / 2 + 1,
+                "conv dgrad: the downsample (1x1 / s2 / p0) output must match this convolution's output");
+    const at::Tensor& w2 = *ds_w;
+    TORCH_CHECK(w2.is_cuda() && w2.scalar_type() == BF16 && w2.dim() == 4 && w2.size(0) == g.N && w2.size(1) == g.C &&
+                    w2.size(2) == 1 && w2.size(3) == 1 && w2.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv dgrad: ds_w must be a channels-last bf16 [Cout, C, 1, 1] weight");
+    check_cuda(*ds_wt, "ds_wt", BF16, g.N * g.C);
+    hip_check(pde_conv_wtrans(w2.data_ptr(), ds_wt->data_ptr(), (int)g.N, 1, (int)g.C, cur_stream()),
+              "conv_wtrans (downsample)");
+    dy2 = ds_dy->data_ptr();
+    wt2 = ds_wt->data_ptr();
+  }
+  hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), rp, dy2, wt2, (int)g.Bn, (int)g.H, (int)g.W,
+                           (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW,
+                           cur_stream()),
             "conv_dgrad");
 }
 
@@ -364,7 +388,8 @@ void register_resnet(pybind11::module& m) {
   m.def("conv_set_stages", [](int64_t n) { pde_conv_set_stages((int)n); });
   m.def("conv_fprop", &conv_fprop);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt"), py::arg("dx"), py::arg("stride"),
-        py::arg("pad"), py::arg("res") = py::none());
+        py::arg("pad"), py::arg("res") = py::none(), py::arg("ds_dy") = py::none(), py::arg("ds_w") = py::none(),
+        py::arg("ds_wt") = py::none());
   m.def("conv_wgrad_splits", &conv_wgrad_splits);
   m.def("conv_wgrad", &conv_wgrad);
 }

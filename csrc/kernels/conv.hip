@@ -57,6 +57,7 @@ __device__ __forceinline__ void wg_frags(uint2 ab, uint2 bb, bf16x8* fa, bf16x8*
 // ============================================================================ fprop / dgrad
 struct Phase {
   int ph, pw, Hq, Wq, ntap;
+  int ntap2;                     // 1: this phase also runs the second source's stages (below)
   float inv_hw, inv_w;           // 1 / (Hq * Wq), 1 / Wq for fdiv
   // per tap, packed into one dword so the wave-uniform lookup in the K loop is a scalar load
   // (byte-sized kernarg elements become VECTOR loads, whose vmcnt wait would drain the in-flight
@@ -71,6 +72,12 @@ struct IgemmArgs {
   const bf16_t* W;      // [NC][T][CA]
   bf16_t* Y;            // NHWC [Bn][OH][OW][NC]
   const bf16_t* R;      // optional, same layout as Y: Y = bf16(acc) + R (residual-gradient accumulate)
+  // optional second K source (dgrad of a ResNet block's 1x1 / stride-2 downsample, folded into the
+  // block's conv1 dgrad): A2 is shaped like A and read at tap delta (0, 0) (the output pixel's own
+  // position), W2 = [NC][1][CA]; phases with ntap2 = 1 append CA / 64 stages over it
+  const bf16_t* A2;
+  const bf16_t* W2;
+  uint32_t a2_bytes, w2_bytes;
   float* stats;         // optional [mtiles][2][NC] (single-phase launches)
   uint32_t a_bytes, w_bytes;
   int Bn, IH, IW, CA;
@@ -109,7 +116,8 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= Mq) return;                              // whole block (phase grids differ in size)
   const int CPT = a.CA >> 6;                         // 64-channel stages per tap
-  const int KT = P.ntap * CPT;
+  const int KT1 = P.ntap * CPT;
+  const int KT = KT1 + P.ntap2 * CPT;
   const int ldw = a.T * a.CA;
 
   // ---- per-thread gather rows: instruction i fills 8-row group 4i + w, this lane row glds_row ----
@@ -140,6 +148,8 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
         const int ih = hb + (int)(signed char)(tp & 0xff), iw = wb + (int)(signed char)((tp >> 8) & 0xff);
         mk |= (tt < P.ntap && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW) ? (1u << tt) : 0u;
       }
+      // bit 9: the pixel's own position (the second source's only tap)
+      mk |= ((unsigned)hb < (unsigned)a.IH && (unsigned)wb < (unsigned)a.IW) ? (1u << 9) : 0u;
       vmask[u] = mk;
     }
   }
@@ -147,8 +157,23 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   uint32_t wrow[BI];
 #pragma unroll
   for (int v = 0; v < BI; ++v) wrow[v] = ((n0 + 8 * (4 * v + w) + lrow) * ldw + ch * 8) * 2;
+  const rsrc_t ar2 = make_rsrc(a.A2, a.a2_bytes), wr2 = make_rsrc(a.W2, a.w2_bytes);
 
   auto issue = [&](int kt, int buf) {
+    if (kt >= KT1) {                                   // second source: own position, W2 rows of CA
+      const int c0 = (kt - KT1) * 64;
+      const char* Ai = smem + buf * STAGE;
+      const char* Bi = Ai + ABYTES;
+#pragma unroll
+      for (int u = 0; u < AI; ++u) {
+        const bool ok = (vmask[u] >> 9) & 1u;
+        glds16(ar2, Ai + (4 * u + w) * 1024, ok ? (uint32_t)(aoff[u] + c0) * 2u : kOOB);
+      }
+#pragma unroll
+      for (int v = 0; v < BI; ++v)
+        glds16(wr2, Bi + (4 * v + w) * 1024, (uint32_t)(((n0 + 8 * (4 * v + w) + lrow) * a.CA + ch * 8 + c0) * 2));
+      return;
+    }
     const int tap = kt / CPT, c0 = (kt - tap * CPT) * 64;
     const int tp = P.tap[tap];
     const int dh = (int)(signed char)(tp & 0xff), dw = (int)(signed char)((tp >> 8) & 0xff), wi = tp >> 16;
@@ -538,14 +563,23 @@ hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStre
 // dX (NHWC [Bn][H][W][C]) from dY ([Bn][OH][OW][N]) and Wt = [C][R*S][N] (pde_conv_wtrans);
 // res (optional, NHWC like dX): dX = dgrad + res -- the residual / second-consumer gradient of the
 // conv input accumulated in the epilogue instead of a separate add pass
-hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, int Bn, int H, int W, int C,
-                          int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st) {
+// dy2 / wt2 (optional): a 1x1 / stride-2 / pad-0 convolution of the same input with the same output
+// shape (a ResNet downsample) whose input gradient is accumulated in the same pass: its dy2 [Bn][OH][OW][N]
+// and transposed weights wt2 [C][1][N] are K stages of the (0, 0) phase (the only input pixels it reads)
+hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, const void* dy2, const void* wt2,
+                          int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW,
+                          hipStream_t st) {
   if (C % 64 || N % 64 || R * S > 9 || stride < 1 || stride > 2) return hipErrorInvalidValue;
+  if (dy2 && (stride != 2 || !wt2 || (H - 1) / 2 + 1 != OH || (W - 1) / 2 + 1 != OW)) return hipErrorInvalidValue;
   IgemmArgs a{};
   a.A = (const bf16_t*)dy;
   a.W = (const bf16_t*)wt;
   a.Y = (bf16_t*)dx;
   a.R = (const bf16_t*)res;
+  a.A2 = (const bf16_t*)dy2;
+  a.W2 = (const bf16_t*)wt2;
+  a.a2_bytes = dy2 ? (uint32_t)((size_t)Bn * OH * OW * N * 2) : 0u;
+  a.w2_bytes = dy2 ? (uint32_t)((size_t)N * C * 2) : 0u;
   a.stats = nullptr;
   a.a_bytes = (uint32_t)((size_t)Bn * OH * OW * N * 2);
   a.w_bytes = (uint32_t)((size_t)N * R * S * C * 2);
@@ -560,6 +594,7 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* 
     P.inv_hw = 1.0f / (float)(P.Hq * P.Wq);
     P.inv_w = 1.0f / (float)P.Wq;
     P.ntap = 0;
+    P.ntap2 = (dy2 && z == 0) ? 1 : 0;
     for (int r = 0; r < R; ++r) {
       const int nh = P.ph + pad - r;
       if (((nh % stride) + stride) % stride) continue;

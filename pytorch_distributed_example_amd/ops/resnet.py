@@ -206,14 +206,19 @@ def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shif
     return dx, dgamma, dbeta, dres
 
 
-def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None):
-    """(dx [+ res, fused into the dgrad epilogue], dw)."""
+def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None):
+    """(dx [+ res, fused into the dgrad epilogue] [+ the input gradient of a 1x1 / stride-2 downsample
+    ``ds = (ds_dy, ds_w)`` of the same input, as extra K stages of the same dgrad pass], dw)."""
     K = kernels()
     dx = None
     if need_dx:
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         wt = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
-        K.conv_dgrad(dy, w, wt, dx, stride, pad, res)
+        if ds is not None:
+            ds_wt = torch.empty(ds[1].numel(), device=w.device, dtype=w.dtype)
+            K.conv_dgrad(dy, w, wt, dx, stride, pad, res, ds[0], ds[1], ds_wt)
+        else:
+            K.conv_dgrad(dy, w, wt, dx, stride, pad, res)
     splits = K.conv_wgrad_splits(x, w, stride, pad)
     part = torch.empty(splits * w.numel(), device=w.device, dtype=torch.float32)
     dw = flat_grad_slot(w)
@@ -260,11 +265,16 @@ class BasicBlockFn(torch.autograd.Function):
         dwd = dgd = dbd = None
         if wd is not None:
             dyd, dgd, dbd, _ = _bn_bwd(dres, idt, yd, gd, bd, md, sd, False, False)
-            dxd, dwd = _conv_bwd(dyd, x, wd, ctx.stride, 0, need_dx=ctx.needs_input_grad[0])
-            other = dxd
+            if ctx.stride == 2 and tuple(wd.shape[2:]) == (1, 1):
+                # the downsample's input gradient rides along conv1's dgrad as extra K stages of its
+                # even-pixel phase: no second dgrad pass, no residual read
+                _, dwd = _conv_bwd(dyd, x, wd, 2, 0, need_dx=False)
+                dx, dw1 = _conv_bwd(dy1, x, w1, 2, 1, need_dx=ctx.needs_input_grad[0], ds=(dyd, wd))
+            else:
+                dxd, dwd = _conv_bwd(dyd, x, wd, ctx.stride, 0, need_dx=ctx.needs_input_grad[0])
+                dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dxd)
         else:
-            other = dres
-        dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=other)
+            dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dres)
         return (dx, dw1, dg1, db1, dw2, dg2, db2, dwd, dgd, dbd) + (None,) * 9
 
 

@@ -151,3 +151,26 @@ def test_conv_dgrad_residual_accumulate(B, C, H, W, N, k, s, p):
     dx1 = torch.empty_like(x, memory_format=torch.channels_last)
     K.conv_dgrad(dy, w, wt, dx1, s, p, res)
     assert torch.equal(dx1, (dx0.float() + res.float()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("B,C,H,W,N", [(4, 64, 56, 56, 128), (3, 128, 14, 14, 256), (2, 64, 9, 7, 64)])
+def test_conv_dgrad_fused_downsample(B, C, H, W, N):
+    """3x3 / s2 / p1 dgrad with a 1x1 / s2 / p0 downsample's input gradient as extra K stages of the
+    even-pixel phase == fp32 sum of both input gradients (one bf16 rounding instead of two)."""
+    torch.manual_seed(12)
+    x = cl(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16))
+    w = cl((torch.randn(N, C, 3, 3, device=dev) / (C * 9) ** 0.5).to(torch.bfloat16))
+    wd = cl((torch.randn(N, C, 1, 1, device=dev) / C ** 0.5).to(torch.bfloat16))
+    y = conv2d_nhwc(x, w, 2, 1)
+    dy = cl(torch.randn_like(y))
+    dyd = cl(torch.randn_like(y))
+    K = kernels()
+    wt = torch.empty(w.numel(), device=dev, dtype=w.dtype)
+    wdt = torch.empty(wd.numel(), device=dev, dtype=w.dtype)
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    K.conv_dgrad(dy, w, wt, dx, 2, 1, None, dyd, wd, wdt)
+    xr = x.float().requires_grad_()
+    (F.conv2d(xr, w.float(), None, 2, 1) * dy.float()).sum().add_(
+        (F.conv2d(xr, wd.float(), None, 2, 0) * dyd.float()).sum()).backward()
+    err = (dx.float() - xr.grad).abs().max().item()
+    assert err <= 1e-2 * xr.grad.abs().max().item() + 1e-3, err
