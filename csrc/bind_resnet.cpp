@@ -253,15 +253,18 @@ void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 // ds_dy / ds_w / ds_wt (optional): the gradient of a 1x1 / stride-2 / pad-0 downsample conv of the same
 // input (dy [B, Cout, OH, OW], weight [Cout, C, 1, 1], bf16 scratch for its transpose) accumulated into dx
 // in the same pass (extra K stages of the even-pixel phase) instead of a second dgrad + residual add
+// wt_ready: wt (and ds_wt) already hold the transposed weights (conv_wtrans_batch), no transpose here
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt, const at::Tensor& dx,
-                int64_t stride, int64_t pad, const OptT& res, const OptT& ds_dy, const OptT& ds_w, const OptT& ds_wt) {
+                int64_t stride, int64_t pad, const OptT& res, const OptT& ds_dy, const OptT& ds_w, const OptT& ds_wt,
+                bool wt_ready) {
   const ConvGeom g = conv_geom(dx, w, stride, pad);
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
               "conv dgrad: dy must be channels-last bf16 [B, Cout, OH, OW]");
   check_cuda(wt, "wt", BF16, g.N * g.C * g.R * g.S);
-  hip_check(pde_conv_wtrans(w.data_ptr(), wt.data_ptr(), (int)g.N, (int)(g.R * g.S), (int)g.C, cur_stream()),
-            "conv_wtrans");
+  if (!wt_ready)
+    hip_check(pde_conv_wtrans(w.data_ptr(), wt.data_ptr(), (int)g.N, (int)(g.R * g.S), (int)g.C, cur_stream()),
+              "conv_wtrans");
   const void* rp = nullptr;
   if (res.has_value() && res->defined()) {
     TORCH_CHECK(res->is_cuda() && res->scalar_type() == BF16 && res->is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -284,8 +287,9 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
                     w2.size(2) == 1 && w2.size(3) == 1 && w2.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv dgrad: ds_w must be a channels-last bf16 [Cout, C, 1, 1] weight");
     check_cuda(*ds_wt, "ds_wt", BF16, g.N * g.C);
-    hip_check(pde_conv_wtrans(w2.data_ptr(), ds_wt->data_ptr(), (int)g.N, 1, (int)g.C, cur_stream()),
-              "conv_wtrans (downsample)");
+    if (!wt_ready)
+      hip_check(pde_conv_wtrans(w2.data_ptr(), ds_wt->data_ptr(), (int)g.N, 1, (int)g.C, cur_stream()),
+                "conv_wtrans (downsample)");
     dy2 = ds_dy->data_ptr();
     wt2 = ds_wt->data_ptr();
   }
@@ -293,6 +297,15 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
                            (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW,
                            cur_stream()),
             "conv_dgrad");
+}
+
+// desc: int64 GPU tensor [nconv][4] = (w ptr, wt ptr, N | T << 32, C | tile0 << 32), the WtDesc table
+void conv_wtrans_batch(const at::Tensor& desc, int64_t total) {
+  TORCH_CHECK(pde_conv_wtdesc_bytes() == 32, "conv_wtrans_batch: descriptor layout mismatch");
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 4 &&
+                  desc.is_contiguous(),
+              "conv_wtrans_batch: desc must be a contiguous int64 GPU tensor [nconv, 4]");
+  hip_check(pde_conv_wtrans_batch(desc.data_ptr(), (int)desc.size(0), (int)total, cur_stream()), "conv_wtrans_batch");
 }
 
 int64_t conv_wgrad_splits(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
@@ -389,7 +402,8 @@ void register_resnet(pybind11::module& m) {
   m.def("conv_fprop", &conv_fprop);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt"), py::arg("dx"), py::arg("stride"),
         py::arg("pad"), py::arg("res") = py::none(), py::arg("ds_dy") = py::none(), py::arg("ds_w") = py::none(),
-        py::arg("ds_wt") = py::none());
+        py::arg("ds_wt") = py::none(), py::arg("wt_ready") = false);
+  m.def("conv_wtrans_batch", &conv_wtrans_batch);
   m.def("conv_wgrad_splits", &conv_wgrad_splits);
   m.def("conv_wgrad", &conv_wgrad);
 }

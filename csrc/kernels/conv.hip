@@ -294,10 +294,10 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
 }
 
 // Wt[c][t][n] = W[n][t][c]  (64x64 tiles through LDS; grid (C/64, N/64, T))
-__global__ __launch_bounds__(256) void k_wtrans(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt, int N,
-                                                int T, int C) {
+__device__ __forceinline__ void wtrans_tile(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt, int N, int T,
+                                            int C, int c0, int n0, int tap) {
   __shared__ bf16_t sh[64][66];
-  const int c0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tap = blockIdx.z, t = threadIdx.x;
+  const int t = threadIdx.x;
   for (int e = t; e < 64 * 64; e += 256) {
     const int n = e >> 6, c = e & 63;
     sh[n][c] = W[((size_t)(n0 + n) * T + tap) * C + c0 + c];
@@ -307,6 +307,28 @@ __global__ __launch_bounds__(256) void k_wtrans(const bf16_t* __restrict__ W, bf
     const int c = e >> 6, n = e & 63;
     Wt[((size_t)(c0 + c) * T + tap) * N + n0 + n] = sh[n][c];
   }
+}
+
+__global__ __launch_bounds__(256) void k_wtrans(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt, int N,
+                                                int T, int C) {
+  wtrans_tile(W, Wt, N, T, C, blockIdx.x * 64, blockIdx.y * 64, blockIdx.z);
+}
+
+// All dgrad weight transposes of a network in ONE launch (one per step instead of one per conv
+// backward): block b finds its convolution in the descriptor table by a scan of the tile offsets.
+struct WtDesc {
+  const bf16_t* w;
+  bf16_t* wt;
+  int N, T, C, tile0;
+};
+__global__ __launch_bounds__(256) void k_wtrans_batch(const WtDesc* __restrict__ d, int nconv) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < nconv && d[i + 1].tile0 <= b) ++i;
+  const WtDesc& q = d[i];
+  const int lt = b - q.tile0, cb = q.C >> 6, nb = q.N >> 6;
+  const int cx = lt % cb, ny = (lt / cb) % nb, tap = lt / (cb * nb);
+  wtrans_tile(q.w, q.wt, q.N, q.T, q.C, cx * 64, ny * 64, tap);
 }
 
 // ============================================================================ wgrad
@@ -559,6 +581,14 @@ hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStre
   hipLaunchKernelGGL(k_wtrans, dim3(C / 64, N / 64, T), dim3(256), 0, st, (const bf16_t*)w, (bf16_t*)wt, N, T, C);
   return hipGetLastError();
 }
+
+// desc: device array of nconv WtDesc (tile0 = running sum of (C/64)*(N/64)*T); total = all tiles
+hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, hipStream_t st) {
+  if (nconv < 1 || total < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wtrans_batch, dim3(total), dim3(256), 0, st, (const WtDesc*)desc, nconv);
+  return hipGetLastError();
+}
+int pde_conv_wtdesc_bytes() { return (int)sizeof(WtDesc); }
 
 // dX (NHWC [Bn][H][W][C]) from dY ([Bn][OH][OW][N]) and Wt = [C][R*S][N] (pde_conv_wtrans);
 // res (optional, NHWC like dX): dX = dgrad + res -- the residual / second-consumer gradient of the

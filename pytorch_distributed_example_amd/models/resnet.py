@@ -13,8 +13,8 @@ import math
 import torch
 import torch.nn as tnn
 
-from ..ops.resnet import (basic_block_eligible, basic_block_train, batch_norm_act, bn_relu_maxpool, conv2d_nhwc,
-                          max_pool3s2, resnet_head)
+from ..ops.resnet import (DgradWeights, basic_block_eligible, basic_block_train, batch_norm_act, bn_relu_maxpool,
+                          conv2d_nhwc, max_pool3s2, resnet_head)
 
 
 class BN(tnn.Module):
@@ -120,9 +120,25 @@ class ResNet(tnn.Module):
             self.__dict__["_nbt_shared"] = sh
         return sh
 
+    def _dgrad_weights(self):
+        """Every block convolution weight whose input gradient the backward computes (all but the stem),
+        in a fixed order, for the one batched transpose launch per training forward."""
+        ws = []
+        for i in range(1, 5):
+            for blk in getattr(self, f"layer{i}"):
+                ws += [blk.conv1.weight, blk.conv2.weight]
+                if blk.downsample is not None:
+                    ws.append(blk.downsample[0].weight)
+        return ws
+
     def forward(self, x):
         if self.training:
             self._bn_counters().add_(1)
+        if self.training and x.is_cuda:
+            ws = self._dgrad_weights()
+            if all(w.is_contiguous(memory_format=torch.channels_last) and w.shape[0] % 64 == 0
+                   and w.shape[1] % 64 == 0 for w in ws):
+                self.__dict__.setdefault("_wt_cache", DgradWeights()).refresh(ws)
         if self.training and x.is_cuda:
             # stem BN + ReLU + max-pool as one fused node: the 64x112x112 post-BN map is never stored
             y, stats = self.conv1(x, True)

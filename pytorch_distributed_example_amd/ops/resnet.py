@@ -206,19 +206,58 @@ def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shif
     return dx, dgamma, dbeta, dres
 
 
-def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None):
+class DgradWeights:
+    """Transposed copies Wt[c][tap][n] of every dgrad convolution weight of a network, made by ONE
+    batched launch per training forward (``k_wtrans_batch``) instead of one transpose kernel inside
+    each convolution's backward (19 launches per ResNet-18 step).  ``refresh`` attaches each copy to
+    its weight as ``_pde_wt``; the BasicBlock forward takes it (so a copy is used by exactly the
+    backward of the forward that made it) and its backward passes it to the dgrad as ready."""
+
+    def __init__(self):
+        self.key = None
+
+    def refresh(self, weights):
+        key = tuple((w.data_ptr(), tuple(w.shape)) for w in weights)
+        if key != self.key:               # (re)built outside graph capture: the warm-up steps see it first
+            dev = weights[0].device
+            self.buf = torch.empty(sum(w.numel() for w in weights), device=dev, dtype=weights[0].dtype)
+            rows, self.views, tile, off = [], [], 0, 0
+            for w in weights:
+                N, C, R, S = w.shape
+                v = self.buf[off: off + w.numel()]
+                rows.append([w.data_ptr(), v.data_ptr(), N | ((R * S) << 32), C | (tile << 32)])
+                tile += (C // 64) * (N // 64) * R * S
+                off += w.numel()
+                self.views.append(v)
+            self.desc = torch.tensor(rows, dtype=torch.int64).to(dev)
+            self.total, self.key = tile, key
+        kernels().conv_wtrans_batch(self.desc, self.total)
+        for w, v in zip(weights, self.views):
+            w._pde_wt = v
+
+
+def _take_wt(w):
+    """The batched transposed copy of ``w`` made by this forward's ``DgradWeights.refresh`` (or None)."""
+    v = w.__dict__.pop("_pde_wt", None) if w is not None else None
+    return v
+
+
+def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None, wt=None, ds_wt=None):
     """(dx [+ res, fused into the dgrad epilogue] [+ the input gradient of a 1x1 / stride-2 downsample
-    ``ds = (ds_dy, ds_w)`` of the same input, as extra K stages of the same dgrad pass], dw)."""
+    ``ds = (ds_dy, ds_w)`` of the same input, as extra K stages of the same dgrad pass], dw).
+    ``wt`` / ``ds_wt``: transposed weights already made by ``DgradWeights`` (else transposed here)."""
     K = kernels()
     dx = None
     if need_dx:
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        wt = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
+        ready = wt is not None and (ds is None or ds_wt is not None)
+        if not ready:
+            wt = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
+            ds_wt = torch.empty(ds[1].numel(), device=w.device, dtype=w.dtype) if ds is not None else None
         if ds is not None:
-            ds_wt = torch.empty(ds[1].numel(), device=w.device, dtype=w.dtype)
-            K.conv_dgrad(dy, w, wt, dx, stride, pad, res, ds[0], ds[1], ds_wt)
+            K.conv_dgrad(dy, w, wt, dx, stride, pad, res, ds[0], ds[1], ds_wt, wt_ready=ready)
         else:
-            K.conv_dgrad(dy, w, wt, dx, stride, pad, res)
+            K.conv_dgrad(dy, w, wt, dx, stride, pad, res, wt_ready=ready)
     splits = K.conv_wgrad_splits(x, w, stride, pad)
     part = torch.empty(splits * w.numel(), device=w.device, dtype=torch.float32)
     dw = flat_grad_slot(w)
@@ -251,6 +290,7 @@ class BasicBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd,
                               idt if wd is not None else None, m1, s1, m2, s2, md, sd, sc1, sh1)
         ctx.stride = stride
+        ctx.wts = (_take_wt(w1), _take_wt(w2), _take_wt(wd))   # batched dgrad transposes (or None)
         return out
 
     @staticmethod
@@ -258,8 +298,9 @@ class BasicBlockFn(torch.autograd.Function):
         (x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd, idt, m1, s1, m2, s2, md,
          sd, sc1, sh1) = ctx.saved_tensors
         dout = _cl(dout)
+        wt1, wt2, wtd = ctx.wts
         dy2, dg2, db2, dres = _bn_bwd(dout, out, y2, g2, b2, m2, s2, True, True)
-        da1, dw2 = _conv_bwd(dy2, a1, w2, 1, 1)
+        da1, dw2 = _conv_bwd(dy2, a1, w2, 1, 1, wt=wt2)
         # bn1 has no residual: its ReLU mask comes from y1 with the forward's scale / shift (a1 not read)
         dy1, dg1, db1, _ = _bn_bwd(da1, None, y1, g1, b1, m1, s1, True, False, sc1, sh1)
         dwd = dgd = dbd = None
@@ -269,12 +310,13 @@ class BasicBlockFn(torch.autograd.Function):
                 # the downsample's input gradient rides along conv1's dgrad as extra K stages of its
                 # even-pixel phase: no second dgrad pass, no residual read
                 _, dwd = _conv_bwd(dyd, x, wd, 2, 0, need_dx=False)
-                dx, dw1 = _conv_bwd(dy1, x, w1, 2, 1, need_dx=ctx.needs_input_grad[0], ds=(dyd, wd))
+                dx, dw1 = _conv_bwd(dy1, x, w1, 2, 1, need_dx=ctx.needs_input_grad[0], ds=(dyd, wd), wt=wt1,
+                                    ds_wt=wtd)
             else:
-                dxd, dwd = _conv_bwd(dyd, x, wd, ctx.stride, 0, need_dx=ctx.needs_input_grad[0])
-                dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dxd)
+                dxd, dwd = _conv_bwd(dyd, x, wd, ctx.stride, 0, need_dx=ctx.needs_input_grad[0], wt=wtd)
+                dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dxd, wt=wt1)
         else:
-            dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dres)
+            dx, dw1 = _conv_bwd(dy1, x, w1, ctx.stride, 1, need_dx=ctx.needs_input_grad[0], res=dres, wt=wt1)
         return (dx, dw1, dg1, db1, dw2, dg2, db2, dwd, dgd, dbd) + (None,) * 9
 
 
