@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ P2, co
       const int i = t >> 4, j = t & 15, gm = mt * 16 + i, gn = nt * 16 + j;
       const float v = red[0][i][j] + red[1][i][j] + red[2][i][j] + red[3][i][j];
       if (gm < kHid) {
-        if (!bias_tile) gW1[(size_t)gm * kFeat + gn] = v;
+        if (!bias_tile) __builtin_nontemporal_store(v, gW1 + (size_t)gm * kFeat + gn);   // read by Adam only
         else if (gn == kFeat) gb1[gm] = v;
       }
     }

@@ -149,9 +149,14 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   // ---- P1 / A1 for backward (this block's 10 channels): issued now, they drain under conv2 ----
   if (t < 360) {
     const int c0 = ct * 10 * 144;
-    reinterpret_cast<float4*>(P1 + (size_t)b * kP1 + c0)[t] = reinterpret_cast<const float4*>(smem + kL_XS + c0)[t];
-    reinterpret_cast<uint32_t*>(A1 + (size_t)b * kP1 + c0)[t] =
-        reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem + kL_CODE) + c0)[t];
+    // non-temporal: read again only by the conv backward three kernels later, so these 1.8 MB are
+    // streamed out instead of sitting dirty in the XCD L2s for the end-of-kernel write-back
+    typedef float nt_f4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(reinterpret_cast<const nt_f4*>(smem + kL_XS + c0)[t],
+                                reinterpret_cast<nt_f4*>(P1 + (size_t)b * kP1 + c0) + t);
+    __builtin_nontemporal_store(
+        reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem + kL_CODE) + c0)[t],
+        reinterpret_cast<uint32_t*>(A1 + (size_t)b * kP1 + c0) + t);
   }
   // ---- phase 2: conv2 (20->50, 5x5): wave = (co tile of 16, 4x4 pixel tile), K = 500 ----
   const int oh = (pxt >> 1) * 4 + (j >> 2), ow = (pxt & 1) * 4 + (j & 3);

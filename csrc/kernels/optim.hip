@@ -247,7 +247,12 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
       adam_elem(pa[j], ma[j], va[j], ga[j] * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
       pack_store(pk, 4 * i + j, pa[j]);
     }
-    p4[i] = pp; m4[i] = mm; v4[i] = vv;
+    p4[i] = pp;
+    // the moments are read again only by the next step's Adam: streamed out (non-temporal) rather than
+    // left dirty in the XCD L2s for the end-of-kernel write-back that the next kernel waits behind
+    typedef float nt_f4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&mm), reinterpret_cast<nt_f4*>(m4 + i));
+    __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&vv), reinterpret_cast<nt_f4*>(v4 + i));
   }
   }
   if (bump > 0 && last_block(arrive, t) && threadIdx.x == 0) {
