@@ -66,26 +66,34 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint4* __restrict__ X, i
 }
 
 // Sum the [nblk][2C] partials of the 64 channels [64*blockIdx.x, +64): 1024 threads = 64 channel
-// lanes x 16 waves striding over the partial rows (4 independent accumulators each), LDS fold.
+// lanes x 16 waves striding over the partial rows, LDS fold.  Each lane keeps 8 row loads in flight
+// (these folds are latency-bound: with 2 in flight, 512 rows cost 16 dependent round trips, ~7 us).
 __device__ __forceinline__ void fold_partials(const float* __restrict__ part, int nblk, int C, int c, float& s,
                                               float& q) {
   __shared__ float sh[16][2][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cc = min(c, C - 1);
-  float s0 = 0.f, s1 = 0.f, q0 = 0.f, q1 = 0.f;
+  float sa[4] = {0.f, 0.f, 0.f, 0.f}, qa[4] = {0.f, 0.f, 0.f, 0.f};
   int b = w;
-  for (; b + 16 < nblk; b += 32) {
-    s0 += part[(size_t)b * 2 * C + cc];
-    q0 += part[(size_t)b * 2 * C + C + cc];
-    s1 += part[(size_t)(b + 16) * 2 * C + cc];
-    q1 += part[(size_t)(b + 16) * 2 * C + C + cc];
+  for (; b + 48 < nblk; b += 64) {
+    float sv[4], qv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = part[(size_t)(b + 16 * u) * 2 * C + cc];
+      qv[u] = part[(size_t)(b + 16 * u) * 2 * C + C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sa[u] += sv[u];
+      qa[u] += qv[u];
+    }
   }
   for (; b < nblk; b += 16) {
-    s0 += part[(size_t)b * 2 * C + cc];
-    q0 += part[(size_t)b * 2 * C + C + cc];
+    sa[0] += part[(size_t)b * 2 * C + cc];
+    qa[0] += part[(size_t)b * 2 * C + C + cc];
   }
-  sh[w][0][lane] = s0 + s1;
-  sh[w][1][lane] = q0 + q1;
+  sh[w][0][lane] = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+  sh[w][1][lane] = (qa[0] + qa[1]) + (qa[2] + qa[3]);
   __syncthreads();
   s = 0.f;
   q = 0.f;
@@ -99,20 +107,24 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
 }
 
 // out[y][c] = sum of partial rows [y*rows_per, (y+1)*rows_per) of part[nblk][W]: folds the many
-// per-tile partials of a conv epilogue (thousands of rows) before the per-channel finalize.
+// per-tile partials of a conv epilogue (thousands of rows) before the per-channel finalize
+// (8 rows in flight per thread).
 __global__ __launch_bounds__(256) void k_fold_rows(const float* __restrict__ part, int nblk, int W, int rows_per,
                                                    float* __restrict__ out) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= W) return;
   const int r0 = blockIdx.y * rows_per, r1 = min(nblk, r0 + rows_per);
-  float s0 = 0.f, s1 = 0.f;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int r = r0;
-  for (; r + 1 < r1; r += 2) {
-    s0 += part[(size_t)r * W + c];
-    s1 += part[(size_t)(r + 1) * W + c];
+  for (; r + 7 < r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + u) * W + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
   }
-  if (r < r1) s0 += part[(size_t)r * W + c];
-  out[(size_t)blockIdx.y * W + c] = s0 + s1;
+  for (; r < r1; ++r) a[0] += part[(size_t)r * W + c];
+  out[(size_t)blockIdx.y * W + c] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // per channel: mean / biased var -> rstd, running-stat update (unbiased var), scale / shift
