@@ -437,6 +437,11 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
   }
 }
 
+// Backward, one thread per POOLED cell (oh, ow, chunk) handling the 2x2 input block (2oh + i, 2ow + j):
+// an even input row / column is covered by window oh / ow only, an odd one by oh and oh + 1, so the
+// four windows {oh, oh+1} x {ow, ow+1} (4 gradient + 4 argmax loads) serve all four input elements
+// (12 loads per 4 output chunks instead of 9 per chunk gathering from each input element).  A block
+// covers rows_per_block pooled rows (2 x as many input rows) of one image.
 template <bool APPLY>
 __global__ __launch_bounds__(512) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
                                                     const uint4* __restrict__ Y, const float* __restrict__ scale,
@@ -462,48 +467,62 @@ __global__ __launch_bounds__(512) void k_bnpool_bwd(const uint4* __restrict__ dP
     }
     s[e] = q[e] = 0.f;
   }
-  const int r0 = blockIdx.x * rows_per_block, r1 = min(H, r0 + rows_per_block);
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(OH, r0 + rows_per_block);
   const uint4* dimg = dP + (size_t)n * OH * OW * CP;
   const uint2* aimg = Arg + (size_t)n * OH * OW * CP;
-  for (int ih = r0; ih < r1; ++ih) {
-    const int oh0 = ih >> 1;
-    const bool oh1ok = (ih & 1) && oh0 + 1 < OH;
-    for (int idx = threadIdx.x; idx < W * CP; idx += blockDim.x) {
-      const int iw = idx >> lgcp, ow0 = iw >> 1;
-      const bool ow1ok = (iw & 1) && ow0 + 1 < OW;
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int oh = r0; oh < r1; ++oh) {
+    for (int idx = threadIdx.x; idx < OW * CP; idx += blockDim.x) {
+      const int ow = idx >> lgcp;
+      float g[2][2][8];
+      uint2 ar[2][2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-          const bool ok = (a == 0 || oh1ok) && (b == 0 || ow1ok);
-          const int oh = a ? min(oh0 + 1, OH - 1) : oh0, ow = b ? min(ow0 + 1, OW - 1) : ow0;
-          const int o = (oh * OW + ow) * CP + c8;
-          float g[8];
-          unpack8(dimg[o], g);
-          const uint2 ar = aimg[o];
-          const uint32_t want = (uint32_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+          const int o = (min(oh + a, OH - 1) * OW + min(ow + b, OW - 1)) * CP + c8;
+          unpack8(dimg[o], g[a][b]);
+          ar[a][b] = aimg[o];
+        }
+      const bool aok = oh + 1 < OH, bok = ow + 1 < OW;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ih = 2 * oh + i;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int iw = 2 * ow + j;
+          if (ih >= H || iw >= W) continue;
+          const size_t yi = ((size_t)(n * H + ih) * W + iw) * CP + c8;
+          float y[8];
+          unpack8(Y[yi], y);
+          float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            if (a > i) continue;                       // window row oh+1 covers odd rows only
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              if (b > j) continue;
+              const bool ok = (a == 0 || aok) && (b == 0 || bok);
+              const uint32_t want = (uint32_t)((i - 2 * a + 1) * 3 + (j - 2 * b + 1));
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const uint32_t ae = ((e < 4 ? ar[a][b].x : ar[a][b].y) >> (8 * (e & 3))) & 0xffu;
+                acc[e] += (ok && ae == want) ? g[a][b][e] : 0.f;
+              }
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const uint32_t ae = ((e < 4 ? ar.x : ar.y) >> (8 * (e & 3))) & 0xffu;
-            acc[e] += (ok && ae == want) ? g[e] : 0.f;
+            const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
+            if (APPLY) {
+              acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
+            } else {
+              s[e] += d;
+              q[e] += d * (y[e] - k0[e]) * k1[e];
+            }
           }
+          if (APPLY) dY[yi] = pack8(acc);
         }
       }
-      const size_t yi = ((size_t)(n * H + ih) * W + iw) * CP + c8;
-      float y[8];
-      unpack8(Y[yi], y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
-        if (APPLY) {
-          acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
-        } else {
-          s[e] += d;
-          q[e] += d * (y[e] - k0[e]) * k1[e];
-        }
-      }
-      if (APPLY) dY[yi] = pack8(acc);
     }
   }
   if (!APPLY) {
@@ -651,8 +670,10 @@ static int ilog2(int v) {
   return l;
 }
 
+// blocks of the backward passes: kBnpoolRows / 2 pooled rows (kBnpoolRows input rows) of one image
 int pde_bnpool_part_floats(int N, int H, int C) {
-  const int nblk = N * ((H + kBnpoolRows - 1) / kBnpoolRows);
+  const int OH = (H - 1) / 2 + 1, rows = kBnpoolRows / 2;
+  const int nblk = N * ((OH + rows - 1) / rows);
   return pde_bn_part_rows(nblk) * 2 * C;
 }
 
@@ -672,11 +693,11 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
                           hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
-  const int lg = ilog2(CP), nt = bnpool_threads(W * CP), gx = (H + kBnpoolRows - 1) / kBnpoolRows;
+  const int lg = ilog2(CP), nt = bnpool_threads(OW * CP), rows = kBnpoolRows / 2, gx = (OH + rows - 1) / rows;
   const size_t lds = (size_t)(nt / CP) * 2 * C * sizeof(float);
   hipLaunchKernelGGL(k_bnpool_bwd<false>, dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp, (const uint2*)arg,
                      (const uint4*)y, scale, shift, mean, rstd, (const float*)nullptr, part, (uint4*)nullptr, H, W, OH,
-                     OW, CP, lg, kBnpoolRows);
+                     OW, CP, lg, rows);
   int nblk = gx * N;
   float* pp = part;
   if (nblk > kFoldThreshold) {
@@ -690,7 +711,7 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
   hipLaunchKernelGGL(k_bnpool_bwd<true>, dim3(gx, N), dim3(nt), 0, st, (const uint4*)dp, (const uint2*)arg,
                      (const uint4*)y, scale, shift, mean, rstd, (const float*)coef, (float*)nullptr, (uint4*)dy, H, W,
-                     OH, OW, CP, lg, kBnpoolRows);
+                     OH, OW, CP, lg, rows);
   return hipGetLastError();
 }
 
