@@ -234,6 +234,12 @@ ConvGeom conv_geom(const at::Tensor& x, const at::Tensor& w, int64_t stride, int
 }
 
 int64_t conv_stats_blocks(int64_t M, int64_t N) { return pde_conv_fprop_mtiles((int)M, (int)N); }
+// rows of BN partials conv_fprop writes for this convolution (the halo-tiled kernel tiles by image rows)
+int64_t conv_stats_rows(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  const ConvGeom g = conv_geom(x, w, stride, pad);
+  return pde_conv_stats_rows((int)g.Bn, (int)g.H, (int)g.W, (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride,
+                             (int)pad, (int)g.OH, (int)g.OW);
+}
 // rows to allocate for a conv-stats buffer that feeds bn_fwd (partials + the finalize's pre-fold)
 int64_t bn_part_rows(int64_t nblk) { return pde_bn_part_rows((int)nblk); }
 
@@ -244,7 +250,7 @@ void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
                   y.size(0) == g.Bn && y.size(1) == g.N && y.size(2) == g.OH && y.size(3) == g.OW,
               "conv: y must be channels-last bf16 [B, Cout, OH, OW]");
   const int64_t M = g.Bn * g.OH * g.OW;
-  float* sp = optr<float>(stats, "stats", F32, conv_stats_blocks(M, g.N) * 2 * g.N);
+  float* sp = optr<float>(stats, "stats", F32, conv_stats_rows(x, w, stride, pad) * 2 * g.N);
   hip_check(pde_conv_fprop(x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)g.Bn, (int)g.H, (int)g.W, (int)g.C,
                            (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, cur_stream()),
             "conv_fprop");
@@ -393,6 +399,7 @@ void register_resnet(pybind11::module& m) {
   m.def("bnpool_fwd", &bnpool_fwd);
   m.def("bnpool_bwd", &bnpool_bwd);
   m.def("conv_stats_blocks", &conv_stats_blocks);
+  m.def("conv_stats_rows", &conv_stats_rows);
   m.def("stem_stats_blocks", &stem_stats_blocks);
   m.def("stem_fwd", &stem_fwd);
   m.def("stem_wgrad_blocks", &stem_wgrad_blocks);

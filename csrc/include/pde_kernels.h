@@ -115,6 +115,7 @@ hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, 
 // ---- implicit-GEMM bf16 convolutions, NHWC (conv.hip) ----
 void pde_conv_set_stages(int nst);
 int pde_conv_fprop_mtiles(int M, int N);
+int pde_conv_stats_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW);
 // ResNet stem (7x7 / stride 2 / pad 3, 3 -> 64 ch, NHWC bf16): stem.hip
 int pde_stem_stats_blocks(int Bn, int OH);
 hipError_t pde_stem_fwd(const void* X, const void* W, void* Wp, void* Y, float* stats, int Bn, int H, int Wd,

@@ -474,6 +474,369 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
     }
 }
 
+// ============================================================================ halo-tiled 3x3 / stride 1
+// The implicit GEMM above re-fetches its A operand through L2 once per tap (9x for a 3x3 conv): at
+// C = 64 (layer1) a stage is 40 KB of DMA for 2 MFLOP, and the kernel runs at the L2 -> LDS rate.
+// k_hconv stages, per 64-channel chunk, the HALO of a block of TH full output rows once --
+// (TH + 2) x (W + 2) input pixels, out-of-image pixels zero-filled by the bounded buffer load -- and
+// reads all nine taps' A fragments from it (a tap is a constant shift of the halo pixel index), so
+// only the weights stream per tap (double-buffered).  Block = TH rows x W columns of output pixels
+// (<= BM, rounded up to MFMA tiles), BN output channels; 4 waves of 64 x 64 as in k_igemm, and the
+// same epilogue (bf16 tile through LDS, BN statistics partials, residual add).  Used for stride-1
+// 3x3 / pad-1 fprop and dgrad (the dgrad of a stride-1 conv is the flipped-tap conv of dy with Wt).
+struct HconvArgs {
+  const bf16_t* A;      // NHWC [Bn][H][W][CA]
+  const bf16_t* Wg;     // [NC][9][CA]
+  bf16_t* Y;            // NHWC [Bn][H][W][NC]
+  const bf16_t* R;      // optional, like Y: Y = bf16(acc) + R
+  float* stats;         // optional [Bn * rtiles][2][NC]
+  uint32_t a_bytes, w_bytes;
+  int Bn, H, W, CA, NC;
+  int TH, rtiles, ntiles;
+  int tap[9];           // pack_tap(dh, dw, widx)
+};
+
+template <int BM> constexpr int hconv_groups() { return BM == 256 ? 50 : 33; }   // 8-pixel halo groups
+
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
+  constexpr int WN = BN / 64, WM = 4 / WN;
+  static_assert(WM * 64 == BM, "wave grid must tile BM x BN with 64x64 wave tiles");
+  constexpr int HG = hconv_groups<BM>(), HU = (HG + 3) / 4;   // halo groups, glds per wave
+  constexpr int HBYTES = HG * 1024;
+  constexpr int BI = BN / 32, BBYTES = BN * 128;
+  constexpr int RS = BN * 2 + 16;
+  constexpr int EPIB = BM * RS + 2 * WM * BN * 4;
+  constexpr int SMEM = HBYTES + 2 * BBYTES > EPIB ? HBYTES + 2 * BBYTES : EPIB;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char* halo = smem;
+  char* bimg = smem + HBYTES;
+
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = id % a.ntiles, mt = id / a.ntiles;
+  const int b = mt / a.rtiles, rt = mt - b * a.rtiles;
+  const int oh0 = rt * a.TH, rows = min(a.TH, a.H - oh0), npx = rows * a.W;
+  const int n0 = nt * BN, HW2 = a.W + 2;
+  const int CPT = a.CA >> 6, ldw = 9 * a.CA;
+
+  // ---- halo DMA sources: group g = w + 4u, lane row glds_row, chunk glds_chunk (group parity = w & 1) ----
+  const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
+  uint32_t hoff[HU];
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const int hr = 8 * (w + 4 * u) + lrow;
+    const int hy = hr / HW2, hx = hr - hy * HW2;
+    const int ih = oh0 - 1 + hy, iw = hx - 1;
+    const bool ok = hy < a.TH + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    hoff[u] = ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * a.CA + ch * 8) * 2) : kOOB;
+  }
+  uint32_t wrow[BI];
+#pragma unroll
+  for (int v = 0; v < BI; ++v) wrow[v] = (uint32_t)(((n0 + 8 * (4 * v + w) + lrow) * ldw + ch * 8) * 2);
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), wr = make_rsrc(a.Wg, a.w_bytes);
+
+  // ---- this lane's MFMA A rows: pixel p of tile i -> halo index of its tap-(0,0) input ----
+  const int wm = w / WN, wn = w % WN, lr = l & 31, lh = l >> 5;
+  int hbase[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int p = wm * 64 + i * 32 + lr;
+    p = p < npx ? p : 0;                               // masked in the epilogue
+    const int py = p / a.W, px = p - py * a.W;
+    hbase[i] = (py + 1) * HW2 + px + 1;
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
+
+  auto issue_b = [&](int tap, int c0, int buf) {
+    const int wi = a.tap[tap] >> 16;
+#pragma unroll
+    for (int v = 0; v < BI; ++v)
+      glds16(wr, bimg + buf * BBYTES + (4 * v + w) * 1024, wrow[v] + (uint32_t)((wi * a.CA + c0) * 2));
+  };
+
+  for (int cc = 0; cc < CPT; ++cc) {
+    const int c0 = cc * 64;
+    if (cc > 0) __syncthreads();                       // every wave is done with the previous chunk
+#pragma unroll
+    for (int u = 0; u < HU; ++u)
+      if (w + 4 * u < HG) glds16(ar, halo + (w + 4 * u) * 1024, hoff[u] == kOOB ? kOOB : hoff[u] + c0 * 2);
+    issue_b(0, c0, 0);
+    for (int tp = 0; tp < 9; ++tp) {
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      if (tp + 1 < 9) issue_b(tp + 1, c0, (tp + 1) & 1);
+      const int pk = a.tap[tp];
+      const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+      const char* Bi = bimg + (tp & 1) * BBYTES;
+      int hp[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) hp[i] = hbase[i] + td;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        bf16x8 fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = row_frag(halo, hp[i], 2 * s4 + lh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, wn * 64 + j * 32 + lr, 2 * s4 + lh);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+      }
+    }
+  }
+  __syncthreads();                                     // every wave is done with the halo / weights
+
+  // ---- epilogue (as k_igemm): bf16 tile through LDS, masked BN partials, coalesced NHWC rows ----
+  char* ot = smem;
+  float* sst = reinterpret_cast<float*>(smem + BM * RS);   // [WM][2][BN]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = wn * 64 + j * 32 + lr;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+        const bf16_t hv = f2bf(acc[i][j][q]);
+        *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv;
+        const float fv = m < npx ? bf2f(hv) : 0.f;
+        s1 += fv;
+        s2 += fv * fv;
+      }
+      if (a.stats) {
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (i == 0) {
+          if (lh == 0) { sst[(wm * 2 + 0) * BN + n] = s1; sst[(wm * 2 + 1) * BN + n] = s2; }
+        } else {
+          if (lh == 0) { sst[(wm * 2 + 0) * BN + n] += s1; sst[(wm * 2 + 1) * BN + n] += s2; }
+        }
+      }
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  const size_t obase = ((size_t)b * a.H + oh0) * a.W;     // first output pixel of the block
+#pragma unroll
+  for (int u = 0; u < BM * CPR / kThreads; ++u) {
+    const int c = t + kThreads * u, row = c / CPR, cc = c % CPR;
+    if (row < npx) {
+      uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
+      const size_t o = (obase + row) * a.NC + n0 + cc * 8;
+      if (a.R) {
+        float f[8], r[8];
+        unpack8(v, f);
+        unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(a.Y + o) = v;
+    }
+  }
+  if (a.stats && t < 2 * BN) {
+    const int which = t / BN, n = t % BN;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < WM; ++k) s += sst[(k * 2 + which) * BN + n];
+    a.stats[((size_t)mt * 2 + which) * a.NC + n0 + n] = s;
+  }
+}
+
+// Persistent variant for C = NC = 64 (ResNet-18 layer1, fprop and dgrad): the whole 3x3 weight
+// (9 taps x [64][64] bf16 = 72 KB) is staged ONCE per block and stays in LDS; the block then walks
+// its row tiles (tile = blockIdx.x + k * gridDim.x) with the halo double-buffered, so the next tile's
+// halo DMA runs under this tile's 9 x 16 MFMAs per wave and no per-tap barrier or weight reload
+// remains.  One block per CU (72 KB weights + 2 x 44 KB halos = 160 KB of LDS); the epilogue uses the
+// current halo buffer as its scratch tile.
+constexpr int kT64 = 512;                             // 8 waves: 2 per SIMD to hide LDS / MFMA latency
+__global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
+  constexpr int HG = 44, HU = (HG + 7) / 8, HB = HG * 1024;   // (TH + 2) * (W + 2) <= 352 halo pixels
+  constexpr int WB = 9 * 64 * 128;                      // 72 KB weights + 2 x 44 KB halos = 160 KB
+  constexpr int RS = 64 * 2 + 16;
+  static_assert(256 * RS + 2 * 8 * 64 * 4 <= HB, "epilogue scratch must fit one halo buffer");
+  __shared__ __attribute__((aligned(16))) char smem[WB + 2 * HB];
+  char* wimg = smem;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int ntile = a.Bn * a.rtiles, HW2 = a.W + 2;
+  const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), wr = make_rsrc(a.Wg, a.w_bytes);
+  if ((int)blockIdx.x >= ntile) return;
+
+  // weights: 72 one-KB groups (tap k = g / 8, rows n = 8 (g % 8) + lrow), 9 per wave
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int g = w + 8 * j, k = g >> 3, wi = a.tap[k] >> 16;
+    glds16(wr, wimg + g * 1024, (uint32_t)((((g & 7) * 8 + lrow) * 9 * 64 + wi * 64 + ch * 8) * 2));
+  }
+  // halo pixel (hy, hx) of this lane's row in group w + 4u: fixed for every tile
+  int hyx[HU];
+#pragma unroll
+  for (int u = 0; u < HU; ++u) {
+    const int hr = 8 * (w + 8 * u) + lrow, hy = hr / HW2;
+    hyx[u] = (hy << 16) | (hr - hy * HW2);
+  }
+  auto issue_halo = [&](int tile, int buf) {
+    const int b = tile / a.rtiles, oh0 = (tile - b * a.rtiles) * a.TH;
+    char* h = smem + WB + buf * HB;
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int hy = hyx[u] >> 16, hx = hyx[u] & 0xffff, ih = oh0 - 1 + hy, iw = hx - 1;
+      const bool ok = hy < a.TH + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      if (w + 8 * u < HG)
+        glds16(ar, h + (w + 8 * u) * 1024, ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * 64 + ch * 8) * 2) : kOOB);
+    }
+  };
+
+  const int wm = w, lr = l & 31, lh = l >> 5;            // 8 x 1 waves of 32 x 64
+  issue_halo(blockIdx.x, 0);
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
+    const int buf = it & 1;
+    const int b = tile / a.rtiles, oh0 = (tile - b * a.rtiles) * a.TH;
+    const int rows = min(a.TH, a.H - oh0), npx = rows * a.W;
+    wait_vm<0>();                                      // this tile's halo (and the weights) landed
+    __builtin_amdgcn_s_barrier();                      // ... for every wave; the other buffer is free
+    if (tile + (int)gridDim.x < ntile) issue_halo(tile + gridDim.x, buf ^ 1);
+    const char* halo = smem + WB + buf * HB;
+    int hbase[1];
+    {
+      int p = wm * 32 + lr;
+      p = p < npx ? p : 0;
+      const int py = p / a.W, px = p - py * a.W;
+      hbase[0] = (py + 1) * HW2 + px + 1;
+    }
+    f32x16 acc[1][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[0][j] = f32x16{0.f};
+    for (int tp = 0; tp < 9; ++tp) {
+      const int pk = a.tap[tp];
+      const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+      const char* Bi = wimg + tp * 8192;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        bf16x8 fa, fb[2];
+        fa = row_frag(halo, hbase[0] + td, 2 * s4 + lh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, j * 32 + lr, 2 * s4 + lh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[0][j] = mfma_bf16(fa, fb[j], acc[0][j]);
+      }
+    }
+    __syncthreads();                                   // every wave is done reading this halo
+    char* ot = smem + WB + buf * HB;                   // epilogue scratch: this tile's halo buffer
+    float* sst = reinterpret_cast<float*>(ot + 256 * RS);   // [8][2][64]
+    {
+      const int i = 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = j * 32 + lr;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          const bf16_t hv = f2bf(acc[i][j][q]);
+          *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv;
+          const float fv = m < npx ? bf2f(hv) : 0.f;
+          s1 += fv;
+          s2 += fv * fv;
+        }
+        if (a.stats) {
+          s1 += __shfl_xor(s1, 32, 64);
+          s2 += __shfl_xor(s2, 32, 64);
+          if (lh == 0) { sst[(wm * 2 + 0) * 64 + n] = s1; sst[(wm * 2 + 1) * 64 + n] = s2; }
+        }
+      }
+    }
+    __syncthreads();
+    const size_t obase = ((size_t)b * a.H + oh0) * a.W;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {                      // 256 rows x 8 chunks of 16 B
+      const int c = t + kT64 * u, row = c >> 3, cc = c & 7;
+      if (row < npx) {
+        uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
+        const size_t o = (obase + row) * 64 + cc * 8;
+        if (a.R) {
+          float f[8], r[8];
+          unpack8(v, f);
+          unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += r[e];
+          v = pack8(f);
+        }
+        *reinterpret_cast<uint4*>(a.Y + o) = v;
+      }
+    }
+    if (a.stats && t < 128) {
+      const int which = t >> 6, n = t & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += sst[(k * 2 + which) * 64 + n];
+      a.stats[((size_t)tile * 2 + which) * 64 + n] = sum;
+    }
+  }
+}
+
+// Geometry of the halo path for a stride-1 3x3 / pad-1 conv over [Bn][H][W] with C -> NC channels:
+// fills TH / rtiles / ntiles and returns BM (0 = not eligible: the implicit GEMM runs instead)
+int hconv_geom(int Bn, int H, int W, int C, int NC, int R, int S, int stride, int pad, int& TH, int& rtiles) {
+  static const bool off = [] {
+    const char* e = getenv("PDE_CONV_HALO");
+    return e && e[0] == '0';
+  }();
+  if (off || stride != 1 || R != 3 || S != 3 || pad != 1 || C % 64 || NC % 64 || W < 14 || W > 64 || Bn < 1)
+    return 0;
+  const int BM = NC % 128 == 0 ? 128 : 256;
+  TH = min(H, BM / W);
+  if (TH < 1 || (TH + 2) * (W + 2) > 8 * (BM == 256 ? hconv_groups<256>() : hconv_groups<128>())) return 0;
+  rtiles = (H + TH - 1) / TH;
+  return BM;
+}
+
+hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, float* stats, int Bn, int H, int W,
+                        int CA, int NC, const int* taps, hipStream_t st) {
+  HconvArgs a{};
+  int TH = 0, rtiles = 0;
+  const int BM = hconv_geom(Bn, H, W, CA, NC, 3, 3, 1, 1, TH, rtiles);
+  if (!BM) return hipErrorInvalidValue;
+  a.A = (const bf16_t*)A;
+  a.Wg = (const bf16_t*)Wm;
+  a.Y = (bf16_t*)Y;
+  a.R = (const bf16_t*)R;
+  a.stats = stats;
+  a.a_bytes = (uint32_t)((size_t)Bn * H * W * CA * 2);
+  a.w_bytes = (uint32_t)((size_t)NC * 9 * CA * 2);
+  a.Bn = Bn; a.H = H; a.W = W; a.CA = CA; a.NC = NC;
+  a.TH = TH; a.rtiles = rtiles;
+  for (int k = 0; k < 9; ++k) a.tap[k] = taps[k];
+  static const bool persistent = [] {
+    const char* e = getenv("PDE_CONV_HALO_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  if (BM == 256 && CA == 64 && NC == 64 && (TH + 2) * (W + 2) <= 8 * 44 && persistent) {   // k_hconv64: 44 used
+    a.ntiles = 1;
+    int ncu = 256, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                  hipSuccess || ncu < 1)
+      ncu = 256;
+    hipLaunchKernelGGL(k_hconv64, dim3(min(Bn * rtiles, ncu)), dim3(kT64), 0, st, a);
+  } else if (BM == 256) {
+    a.ntiles = NC / 64;
+    hipLaunchKernelGGL((k_hconv<256, 64>), dim3(Bn * rtiles * a.ntiles), dim3(kThreads), 0, st, a);
+  } else {
+    a.ntiles = NC / 128;
+    hipLaunchKernelGGL((k_hconv<128, 128>), dim3(Bn * rtiles * a.ntiles), dim3(kThreads), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
 // dW (bf16) = sum over splits of the fp32 slabs [splits][n].  A 256-thread block = SL split lanes x
 // 256/SL output lanes of 4 elements: the split range is walked by SL lanes in parallel (two slabs in
 // flight each) and folded through LDS, so a small weight with hundreds of splits (1x1 downsample:
@@ -551,9 +914,24 @@ void pde_conv_set_stages(int nst) { g_conv_nst = nst == 3 ? 3 : 2; }
 
 int pde_conv_fprop_mtiles(int M, int N) { return N % 128 == 0 ? (M + 127) / 128 : (M + 255) / 256; }
 
+// rows of BN-statistics partials an fprop writes: one per M tile of whichever kernel runs it
+int pde_conv_stats_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW) {
+  int TH = 0, rtiles = 0;
+  if (hconv_geom(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles)) return Bn * rtiles;
+  return pde_conv_fprop_mtiles(Bn * OH * OW, N);
+}
+
 hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, int Bn, int H, int W, int C, int N,
                           int R, int S, int stride, int pad, int OH, int OW, hipStream_t st) {
   if (C % 64 || N % 64 || R * S > 9) return hipErrorInvalidValue;
+  {
+    int TH = 0, rtiles = 0;
+    if (hconv_geom(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles)) {
+      int taps[9];
+      for (int k = 0; k < 9; ++k) taps[k] = pack_tap(k / 3 - 1, k % 3 - 1, k);
+      return launch_hconv(x, w, y, nullptr, stats, Bn, H, W, C, N, taps, st);
+    }
+  }
   IgemmArgs a{};
   a.A = (const bf16_t*)x;
   a.W = (const bf16_t*)w;
@@ -601,6 +979,15 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* 
                           hipStream_t st) {
   if (C % 64 || N % 64 || R * S > 9 || stride < 1 || stride > 2) return hipErrorInvalidValue;
   if (dy2 && (stride != 2 || !wt2 || (H - 1) / 2 + 1 != OH || (W - 1) / 2 + 1 != OW)) return hipErrorInvalidValue;
+  {
+    // stride-1 3x3 / pad-1: the input gradient is the flipped-tap conv of dy with Wt (halo path)
+    int TH = 0, rtiles = 0;
+    if (!dy2 && OH == H && OW == W && hconv_geom(Bn, H, W, N, C, R, S, stride, pad, TH, rtiles)) {
+      int taps[9];
+      for (int k = 0; k < 9; ++k) taps[k] = pack_tap(1 - k / 3, 1 - k % 3, k);
+      return launch_hconv(dy, wt, dx, res, nullptr, Bn, H, W, N, C, taps, st);
+    }
+  }
   IgemmArgs a{};
   a.A = (const bf16_t*)dy;
   a.W = (const bf16_t*)wt;

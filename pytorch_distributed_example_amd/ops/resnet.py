@@ -85,7 +85,7 @@ class Conv2dNHWCFn(torch.autograd.Function):
         y = torch.empty(N, O, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         stats = None
         if with_stats:
-            nblk = K.conv_stats_blocks(N * OH * OW, O)
+            nblk = K.conv_stats_rows(x, w, stride, pad)     # one partial row per M tile of the kernel
             stats = torch.empty(K.bn_part_rows(nblk) * 2 * O, device=x.device, dtype=torch.float32)
             ctx.nblk = nblk
             ctx.mark_non_differentiable(stats)
@@ -172,7 +172,7 @@ def _conv_fwd(x, w, stride, pad):
     O, _, R, S = w.shape
     OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     y = torch.empty(N, O, OH, OW, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
-    nblk = K.conv_stats_blocks(N * OH * OW, O)
+    nblk = K.conv_stats_rows(x, w, stride, pad)
     part = torch.empty(K.bn_part_rows(nblk) * 2 * O, device=x.device, dtype=torch.float32)
     K.conv_fprop(x, w, y, part, stride, pad)
     return y, part, nblk
@@ -364,11 +364,11 @@ def conv2d_nhwc(x, w, stride: int = 1, pad: int = 0, with_stats: bool = False):
             return y, (part, kernels().stem_stats_blocks(y.shape[0], y.shape[2]))
         return out
     if igemm_eligible(x, w, stride, pad):
-        out = Conv2dNHWCFn.apply(x.contiguous(memory_format=torch.channels_last),
-                                 w.contiguous(memory_format=torch.channels_last), stride, pad, with_stats)
+        xc, wc = x.contiguous(memory_format=torch.channels_last), w.contiguous(memory_format=torch.channels_last)
+        out = Conv2dNHWCFn.apply(xc, wc, stride, pad, with_stats)
         if with_stats:
             y, part = out
-            return y, (part, kernels().conv_stats_blocks(y.shape[0] * y.shape[2] * y.shape[3], w.shape[0]))
+            return y, (part, kernels().conv_stats_rows(xc, wc, stride, pad))
         return out
     if x.is_cuda:
         # no silent library fallback on the GPU: every ResNet-18 convolution is covered above

@@ -21,6 +21,11 @@ SHAPES = [
     (5, 128, 13, 11, 256, 3, 2, 1),
     (4, 64, 56, 56, 64, 3, 1, 1),      # ResNet-18 layer1 geometry
     (2, 512, 7, 7, 512, 3, 1, 1),      # layer4
+    # halo-tiled stride-1 3x3 kernel (k_hconv): layer2 / layer3 geometry, partial row tiles, odd widths
+    (2, 128, 28, 28, 128, 3, 1, 1),
+    (2, 256, 14, 14, 256, 3, 1, 1),
+    (3, 64, 17, 23, 128, 3, 1, 1),
+    (2, 128, 20, 15, 64, 3, 1, 1),
 ]
 
 
@@ -72,18 +77,21 @@ def test_conv_exact_integer_data():
 
 
 @pytest.mark.parametrize("N", [64, 128])
-def test_conv_fprop_bn_stats(N):
+@pytest.mark.parametrize("B,H,W", [(3, 10, 9), (2, 12, 20), (2, 9, 56)])
+def test_conv_fprop_bn_stats(N, B, H, W):
+    """BN statistics partials from the conv epilogue (implicit GEMM for narrow images, the halo-tiled
+    kernel for W >= 14): one row per M tile of whichever kernel ran, folding to the batch sums."""
     torch.manual_seed(11)
     K = kernels()
-    B, C, H, W = 3, 64, 10, 9
+    C = 64
     x = cl(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16))
     w = cl((torch.randn(N, C, 3, 3, device=dev) / 24).to(torch.bfloat16))
     y = cl(torch.empty(B, N, H, W, device=dev, dtype=torch.bfloat16))
-    M = B * H * W
-    nblk = K.conv_stats_blocks(M, N)
+    nblk = K.conv_stats_rows(x, w, 1, 1)
     stats = torch.empty(nblk * 2 * N, device=dev)
     K.conv_fprop(x, w, y, stats, 1, 1)
     st = stats.view(nblk, 2, N).sum(0)
+    assert torch.allclose(y.float(), F.conv2d(x.float(), w.float(), None, 1, 1), rtol=2e-2, atol=2e-2)
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, N)
     assert torch.allclose(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
