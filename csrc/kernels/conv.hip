@@ -498,6 +498,17 @@ struct HconvArgs {
 
 template <int BM> constexpr int hconv_groups() { return BM == 256 ? 50 : 33; }   // 8-pixel halo groups
 
+// Halo image layout: pixel row r at r * 128 B, 16-byte channel chunk c in slot c ^ ((r >> 1) & 7).  A tap
+// shifts the rows a wave reads by an arbitrary amount, so the image must be conflict-free for ANY 16
+// consecutive rows (one ds_read_b128 phase), not only for 8-aligned ones as the toff() tile layout is:
+// 16 consecutive rows have distinct r mod 16, i.e. distinct (bank half r & 1, slot (r >> 1) & 7).
+// LDS-DMA fills a 1 KB group lane-linearly: lane l -> row l >> 3 of the group, slot l & 7.
+__device__ __forceinline__ bf16x8 halo_frag(const char* halo, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(halo + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+}
+// channel chunk that lane l loads for halo group g (parity gpar = g & 1; groups are 8 rows)
+__device__ __forceinline__ int halo_dma_chunk(int l, int gpar) { return (l & 7) ^ ((4 * gpar + (l >> 4)) & 7); }
+
 template <int BM, int BN>
 __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   constexpr int WN = BN / 64, WM = 4 / WN;
@@ -522,14 +533,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
 
   // ---- halo DMA sources: group g = w + 4u, lane row glds_row, chunk glds_chunk (group parity = w & 1) ----
   const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
+  const int hrow = l >> 3, hch = halo_dma_chunk(l, w & 1);   // halo groups w + 4u share parity w & 1
   uint32_t hoff[HU];
 #pragma unroll
   for (int u = 0; u < HU; ++u) {
-    const int hr = 8 * (w + 4 * u) + lrow;
+    const int hr = 8 * (w + 4 * u) + hrow;
     const int hy = hr / HW2, hx = hr - hy * HW2;
     const int ih = oh0 - 1 + hy, iw = hx - 1;
     const bool ok = hy < a.TH + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-    hoff[u] = ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * a.CA + ch * 8) * 2) : kOOB;
+    hoff[u] = ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * a.CA + hch * 8) * 2) : kOOB;
   }
   uint32_t wrow[BI];
 #pragma unroll
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
       for (int s4 = 0; s4 < 4; ++s4) {
         bf16x8 fa[2], fb[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[i] = row_frag(halo, hp[i], 2 * s4 + lh);
+        for (int i = 0; i < 2; ++i) fa[i] = halo_frag(halo, hp[i], 2 * s4 + lh);
 #pragma unroll
         for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, wn * 64 + j * 32 + lr, 2 * s4 + lh);
 #pragma unroll
@@ -680,7 +692,7 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
   int hyx[HU];
 #pragma unroll
   for (int u = 0; u < HU; ++u) {
-    const int hr = 8 * (w + 8 * u) + lrow, hy = hr / HW2;
+    const int hr = 8 * (w + 8 * u) + (l >> 3), hy = hr / HW2;
     hyx[u] = (hy << 16) | (hr - hy * HW2);
   }
   auto issue_halo = [&](int tile, int buf) {
@@ -691,7 +703,8 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
       const int hy = hyx[u] >> 16, hx = hyx[u] & 0xffff, ih = oh0 - 1 + hy, iw = hx - 1;
       const bool ok = hy < a.TH + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (w + 8 * u < HG)
-        glds16(ar, h + (w + 8 * u) * 1024, ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * 64 + ch * 8) * 2) : kOOB);
+        glds16(ar, h + (w + 8 * u) * 1024,
+               ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * 64 + halo_dma_chunk(l, w & 1) * 8) * 2) : kOOB);
     }
   };
 
@@ -723,7 +736,7 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         bf16x8 fa, fb[2];
-        fa = row_frag(halo, hbase[0] + td, 2 * s4 + lh);
+        fa = halo_frag(halo, hbase[0] + td, 2 * s4 + lh);
 #pragma unroll
         for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, j * 32 + lr, 2 * s4 + lh);
 #pragma unroll
