@@ -316,7 +316,8 @@ void conv_wtrans_batch(const at::Tensor& desc, int64_t total) {
 
 int64_t conv_wgrad_splits(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
   const ConvGeom g = conv_geom(x, w, stride, pad);
-  return pde_conv_wgrad_splits((int)g.Bn, (int)g.OH, (int)g.OW, (int)g.N, (int)(g.R * g.S), (int)g.C);
+  return pde_conv_wgrad_splits2((int)g.Bn, (int)g.H, (int)g.W, (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride,
+                                (int)pad, (int)g.OH, (int)g.OW);
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& part,

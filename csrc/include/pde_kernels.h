@@ -131,6 +131,7 @@ int pde_conv_wtdesc_bytes();
 hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, const void* dy2, const void* wt2,
                           int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW,
                           hipStream_t st);
+int pde_conv_wgrad_splits2(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW);
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C);
 hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hipStream_t st);
 hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,

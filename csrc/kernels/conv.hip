@@ -797,6 +797,165 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
   }
 }
 
+// ---- halo-tiled weight gradient, C = N = 64 (ResNet-18 layer1) ----
+// dW[n][tap][c] = sum_p dY[p][n] X[p + d_tap][c]: the K dimension is the pixel, so both operands are
+// read TRANSPOSED (ds_read_b64_tr_b16, K along image rows).  The implicit GEMM (k_wgrad) stages X once
+// per tap column tile; here a persistent block walks row tiles (TH rows x W pixels, as k_hconv64),
+// stages the tile's dY rows and its X halo once (double-buffered, both in the halo image layout), and
+// accumulates all 9 taps x 64 c x 64 n in registers (4 waves x 9 32x32 tiles; a tap is a constant
+// shift of the B rows); one fp32 slab per block, summed by k_wgrad_reduce.
+__device__ __forceinline__ s4v tr_read_b64(uint32_t addr) {
+  s4v v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+// byte offset of the 8-byte piece (half hf) of 16-byte chunk ch in row r of a halo-layout image
+__device__ __forceinline__ uint32_t hoffs(int r, int ch, int hf) {
+  return (uint32_t)(r * 128 + 16 * (ch ^ ((r >> 1) & 7)) + 8 * hf);
+}
+
+struct HwgArgs {
+  const bf16_t* dY;     // [Bn][H][W][64]
+  const bf16_t* X;      // [Bn][H][W][64]
+  float* part;          // [gridDim.x][64][9 * 64]
+  uint32_t dy_bytes, x_bytes;
+  int Bn, H, W, TH, rtiles;
+  int tap[9];           // pack_tap(dh, dw, widx): column block widx gets shift (dh, dw)
+};
+
+constexpr int kHwgThreads = 576;                     // 9 waves: wave w owns tap w
+__global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
+  constexpr int NW = 9;
+  constexpr int HG = 44, HB = HG * 1024;               // X halo: <= 352 rows
+  constexpr int DG = 32, DB = DG * 1024;               // dY tile: 256 rows
+  constexpr int BUF = HB + DB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int ntile = a.Bn * a.rtiles, HW2 = a.W + 2;
+  const rsrc_t yr = make_rsrc(a.dY, a.dy_bytes), xr = make_rsrc(a.X, a.x_bytes);
+  if ((int)blockIdx.x >= ntile) return;
+
+  auto issue = [&](int tile, int buf) {
+    const int b = tile / a.rtiles, oh0 = (tile - b * a.rtiles) * a.TH;
+    const int npx = min(a.TH, a.H - oh0) * a.W;
+    const int pbase = (b * a.H + oh0) * a.W;
+    char* h = smem + buf * BUF;
+#pragma unroll
+    for (int u = 0; u < (HG + NW - 1) / NW; ++u) {
+      const int g = w + NW * u;
+      if (g < HG) {
+        const int hr = 8 * g + (l >> 3), hy = hr / HW2, hx = hr - hy * HW2;
+        const int ih = oh0 - 1 + hy, iw = hx - 1;
+        const bool ok = hy < a.TH + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const int dch = halo_dma_chunk(l, g & 1);
+        glds16(xr, h + g * 1024, ok ? (uint32_t)((((b * a.H + ih) * a.W + iw) * 64 + dch * 8) * 2) : kOOB);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (DG + NW - 1) / NW; ++u) {
+      const int g = w + NW * u;
+      if (g < DG) {
+        const int k = 8 * g + (l >> 3), dch = halo_dma_chunk(l, g & 1);
+        glds16(yr, h + HB + g * 1024, k < npx ? (uint32_t)(((pbase + k) * 64 + dch * 8) * 2) : kOOB);
+      }
+    }
+  };
+
+  // wave w = tap w: D[n][(w, c)] over both 32-row n tiles and both 32-column c halves
+  const int g4 = l >> 4, i16 = l & 15, q = i16 >> 2, p4 = i16 & 3, h2 = g4 >> 1;
+  const int hf = p4 & 1, cpart = 2 * (g4 & 1) + (p4 >> 1);
+  const int pk = a.tap[w];
+  const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0.f};
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  // fragments of one k-step: A (dY rows k, n chunks) x 2 n tiles, B (halo rows r + td, c chunks) x 2 halves
+  struct Fr {
+    s4v a[2][2], b[2][2];
+  };
+  auto load = [&](Fr& f, uint32_t hbase, uint32_t ybase, int ks, int npx) {
+    const int k0 = 16 * ks + 4 * h2 + q, k1 = k0 + 8;
+    const int c0 = min(k0, npx - 1), c1 = min(k1, npx - 1);   // dY rows past npx are zero
+    const int y0 = c0 / a.W, y1 = c1 / a.W;
+    const int r0 = (y0 + 1) * HW2 + (c0 - y0 * a.W) + 1 + td, r1 = (y1 + 1) * HW2 + (c1 - y1 * a.W) + 1 + td;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f.a[i][0] = tr_read_b64(ybase + hoffs(k0, 4 * i + cpart, hf));
+      f.a[i][1] = tr_read_b64(ybase + hoffs(k1, 4 * i + cpart, hf));
+      f.b[i][0] = tr_read_b64(hbase + hoffs(r0, 4 * i + cpart, hf));
+      f.b[i][1] = tr_read_b64(hbase + hoffs(r1, 4 * i + cpart, hf));
+    }
+  };
+  auto mma = [&](const Fr& f) {
+    bf16x8 fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      fa[i][0] = f.a[i][0][0]; fa[i][1] = f.a[i][0][1]; fa[i][2] = f.a[i][0][2]; fa[i][3] = f.a[i][0][3];
+      fa[i][4] = f.a[i][1][0]; fa[i][5] = f.a[i][1][1]; fa[i][6] = f.a[i][1][2]; fa[i][7] = f.a[i][1][3];
+      fb[i][0] = f.b[i][0][0]; fb[i][1] = f.b[i][0][1]; fb[i][2] = f.b[i][0][2]; fb[i][3] = f.b[i][0][3];
+      fb[i][4] = f.b[i][1][0]; fb[i][5] = f.b[i][1][1]; fb[i][6] = f.b[i][1][2]; fb[i][7] = f.b[i][1][3];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+  };
+
+  issue(blockIdx.x, 0);
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
+    const int buf = it & 1;
+    const int b = tile / a.rtiles, oh0 = (tile - b * a.rtiles) * a.TH;
+    const int npx = min(a.TH, a.H - oh0) * a.W;
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (tile + (int)gridDim.x < ntile) issue(tile + gridDim.x, buf ^ 1);
+    const uint32_t hbase = lds0 + buf * BUF, ybase = hbase + HB;
+    const int nks = (npx + 15) >> 4;
+    // software pipeline: the 8 transposed reads of k-step ks+1 are in flight during ks's 4 MFMAs
+    Fr f0, f1;
+    load(f0, hbase, ybase, 0, npx);
+    for (int ks = 0; ks < nks; ks += 2) {
+      if (ks + 1 < nks) {
+        load(f1, hbase, ybase, ks + 1, npx);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(f0);
+      if (ks + 1 < nks) {
+        if (ks + 2 < nks) {
+          load(f0, hbase, ybase, ks + 2, npx);
+          asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(f1);
+      }
+    }
+  }
+  // D[n][col]: registers = rows n, lane column = c; this wave's tap w -> dW[n][w][c]
+  float* out = a.part + (size_t)blockIdx.x * 64 * 576;
+  const int lr = l & 31, wi = pk >> 16;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = wi * 64 + 32 * j + lr;
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) {
+        const int n = 32 * i + (qq & 3) + 8 * (qq >> 2) + 4 * (l >> 5);
+        out[(size_t)n * 576 + col] = acc[i][j][qq];
+      }
+    }
+}
+
 // Geometry of the halo path for a stride-1 3x3 / pad-1 conv over [Bn][H][W] with C -> NC channels:
 // fills TH / rtiles / ntiles and returns BM (0 = not eligible: the implicit GEMM runs instead)
 int hconv_geom(int Bn, int H, int W, int C, int NC, int R, int S, int stride, int pad, int& TH, int& rtiles) {
@@ -1041,6 +1200,30 @@ hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* 
   return dispatch_igemm(a, st);
 }
 
+// halo-tiled layer1 wgrad (k_hwgrad64): row tiles as k_hconv64; returns the persistent grid (= slabs)
+// or 0 when not eligible
+static int hwgrad_grid(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int& TH, int& rtiles) {
+  static const bool off = [] {
+    const char* e = getenv("PDE_CONV_HALO_WGRAD");
+    return e && e[0] == '0';
+  }();
+  if (off || C != 64 || N != 64 || R != 3 || S != 3 || stride != 1 || pad != 1 || W < 14 || W > 64) return 0;
+  TH = min(H, 256 / W);
+  if (TH < 1 || (TH + 2) * (W + 2) > 352) return 0;
+  rtiles = (H + TH - 1) / TH;
+  int ncu = 256, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+    ncu = 256;
+  return min(Bn * rtiles, ncu);
+}
+
+int pde_conv_wgrad_splits2(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW) {
+  int TH = 0, rtiles = 0;
+  const int g = hwgrad_grid(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles);
+  return g ? g : pde_conv_wgrad_splits(Bn, OH, OW, N, R * S, C);
+}
+
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C) {
   // ~2 blocks per CU in total and >= 16 pixel stages per block: enough parallelism without
   // making the fp32 slab round trip (splits x N x T*C x 4 B, written and re-read) dominate.
@@ -1062,6 +1245,23 @@ hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hi
 hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits, void* dw, int Bn, int H, int W,
                           int C, int N, int R, int S, int stride, int pad, int OH, int OW, hipStream_t st) {
   if (C % 64 || N % 64 || splits < 1) return hipErrorInvalidValue;
+  {
+    int TH = 0, rtiles = 0;
+    const int g = hwgrad_grid(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles);
+    if (g && g == splits) {
+      HwgArgs h{};
+      h.dY = (const bf16_t*)dy;
+      h.X = (const bf16_t*)x;
+      h.part = part;
+      h.dy_bytes = (uint32_t)((size_t)Bn * H * W * 64 * 2);
+      h.x_bytes = h.dy_bytes;
+      h.Bn = Bn; h.H = H; h.W = W; h.TH = TH; h.rtiles = rtiles;
+      for (int k = 0; k < 9; ++k) h.tap[k] = pack_tap(k / 3 - 1, k % 3 - 1, k);
+      hipLaunchKernelGGL(k_hwgrad64, dim3(g), dim3(kHwgThreads), 0, st, h);
+      PDE_HIP_CHECK(hipGetLastError());
+      return launch_wgrad_reduce(part, splits, (int64_t)N * 9 * C, (bf16_t*)dw, st);
+    }
+  }
   WgradArgs a{};
   a.dY = (const bf16_t*)dy;
   a.X = (const bf16_t*)x;

@@ -26,6 +26,7 @@ SHAPES = [
     (2, 256, 14, 14, 256, 3, 1, 1),
     (3, 64, 17, 23, 128, 3, 1, 1),
     (2, 128, 20, 15, 64, 3, 1, 1),
+    (3, 64, 17, 20, 64, 3, 1, 1),      # halo-tiled layer1 wgrad with a ragged last row tile
 ]
 
 
