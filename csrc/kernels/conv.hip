@@ -498,16 +498,23 @@ struct HconvArgs {
 
 template <int BM> constexpr int hconv_groups() { return BM == 256 ? 50 : 33; }   // 8-pixel halo groups
 
-// Halo image layout: pixel row r at r * 128 B, 16-byte channel chunk c in slot c ^ ((r >> 1) & 7).  A tap
-// shifts the rows a wave reads by an arbitrary amount, so the image must be conflict-free for ANY 16
-// consecutive rows (one ds_read_b128 phase), not only for 8-aligned ones as the toff() tile layout is:
-// 16 consecutive rows have distinct r mod 16, i.e. distinct (bank half r & 1, slot (r >> 1) & 7).
-// LDS-DMA fills a 1 KB group lane-linearly: lane l -> row l >> 3 of the group, slot l & 7.
+// Halo image layout: pixel row r at r * 128 B, 16-byte channel chunk c in slot c ^ hsw((r >> 1) & 7) with
+// hsw(v) = (v0 << 2) | v1 << 1 | v2 (bit-reversed v).  A tap shifts the rows a wave reads by an
+// arbitrary amount, so the image must be conflict-free for unaligned rows, for two access shapes:
+//  * ds_read_b128 row fragments (k_hconv A): 16 consecutive rows, one chunk -> per bank half (r & 1)
+//    8 consecutive v, hsw a bijection -> 8 distinct slots;
+//  * ds_read_b64_tr_b16 (k_hwgrad64): 4 consecutive rows x a 4-chunk half (c..c+3, c = 0 or 4) -> the
+//    two rows sharing a bank half have consecutive v, whose hsw differ in bit 2 (= v0), so their 4-slot
+//    sets land in opposite halves of the row.
+// (The first version, c ^ v, mapped a chunk pair onto itself for v, v+1: 1.8 conflict cycles per LDS
+// instruction in the transposed reads.)  LDS-DMA fills a 1 KB group lane-linearly: lane l -> row
+// l >> 3 of the group, slot l & 7.
+__device__ __forceinline__ int hsw(int v) { return ((v & 1) << 2) | (v & 2) | ((v >> 2) & 1); }
 __device__ __forceinline__ bf16x8 halo_frag(const char* halo, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(halo + row * 128 + 16 * (chunk ^ ((row >> 1) & 7)));
+  return *reinterpret_cast<const bf16x8*>(halo + row * 128 + 16 * (chunk ^ hsw((row >> 1) & 7)));
 }
 // channel chunk that lane l loads for halo group g (parity gpar = g & 1; groups are 8 rows)
-__device__ __forceinline__ int halo_dma_chunk(int l, int gpar) { return (l & 7) ^ ((4 * gpar + (l >> 4)) & 7); }
+__device__ __forceinline__ int halo_dma_chunk(int l, int gpar) { return (l & 7) ^ hsw((4 * gpar + (l >> 4)) & 7); }
 
 template <int BM, int BN>
 __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
@@ -811,7 +818,7 @@ __device__ __forceinline__ s4v tr_read_b64(uint32_t addr) {
 }
 // byte offset of the 8-byte piece (half hf) of 16-byte chunk ch in row r of a halo-layout image
 __device__ __forceinline__ uint32_t hoffs(int r, int ch, int hf) {
-  return (uint32_t)(r * 128 + 16 * (ch ^ ((r >> 1) & 7)) + 8 * hf);
+  return (uint32_t)(r * 128 + 16 * (ch ^ hsw((r >> 1) & 7)) + 8 * hf);
 }
 
 struct HwgArgs {
