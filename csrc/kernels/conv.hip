@@ -884,17 +884,42 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
   struct Fr {
     s4v a[2][2], b[2][2];
   };
-  auto load = [&](Fr& f, uint32_t hbase, uint32_t ybase, int ks, int npx) {
-    const int k0 = 16 * ks + 4 * h2 + q, k1 = k0 + 8;
-    const int c0 = min(k0, npx - 1), c1 = min(k1, npx - 1);   // dY rows past npx are zero
-    const int y0 = c0 / a.W, y1 = c1 / a.W;
-    const int r0 = (y0 + 1) * HW2 + (c0 - y0 * a.W) + 1 + td, r1 = (y1 + 1) * HW2 + (c1 - y1 * a.W) + 1 + td;
+  // this lane's two K rows advance by 16 pixels per k-step: image (row, column) kept incrementally
+  // (no integer division in the loop); rows past npx read a valid halo row (their dY rows are zero)
+  int kk0 = 0, py0 = 0, px0 = 0, py1 = 0, px1 = 0;
+  auto start = [&]() {
+    kk0 = 4 * h2 + q;
+    py0 = kk0 / a.W; px0 = kk0 - py0 * a.W;
+    const int k1 = kk0 + 8;
+    py1 = k1 / a.W; px1 = k1 - py1 * a.W;
+  };
+  auto advance = [&]() {
+    kk0 += 16;
+    px0 += 16; px1 += 16;
+    while (px0 >= a.W) { px0 -= a.W; ++py0; }
+    while (px1 >= a.W) { px1 -= a.W; ++py1; }
+  };
+  // dY (A) rows advance by exactly 16 per k-step, which leaves their swizzle unchanged: the four A
+  // offsets are per-lane constants plus 2048 * ks
+  uint32_t aoffs[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    aoffs[i][0] = hoffs(4 * h2 + q, 4 * i + cpart, hf);
+    aoffs[i][1] = hoffs(4 * h2 + q + 8, 4 * i + cpart, hf);
+  }
+  auto load = [&](Fr& f, uint32_t hbase, uint32_t ybase, int npx) {
+    const int k0 = kk0, k1 = kk0 + 8;
+    const int r0 = (k0 < npx ? (py0 + 1) * HW2 + px0 + 1 : HW2 + 1) + td;
+    const int r1 = (k1 < npx ? (py1 + 1) * HW2 + px1 + 1 : HW2 + 1) + td;
+    const uint32_t ya = ybase + 128u * (uint32_t)(kk0 - 4 * h2 - q);     // 2048 * ks
+    const uint32_t b0 = hbase + r0 * 128 + 8 * hf, b1 = hbase + r1 * 128 + 8 * hf;
+    const int s0 = hsw((r0 >> 1) & 7), s1 = hsw((r1 >> 1) & 7);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      f.a[i][0] = tr_read_b64(ybase + hoffs(k0, 4 * i + cpart, hf));
-      f.a[i][1] = tr_read_b64(ybase + hoffs(k1, 4 * i + cpart, hf));
-      f.b[i][0] = tr_read_b64(hbase + hoffs(r0, 4 * i + cpart, hf));
-      f.b[i][1] = tr_read_b64(hbase + hoffs(r1, 4 * i + cpart, hf));
+      f.a[i][0] = tr_read_b64(ya + aoffs[i][0]);
+      f.a[i][1] = tr_read_b64(ya + aoffs[i][1]);
+      f.b[i][0] = tr_read_b64(b0 + 16 * ((4 * i + cpart) ^ s0));
+      f.b[i][1] = tr_read_b64(b1 + 16 * ((4 * i + cpart) ^ s1));
     }
   };
   auto mma = [&](const Fr& f) {
@@ -925,10 +950,12 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
     const int nks = (npx + 15) >> 4;
     // software pipeline: the 8 transposed reads of k-step ks+1 are in flight during ks's 4 MFMAs
     Fr f0, f1;
-    load(f0, hbase, ybase, 0, npx);
+    start();
+    load(f0, hbase, ybase, npx);
     for (int ks = 0; ks < nks; ks += 2) {
       if (ks + 1 < nks) {
-        load(f1, hbase, ybase, ks + 1, npx);
+        advance();
+        load(f1, hbase, ybase, npx);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -937,7 +964,8 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
       mma(f0);
       if (ks + 1 < nks) {
         if (ks + 2 < nks) {
-          load(f0, hbase, ybase, ks + 2, npx);
+          advance();
+          load(f0, hbase, ybase, npx);
           asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         } else {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
