@@ -464,28 +464,49 @@ __global__ __launch_bounds__(256) void k_adamw_master(float* __restrict__ master
   const float bc2 = 1.f - powf(b2, (float)step);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
-  float4* mp = reinterpret_cast<float4*>(master);
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 p = mp[i], m = m4[i], v = v4[i];
+  // 28 B of HBM traffic per parameter, each byte touched once (the state is GBs, far past L2 / MALL):
+  // two elements' loads are issued before either is used (more bytes in flight per thread), and the
+  // fp32 streams bypass the caches (non-temporal); the bf16 weights are read by the next forward.
+  typedef float nt4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int nt2 __attribute__((ext_vector_type(2)));
+  nt4* mp = reinterpret_cast<nt4*>(master);
+  nt4* mq = reinterpret_cast<nt4*>(m4);
+  nt4* vq = reinterpret_cast<nt4*>(v4);
+  const nt2* gq = reinterpret_cast<const nt2*>(g16);
+  auto update = [&](int64_t i, nt4 p, nt4 m, nt4 v, nt2 graw) {
     float g[4];
-    unpack4(g16[i], g);
+    unpack4(make_uint2(graw.x, graw.y), g);
     const float dec = (decay_blk == nullptr || decay_blk[i >> 4]) ? (1.f - lr * wd) : 1.f;
-    float* pp = &p.x;
-    float* mm = &m.x;
-    float* vv = &v.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float gg = g[e] * gs;
-      pp[e] *= dec;
-      mm[e] = mm[e] + (gg - mm[e]) * (1.f - b1);
-      vv[e] = vv[e] * b2 + (1.f - b2) * gg * gg;
-      const float denom = sqrtf(vv[e]) / bc2s + eps;
-      pp[e] -= step_size * mm[e] / denom;
+      p[e] *= dec;
+      m[e] = m[e] + (gg - m[e]) * (1.f - b1);
+      v[e] = v[e] * b2 + (1.f - b2) * gg * gg;
+      const float denom = sqrtf(v[e]) / bc2s + eps;
+      p[e] -= step_size * m[e] / denom;
     }
-    mp[i] = p;
-    m4[i] = m;
-    v4[i] = v;
-    p16[i] = pack4(pp);
+    __builtin_nontemporal_store(p, mp + i);
+    __builtin_nontemporal_store(m, mq + i);
+    __builtin_nontemporal_store(v, vq + i);
+    const float pf[4] = {p[0], p[1], p[2], p[3]};
+    p16[i] = pack4(pf);
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += 2 * stride) {
+    const int64_t j = i + stride;
+    const nt4 p0 = __builtin_nontemporal_load(mp + i), m0 = __builtin_nontemporal_load(mq + i),
+              v0 = __builtin_nontemporal_load(vq + i);
+    const nt2 g0 = __builtin_nontemporal_load(gq + i);
+    if (j < n4) {
+      const nt4 p1 = __builtin_nontemporal_load(mp + j), m1 = __builtin_nontemporal_load(mq + j),
+                v1 = __builtin_nontemporal_load(vq + j);
+      const nt2 g1 = __builtin_nontemporal_load(gq + j);
+      update(i, p0, m0, v0, g0);
+      update(j, p1, m1, v1, g1);
+    } else {
+      update(i, p0, m0, v0, g0);
+    }
   }
 }
 
