@@ -120,7 +120,7 @@ void sumsq_bf16(const at::Tensor& g, double scale, const at::Tensor& out) {
 
 void adamw_master(const at::Tensor& master, const at::Tensor& p16, const at::Tensor& g16, const at::Tensor& m,
                   const at::Tensor& v, double lr, double b1, double b2, double eps, double wd, double grad_scale,
-                  int64_t step, const OptT& decay_blk, const OptT& clip_sumsq, double max_norm) {
+                  int64_t step, const OptT& decay_blk, const OptT& clip_sumsq, double max_norm, const OptT& step_dev) {
   const int64_t n = master.numel();
   TORCH_CHECK(n % 64 == 0, "adamw_master: flat buffers are padded to 64 elements");
   check_cuda(master, "master", F32);
@@ -130,9 +130,10 @@ void adamw_master(const at::Tensor& master, const at::Tensor& p16, const at::Ten
   check_cuda(v, "exp_avg_sq", F32, n);
   const uint8_t* db = optr<uint8_t>(decay_blk, "decay_blk", U8, n / 64);
   const float* cs = optr<float>(clip_sumsq, "clip_sumsq", F32, 1);
+  const float* sd = optr<float>(step_dev, "step_dev", F32, 1);
   hip_check(pde_adamw_master(ptr<float>(master), p16.data_ptr(), g16.data_ptr(), ptr<float>(m), ptr<float>(v), n,
                              (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)grad_scale, (int)step, db,
-                             cs, (float)max_norm, cur_stream()),
+                             cs, (float)max_norm, sd, cur_stream()),
             "adamw_master");
 }
 
@@ -277,7 +278,7 @@ void register_transformer(pybind11::module& m) {
   m.def("adamw_master", &adamw_master, py::arg("master"), py::arg("p16"), py::arg("g16"), py::arg("m"), py::arg("v"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("grad_scale"),
         py::arg("step"), py::arg("decay_blk") = py::none(), py::arg("clip_sumsq") = py::none(),
-        py::arg("max_norm") = 1.0);
+        py::arg("max_norm") = 1.0, py::arg("step_dev") = py::none());
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("sum_f32", &sum_f32);
   m.def("colsum_bf16_splits", &colsum_bf16_splits);

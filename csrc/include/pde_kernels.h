@@ -106,7 +106,8 @@ hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* d
 hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st);
 hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m, float* v, int64_t n, float lr,
                             float b1, float b2, float eps, float wd, float grad_scale, int step,
-                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st);
+                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, const float* step_dev,
+                            hipStream_t st);
 hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
 hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st);
 int pde_colsum_bf16_splits(int C);

@@ -454,8 +454,10 @@ __global__ __launch_bounds__(256) void k_adamw_master(float* __restrict__ master
                                                       float4* __restrict__ v4, int64_t n4, float lr, float b1,
                                                       float b2, float eps, float wd, float grad_scale, int step,
                                                       const uint8_t* __restrict__ decay_blk,
-                                                      const float* __restrict__ clip_sumsq, float max_norm) {
+                                                      const float* __restrict__ clip_sumsq, float max_norm,
+                                                      const float* __restrict__ step_dev) {
   float gs = grad_scale;
+  if (step_dev) step = (int)*step_dev;               // capturable mode: the step count lives on the device
   if (clip_sumsq) {
     const float norm = sqrtf(*clip_sumsq);
     gs *= fminf(1.f, max_norm / (norm + 1e-6f));
@@ -701,11 +703,12 @@ hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hip
 
 hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m, float* v, int64_t n, float lr,
                             float b1, float b2, float eps, float wd, float grad_scale, int step,
-                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, hipStream_t st) {
+                            const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, const float* step_dev,
+                            hipStream_t st) {
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(k_adamw_master, dim3(grid_for(n4, 256, 2048)), dim3(256), 0, st, master, (uint2*)p16,
                      (const uint2*)g16, (float4*)m, (float4*)v, n4, lr, b1, b2, eps, wd, grad_scale, step, decay_blk,
-                     clip_sumsq, max_norm);
+                     clip_sumsq, max_norm, step_dev);
   return hipGetLastError();
 }
 

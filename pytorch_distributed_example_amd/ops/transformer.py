@@ -285,10 +285,17 @@ class LMHeadLossFn(torch.autograd.Function):
         h2, w, dlogits = ctx.saved_tensors
         if not (isinstance(g, torch.Tensor) and g.numel() == 1):
             raise RuntimeError("LM head loss expects a scalar gradient")
-        if float(g) != 1.0:
+        # dlogits already holds d(mean loss)/dlogits for g = 1.  Eagerly, a g != 1 rescales it (host
+        # check); inside a hipGraph capture there is no host read, so g scales the two (small) outputs
+        # instead -- exact for the usual g = 1
+        post = torch.cuda.is_current_stream_capturing()
+        if not post and float(g) != 1.0:
             dlogits.mul_(g.to(dlogits.dtype))
         dh = G.dgrad(dlogits, w)                             # [N, C]
         dw, _ = G.wgrad(dlogits, h2)                         # [Vp, C]
+        if post:
+            dh.mul_(g.to(dh.dtype))
+            dw.mul_(g.to(dw.dtype))
         return dh.reshape(ctx.hshape), dw, None, None
 
 

@@ -6,7 +6,8 @@ parameters' flat layout (shared with DDP's buckets when the model is wrapped fir
 one streaming pass with no host synchronisation:
 
 * ``AdamWMaster``: g = grad * grad_scale * min(1, max_norm / ||grad||) (global-norm clipping computed
-  on device), decoupled weight decay, torch.optim.AdamW math; writes p32 and bf16(p32).
+  on device), decoupled weight decay, torch.optim.AdamW math; writes p32 and bf16(p32).  With
+  ``capturable=True`` the step count lives on the device, so the whole step can be a hipGraph.
 * ``SGDMaster``:   torch.optim.SGD math (momentum, coupled weight decay, optional nesterov).
 
 Per-group weight decay is a per-64-element flag table (every parameter starts on a 64-element
@@ -23,6 +24,8 @@ from ..parallel.flat import FlatLayout, shared_flat
 
 class _MasterBase(torch.optim.Optimizer):
     _state_keys: tuple = ()
+
+    capturable = False
 
     def __init__(self, params, defaults, grad_scale: float):
         super().__init__(params, defaults)
@@ -68,13 +71,14 @@ class _MasterBase(torch.optim.Optimizer):
         for k in self._state_keys:
             bufs[k] = torch.zeros(n, device=dev, dtype=torch.float32)
         self._flat = dict(layout=layout, p=fp, g=fg, bufs=bufs, decay=decay.to(dev),
-                          sumsq=torch.zeros(1025, device=dev, dtype=torch.float32))   # [0] + partials
+                          sumsq=torch.zeros(1025, device=dev, dtype=torch.float32),   # [0] + partials
+                          step_dev=torch.full((1,), float(self._step), device=dev, dtype=torch.float32))
         for p in params:
             st = self.state[p]
             name = p._pde_flat[3]
             for k, buf in bufs.items():
                 st[k] = layout.view(buf, name)
-            st["step"] = torch.tensor(float(self._step))
+            st["step"] = self._flat["step_dev"] if self.capturable else torch.tensor(float(self._step))
 
     def _sync_grads(self):
         f = self._flat
@@ -111,9 +115,12 @@ class _MasterBase(torch.optim.Optimizer):
             self._build()
         self._sync_grads()
         self._step += 1
+        if self.capturable:
+            self._flat["step_dev"].add_(1.0)             # stream-ordered: a graph replay counts too
         self._kernel()
-        for p in self._all_params():
-            self.state[p]["step"] = torch.tensor(float(self._step))
+        if not self.capturable:
+            for p in self._all_params():
+                self.state[p]["step"] = torch.tensor(float(self._step))
         return loss
 
     def load_state_dict(self, state_dict):
@@ -132,6 +139,10 @@ class _MasterBase(torch.optim.Optimizer):
                     view.copy_(p.detach().float())
                 st[k] = view
             self._step = int(float(st.get("step", 0)))
+        f["step_dev"].fill_(float(self._step))
+        if self.capturable:
+            for p in self._all_params():
+                self.state[p]["step"] = f["step_dev"]
         kernels().f32_to_bf16(f["bufs"]["master"], f["p"])     # the bf16 weights follow the master copy
 
 
@@ -139,9 +150,13 @@ class AdamWMaster(_MasterBase):
     _state_keys = ("exp_avg", "exp_avg_sq")
 
     def __init__(self, params, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=None,
-                 grad_scale: float = 1.0):
+                 grad_scale: float = 1.0, capturable: bool = False):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay), grad_scale)
         self.max_grad_norm = max_grad_norm
+        # capturable (torch.optim's name): the step count is a device tensor read by the kernel, so a
+        # step captured into a hipGraph and replayed applies the right bias corrections; the per-param
+        # state "step" is then that shared device tensor
+        self.capturable = capturable
 
     def _kernel(self):
         f, K = self._flat, kernels()
@@ -153,7 +168,7 @@ class AdamWMaster(_MasterBase):
         b1, b2 = g0["betas"]
         K.adamw_master(f["bufs"]["master"], f["p"], f["g"], f["bufs"]["exp_avg"], f["bufs"]["exp_avg_sq"], g0["lr"],
                        b1, b2, g0["eps"], self._wd, self.grad_scale, self._step, f["decay"], clip,
-                       float(self.max_grad_norm or 1.0))
+                       float(self.max_grad_norm or 1.0), f["step_dev"] if self.capturable else None)
 
     def grad_norm(self) -> float:
         """Global grad norm of the last clipped step (host sync; for logging only)."""

@@ -197,6 +197,48 @@ def test_gpt2_trains():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
+def test_gpt2_step_replays_as_hipgraph():
+    """The bench's whole-step hipGraph (capturable AdamW: device step count): replays of the captured
+    step give the same weights as the same number of eager steps (bias corrections included)."""
+    cfg = _tiny_cfg()
+    torch.manual_seed(9)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 129), device=dev) for _ in range(5)]
+
+    def run(graph_mode):
+        m = build_gpt2(cfg, seed=2, device=dev)
+        opt = AdamWMaster(m.decay_groups(0.1), lr=3e-3, max_grad_norm=1.0, capturable=graph_mode)
+
+        def one(b):
+            opt.zero_grad()
+            loss = m(b[:, :-1], b[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        losses = [one(batches[0]).item(), one(batches[1]).item()]      # two eager steps first (warm-up)
+        if not graph_mode:
+            losses += [one(b).item() for b in batches[2:]]
+        else:
+            sb = batches[2].clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                sl = one(sb)
+            for b in batches[2:]:
+                sb.copy_(b)
+                g.replay()
+                losses.append(sl.item())
+        torch.cuda.synchronize()
+        return losses, [p.detach().float().clone() for p in m.parameters()], opt
+
+    le, pe, _ = run(False)
+    lg, pg, opt = run(True)
+    # (the embedding backward accumulates with float atomics: equal up to summation order)
+    assert le == pytest.approx(lg, rel=2e-3)
+    for a, b in zip(pe, pg):
+        assert rel_err(a, b) < 1e-2
+    assert float(next(iter(opt.state.values()))["step"]) == 5.0
+
+
 @pytest.mark.parametrize("N,fin,fout", [(16384, 768, 2304), (4096, 3072, 768), (300, 64, 1000), (37, 128, 24)])
 def test_linear_splitk_and_bias_grad(N, fin, fout):
     torch.manual_seed(10)
