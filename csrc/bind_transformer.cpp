@@ -114,7 +114,8 @@ void embed_bwd(const at::Tensor& dX, const at::Tensor& idx, const at::Tensor& dw
 void sumsq_bf16(const at::Tensor& g, double scale, const at::Tensor& out) {
   check_cuda(g, "g", BF16);
   check_cuda(out, "out", F32, 1025);      // [0] result, [1..1024] per-block partials
-  TORCH_CHECK(g.numel() % 4 == 0, "sumsq: numel % 4");
+  TORCH_CHECK(g.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0,
+              "sumsq: numel % 8 and a 16-byte aligned buffer");
   hip_check(pde_sumsq_bf16(g.data_ptr(), g.numel(), (float)scale, ptr<float>(out), cur_stream()), "sumsq_bf16");
 }
 
