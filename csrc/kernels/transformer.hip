@@ -261,6 +261,88 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
   m = mn;
 }
 
+// Register-resident variant (rows of <= 256 * NJ 16-byte chunks: GPT-2's 50304-wide padded vocab is
+// 6288): a thread's NJ chunks of the row are loaded ONCE, all in flight together, and both the
+// softmax statistics and the dlogits come from registers -- the two-pass kernel below reads each
+// 100 KB row twice (the second time mostly from the last-level cache) for 3 row-sized transfers;
+// this one moves 2 (read + write).
+template <int NJ>
+__global__ __launch_bounds__(256) void k_xent_bf16_reg(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt,
+                                                       int Vp, int V, float scale, float* __restrict__ loss_rows,
+                                                       int write_grad) {
+  __shared__ float shm[4], shs[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint4* Lr = reinterpret_cast<uint4*>(L + (size_t)row * Vp);
+  const int nch = Vp >> 3;
+  const int64_t t = tgt[row];
+  const int t32 = (t >= 0 && t < V) ? (int)t : -1;
+  uint4 q[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = tid + 256 * j;
+    q[j] = c < nch ? Lr[c] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  float m = -INFINITY, s = 0.f, xt = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col0 = (tid + 256 * j) * 8;
+    float v[8];
+    unpack8(q[j], v);
+    float bm = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bm = fmaxf(bm, col0 + e < V ? v[e] : -INFINITY);
+    float bs = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs += col0 + e < V ? __expf(v[e] - bm) : 0.f;
+      xt += col0 + e == t32 ? v[e] : 0.f;
+    }
+    ms_combine(m, s, bm, bs);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    ms_combine(m, s, m2, s2);
+    xt += __shfl_xor(xt, o, 64);
+  }
+  __shared__ float shx[4];
+  if (lane == 0) {
+    shm[w] = m;
+    shs[w] = s;
+    shx[w] = xt;
+  }
+  __syncthreads();
+  m = shm[0];
+  s = shs[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) ms_combine(m, s, shm[k], shs[k]);
+  xt = (shx[0] + shx[1]) + (shx[2] + shx[3]);
+  const float lse = m + __logf(s);
+  const bool valid = t >= 0 && t < V;
+  if (tid == 0) loss_rows[row] = valid ? lse - xt : 0.f;
+  if (!write_grad) return;
+  const float sc = valid ? scale : 0.f;
+  // opaque to the optimiser: the pass-1 unpacked floats are re-derived from the packed words
+  // (2 VGPRs per 4 values) instead of being kept live across the reduction (248 -> fewer VGPRs)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(q[j].x), "+v"(q[j].y), "+v"(q[j].z), "+v"(q[j].w));
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = tid + 256 * j;
+    if (c < nch) {
+      float v[8];
+      unpack8(q[j], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = c * 8 + e;
+        const float p = col < V ? __expf(v[e] - lse) : 0.f;
+        v[e] = (p - (col == t32 ? 1.f : 0.f)) * sc;
+      }
+      Lr[c] = pack8(v);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_xent_bf16(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt, int Vp,
                                                    int V, float scale, float* __restrict__ loss_rows,
                                                    int write_grad) {
@@ -682,6 +764,11 @@ hipError_t pde_gelu_bwd(const void* dY, const void* X, void* dX, int64_t n, hipS
 
 hipError_t pde_xent_bf16(void* logits, const int64_t* tgt, int N, int Vp, int V, float scale, float* loss_rows,
                          int write_grad, hipStream_t st) {
+  if ((Vp >> 3) <= 256 * 25 && Vp >= 256 * 8 * 16) {   // wide rows (GPT-2 vocab): one read, one write
+    hipLaunchKernelGGL(k_xent_bf16_reg<25>, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale,
+                       loss_rows, write_grad);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_xent_bf16, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale, loss_rows,
                      write_grad);
   return hipGetLastError();
