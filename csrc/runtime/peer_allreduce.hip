@@ -209,12 +209,16 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
       const int64_t g = (int64_t)(k / U) * a.chunk4 + i + (k % U) * stride;
       v[k] = a.in[g < last ? g : last];             // clamped: every load unconditional
     }
-    // unconditional stores to the same clamped addresses: an out-of-slice index rewrites an element
-    // with the identical input value (benign), and no branch keeps v[] out of registers
+    // stores only for this block's own slice (index inside its chunk and inside the buffer).  (An
+    // earlier version also stored clamped / next-chunk indices, "rewriting an element with the same
+    // input" -- but the all-reduce runs in place: the block owning that element may already have
+    // passed its barrier and written the REDUCED value into a.in, and the lagging block then staged
+    // that sum over the peers' input: a wrong last vector on every rank, seen with 4 ranks
+    // time-sharing one GPU.)
 #pragma unroll
     for (int k = 0; k < NC * U; ++k) {
-      const int64_t g = (int64_t)(k / U) * a.chunk4 + i + (k % U) * stride;
-      my_stage[g < last ? g : last] = v[k];
+      const int64_t idx = i + (k % U) * stride, g = (int64_t)(k / U) * a.chunk4 + idx;
+      if (idx < a.chunk4 && g <= last) my_stage[g] = v[k];
     }
   }
   const int64_t tail_off = a.n4 * Op::kPerVec;
