@@ -100,7 +100,9 @@ __device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
 #pragma unroll
     for (int c = 0; c < kPeerMaxRanks; ++c) {
       const int64_t g = (int64_t)c * chunk4 + i;
-      if (c < NC) my_stage[g < last ? g : last] = v[c];   // clamped duplicates rewrite identical values
+      // own slice only: a clamped duplicate store would re-stage a value that the in-place output
+      // of the owning virtual block may already have overwritten with the reduced sum
+      if (c < NC && g <= last) my_stage[g] = v[c];
     }
   }
   if (vb == 0 && threadIdx.x < tail) reinterpret_cast<float*>(my_stage)[n4 * 4 + threadIdx.x] = in_f[n4 * 4 + threadIdx.x];
