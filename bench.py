@@ -12,7 +12,9 @@ Adam update, loss/accuracy meters.  Each rank trains on its DistributedSampler s
 60,000-sample synthetic set (random-init weights, synthetic data: no network on the box).
 
   python bench.py --gpus N --steps K --warmup W
-  (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...)
+  (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...,
+   or the same command without a launcher: bench.py then starts the N ranks itself and relays rank 0's
+   line; a launch whose WORLD_SIZE differs from --gpus is refused with an error line, exit code 2)
 
 Every captured hipGraph -- at both step parities of the prefetching engine, so no warm-up / step count
 can leave a capture or first launch for the timed window -- is replayed (``--prime-replays``, default
@@ -185,6 +187,19 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     if gc_off:       # as timeit does: no Python GC pause between graph launches inside the window;
         gc.collect()     # collected BEFORE the warm-up, so the GPU does not idle (and clock down) for the
         gc.disable()     # collection between the last warm-up step and the timed window
+    try:
+        return _timed_window(job, eng, comm, extra, run, steps, warmup)
+    finally:
+        if gc_off:
+            gc.enable()
+
+
+def _timed_window(job, eng, comm, extra, run, steps, warmup):
+    import torch
+
+    from pytorch_distributed_example_amd import dist
+
+    world = job.world
     run(warmup)
     torch.cuda.synchronize()
     eng.read_meters(reset=True)                    # meters cover the timed steps only
@@ -205,8 +220,6 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if gc_off:
-        gc.enable()
     if trace:
         print(json.dumps({"trace_host_us": round(elapsed * 1e6, 1), "trace_launch_us": round(t_launch * 1e6, 1),
                           "trace_gpu_us": round(ev0.elapsed_time(ev1) * 1e3, 1)}), file=sys.stderr)
@@ -227,8 +240,6 @@ def lenet_main(job: _Job):
     from pytorch_distributed_example_amd import dist
 
     args, world, rank = job.args, job.world, job.rank
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(job.local_rank)
     comm_world = world > 1 or args.force_comm
     elapsed, eng, comm, extra = _run_lenet(job, args.force_comm, args.steps, args.warmup, comm_world)
@@ -278,14 +289,60 @@ def lenet_main(job: _Job):
         except Exception as e:   # noqa: BLE001 - the headline stands; report the secondary failure
             out["w1_rccl_comm"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        from pytorch_distributed_example_amd.utils.stdio import emit_result
+        emit_result(out)
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
-def main():
-    args = build_parser().parse_args()
+def _error_line(args, world, msg: str) -> dict:
+    return {"metric": BASELINE_METRIC if args.model == "lenet" else args.model, "value": None,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "error": msg}
+
+
+def _self_launch(args, argv) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes of this script, one per GPU
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1, env:// rendezvous, the launcher's
+    gang-kill on the first failure), and relay rank 0's JSON line on this process's stdout.  The
+    parent makes no HIP call (it never imports torch); the ranks' own stdout goes to stderr so the
+    relayed line stays the only one here."""
+    import tempfile
+
+    from pytorch_distributed_example_amd.launch import free_port, run_gang
+
+    fd, result = tempfile.mkstemp(prefix="pde_bench_", suffix=".json")
+    os.close(fd)
+    try:
+        cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+        rc = run_gang(cmd, args.gpus, "127.0.0.1", free_port(), extra_env={"PDE_BENCH_RESULT": result},
+                      stdout=sys.stderr)
+        with open(result) as f:
+            line = f.read().strip()
+    finally:
+        os.unlink(result)
+    if line:
+        print(line, flush=True)
+    else:
+        print(json.dumps(_error_line(args, args.gpus, f"rank 0 reported no result (gang exit code {rc})")),
+              flush=True)
+    return rc if rc else (0 if line else 1)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = build_parser().parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(_self_launch(args, argv))
     job = _Job(args)
+    print(f"[bench] rank {job.rank}/{job.world} local_rank {job.local_rank} pid {os.getpid()}", file=sys.stderr,
+          flush=True)
+    if job.world != args.gpus:
+        # a mislabelled run (e.g. --gpus 8 on a 1-rank launch) must not report as the other config
+        if job.rank == 0:
+            print(json.dumps(_error_line(args, job.world, f"--gpus {args.gpus} but WORLD_SIZE={job.world}")),
+                  flush=True)
+        sys.exit(2)
     if not args.no_spin_wait:
         # before any HIP context exists: spinning host waits keep the graph-launch path fast
         from pytorch_distributed_example_amd.utils.hipsched import set_schedule
@@ -298,9 +355,8 @@ def main():
     except Exception as e:   # noqa: BLE001 - always one JSON line, then a non-zero exit
         traceback.print_exc(file=sys.stderr)
         if job.rank == 0:
-            print(json.dumps({"metric": BASELINE_METRIC if args.model == "lenet" else args.model, "value": None,
-                              "n_gpus": job.world, "steps": args.steps, "warmup": args.warmup,
-                              "error": f"{type(e).__name__}: {e}"}), flush=True)
+            from pytorch_distributed_example_amd.utils.stdio import emit_result
+            emit_result(_error_line(args, job.world, f"{type(e).__name__}: {e}"))
         sys.exit(1)
 
 

@@ -162,7 +162,8 @@ def bench_gpt2(args):
     tps = tokens / elapsed
     flops = model.flops_per_token() * tps
     if rank == 0:
-        print(json.dumps({
+        from pytorch_distributed_example_amd.utils.stdio import emit_result
+        emit_result({
             "metric": "tokens/sec (whole node), GPT-2-small DDP",
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -174,7 +175,7 @@ def bench_gpt2(args):
                        "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **extra},
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),
             "last_loss": round(float(losses[-1]), 4),
-        }), flush=True)
+        })
     if world > 1:
         dist.destroy_process_group()
 

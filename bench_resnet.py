@@ -73,7 +73,8 @@ def bench_resnet18(args):
     elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
     ips = args.steps * B * world / elapsed
     if rank == 0:
-        print(json.dumps({
+        from pytorch_distributed_example_amd.utils.stdio import emit_result
+        emit_result({
             "metric": "images/sec (whole node), ResNet-18 bf16 DDP",
             "value": round(ips, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -85,6 +86,6 @@ def bench_resnet18(args):
                        "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", **extra,
                        "memory_format": "channels_last"},
             "last_loss": round(float(losses[-1]), 4),
-        }), flush=True)
+        })
     if world > 1:
         dist.destroy_process_group()

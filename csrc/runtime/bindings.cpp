@@ -222,6 +222,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("device", &PeerAllReduce::device)
       .def_property_readonly("is_open", &PeerAllReduce::is_open)
       .def("device_args", [](PeerAllReduce& p) { return py::bytes(p.device_args()); })
+      .def("device_probe_f32", &PeerAllReduce::device_probe_f32, py::arg("inp"), py::arg("out"), py::arg("count"),
+           py::arg("scale"), py::arg("two"), py::arg("stream"))
+      .def("debug_skip_stage", &PeerAllReduce::debug_skip_stage)
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
       .def("reset_error", &PeerAllReduce::reset_error)
       .def("set_timeout_ms", &PeerAllReduce::set_timeout_ms)

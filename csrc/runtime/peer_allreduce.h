@@ -58,6 +58,11 @@ class PeerAllReduce {
   // Device-side view (flags/data of every rank, ctrl) for kernels that run the algorithm in side
   // blocks (pde_peer_dev.h); raw bytes of a PeerDev struct.
   std::string device_args() const;
+  // The device-side protocol (pde_peer_dev.h) run as its own kernel, fp32: self-test of that path.
+  void device_probe_f32(uintptr_t in, uintptr_t out, int64_t count, float scale, int two, uintptr_t stream);
+  // Test hook: the next n host-kernel calls of this rank skip staging their input (peers then read
+  // this rank's stage buffer as it was two calls ago): the self-test must catch it.
+  void debug_skip_stage(int n) { debug_skip_stage_ = n; }
   int64_t error();
   void reset_error();
   void set_timeout_ms(int64_t ms) { timeout_ticks_ = ms * 100000; }   // s_memrealtime runs at 100 MHz
@@ -80,6 +85,7 @@ class PeerAllReduce {
   int64_t timeout_ticks_ = 10LL * 100000000;   // 10 s
   int64_t one_shot_max_ = 256 * 1024;
   int max_blocks_ = 64;
+  int debug_skip_stage_ = 0;
 };
 
 }  // namespace pde

@@ -1,5 +1,6 @@
 // Peer all-reduce over xGMI-mapped peer memory (design notes in peer_allreduce.h).
 #include "peer_allreduce.h"
+#include "pde_peer_dev.h"
 
 #include <hip/hip_runtime.h>
 
@@ -38,6 +39,7 @@ struct Args {
   int64_t timeout;                // s_memrealtime ticks
   float scale;
   int rank;
+  int skip_stage;                 // test hook: leave own stage[par] as it is (a stale-buffer injection)
 };
 
 __device__ __forceinline__ uint32_t* flag_ptr(uint8_t* region, int phase, int block, int src) {
@@ -202,7 +204,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 
   // 1. stage this rank's input.  Slices are chunk-relative (vector i of every chunk belongs to block
   //    (i / kThreads) % gridDim.x on every rank), so a block-level barrier suffices below.
-  for (int64_t i = t0; i < a.chunk4; i += U * stride) {
+  for (int64_t i = a.skip_stage ? a.chunk4 : t0; i < a.chunk4; i += U * stride) {
     vec_t v[NC * U];
 #pragma unroll
     for (int k = 0; k < NC * U; ++k) {
@@ -222,7 +224,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
     }
   }
   const int64_t tail_off = a.n4 * Op::kPerVec;
-  if (blockIdx.x == 0 && threadIdx.x < a.tail)
+  if (blockIdx.x == 0 && threadIdx.x < a.tail && !a.skip_stage)
     Op::tail_copy(reinterpret_cast<uint8_t*>(my_stage), reinterpret_cast<const uint8_t*>(a.in),
                   tail_off + threadIdx.x);
   peer_barrier<W>(a, 0, target, failed);
@@ -263,6 +265,15 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
       __hip_atomic_store(a.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// The device-side protocol of pde_peer_dev.h (run by side blocks of the fused LeNet / Adam kernels)
+// as a kernel of its own: every block is one virtual block.  Used by the self-test, so that path is
+// checked across devices before any schedule that uses it is timed.
+__global__ void __launch_bounds__(kThreads) peer_dev_probe_kernel(PeerDev d, const float* in, float* out,
+                                                                  int64_t count, float scale, int two) {
+  __shared__ uint32_t lds2[2];
+  peer_ar_f32_vblock(d, in, out, count, scale, blockIdx.x, gridDim.x, two != 0, lds2);
 }
 
 template <int W, typename Op>
@@ -391,6 +402,11 @@ void PeerAllReduce::launch(uintptr_t in, uintptr_t out, int64_t count, float sca
   a.timeout = timeout_ticks_;
   a.scale = scale;
   a.rank = rank_;
+  a.skip_stage = 0;
+  if (debug_skip_stage_ > 0) {
+    a.skip_stage = 1;
+    --debug_skip_stage_;
+  }
   const bool two = algo == 2 || (algo == 0 && world_ > 2 && count * esize > one_shot_max_);
   a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
   int64_t work = two ? a.chunk4 : a.n4;
@@ -428,6 +444,31 @@ std::string PeerAllReduce::device_args() const {
   d.rank = rank_;
   d.world = world_;
   return std::string(reinterpret_cast<const char*>(&d), sizeof(d));
+}
+
+void PeerAllReduce::device_probe_f32(uintptr_t in, uintptr_t out, int64_t count, float scale, int two,
+                                     uintptr_t stream) {
+  if (!opened_) throw std::runtime_error("peer all-reduce used before open()");
+  if (count <= 0) return;
+  if (count * 4 > cap_) throw std::invalid_argument("peer all-reduce buffer exceeds the registered capacity");
+  if ((in | out) & 15) throw std::invalid_argument("peer all-reduce needs 16-byte aligned buffers");
+  PeerDev d{};
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    d.flags[p] = p < world_ ? peer_flags_[p] : nullptr;
+    d.data[p] = p < world_ ? peers_[p] : nullptr;
+  }
+  d.ctrl = ctrl_;
+  d.cap = cap_;
+  d.timeout = timeout_ticks_;
+  d.rank = rank_;
+  d.world = world_;
+  const int64_t n4 = count / 4;
+  const int64_t work = two ? (n4 + world_ - 1) / world_ : n4;
+  int64_t nb = (work + kThreads - 1) / kThreads;
+  nb = nb < 1 ? 1 : (nb > 16 ? 16 : nb);
+  hipLaunchKernelGGL(peer_dev_probe_kernel, dim3((int)nb), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), d,
+                     reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), count, scale, two);
+  hip_check(hipGetLastError(), "peer device-path probe launch");
 }
 
 int64_t PeerAllReduce::error() {

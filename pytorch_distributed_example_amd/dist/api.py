@@ -186,18 +186,25 @@ class ProcessGroup:
         self.watchdog = None
         if rccl is not None and os.environ.get("PDE_RCCL_WATCHDOG", "1") != "0":
             self.watchdog = runtime().CommWatchdog(rccl, timeout_ms)
-        # host isend/irecv are batched until the first wait / collective: one full-duplex exchange
-        # then moves them all, so a pairwise exchange larger than the socket buffers cannot deadlock
+        # host isend/irecv are batched until the first wait / is_completed, the group's next
+        # collective or p2p call (host or RCCL), or destroy / shutdown: one full-duplex exchange then
+        # moves them all, so a pairwise exchange larger than the socket buffers cannot deadlock (a
+        # single background worker runs the group's host ops in order)
         self._p2p_pending = []
+        # started exchanges and the tensors they read / write: kept alive here until the exchange
+        # completes, even when the caller dropped the isend / irecv handle
+        self._p2p_inflight = []
 
     def p2p_flush(self):
         """Start every deferred host isend/irecv as ONE exchange (in program order)."""
+        self._p2p_inflight = [(n, k) for n, k in self._p2p_inflight if not n.is_completed()]
         if not self._p2p_pending:
             return
         pend, self._p2p_pending = self._p2p_pending, []
         sends = [(peer, t.data_ptr(), t.numel() * t.element_size()) for kind, peer, t, _ in pend if kind == "s"]
         recvs = [(peer, t.data_ptr(), t.numel() * t.element_size()) for kind, peer, t, _ in pend if kind == "r"]
         native = self.host.p2p(sends, recvs, True)
+        self._p2p_inflight.append((native, [t for _, _, t, _ in pend]))
         for _, _, t, w in pend:
             w._native = native
 
@@ -233,6 +240,10 @@ class ProcessGroup:
         return True
 
     def shutdown(self):
+        try:
+            self.p2p_flush()          # queued host isend/irecv still go out (the worker drains its queue)
+        except Exception:
+            pass
         try:
             self.host.shutdown()
         except Exception:
@@ -425,6 +436,7 @@ def destroy_process_group(group=None):
         if g is not _WORLD:
             g.shutdown()
     try:
+        _WORLD.p2p_flush()        # an un-waited isend/irecv must still reach its peer
         _WORLD.host.barrier()     # let every rank finish before the store server goes away
     except Exception:
         pass
@@ -453,6 +465,7 @@ def _check(t: torch.Tensor):
 def _gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool, what: str = "collective"):
     """Run fn(stream_handle) on the group's comm stream, ordered after the caller's stream."""
     g.check_health()
+    g.p2p_flush()        # host isend/irecv issued before this collective start now (asynchronously)
     cur = torch.cuda.current_stream(g.device)
     cs = g.comm_stream
     cs.wait_stream(cur)

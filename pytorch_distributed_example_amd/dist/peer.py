@@ -14,7 +14,8 @@ answer.  Any failure on any rank (IPC unsupported, wrong sums, a barrier time-ou
 path on every rank and the caller keeps using RCCL.
 
 ``PDE_PEER_FORCE_FAIL=<rank>[,<rank>...]`` makes those ranks fail the set-up (failure-path tests:
-every rank must then agree on RCCL only).
+every rank must then agree on RCCL only).  ``PDE_PEER_DEBUG_STALE=<rank>`` makes that rank skip
+staging one self-test call (a stale stage buffer): the self-test must then disable the path.
 
 ``tune_routes`` times RCCL against the one-/two-shot peer kernels at the sizes an engine will use
 (max over ranks, so every rank takes the same decision) and returns the fastest per size.
@@ -127,24 +128,52 @@ class PeerAllReduce:
         return int(self.native.error()) if self.native is not None else 0
 
     def _self_test(self):
+        """Both algorithms of the host kernel (f32 and bf16, ragged sizes) and the device-side protocol
+        of pde_peer_dev.h (f32, one- and two-shot), against the exact answer.  Every call gets data of
+        its own (a per-call counter is mixed into every element), and a run of consecutive calls
+        visits both stage parities several times: a rank that reads a peer's stage buffer as it was
+        one or two calls ago gets a wrong sum (``PDE_PEER_DEBUG_STALE=<rank>`` injects exactly that:
+        the rank skips staging one call).  Values are small integers, so every sum is exact in bf16."""
         W, r = self.world, self.rank
         cap_el = self.capacity_bytes // 4
         sizes = sorted({1, 3, 5, 1000, 4099, min(cap_el, 70001), cap_el - 3})
+        call = [0]
+
+        def data(n, rank, c):
+            i = torch.arange(n, device=self.device, dtype=torch.int64)
+            return (((i * 7 + c * 13 + rank * 5) % 17) - 8).to(torch.float32)
+
+        def check(x, n, dtype, what):
+            c = call[0]
+            call[0] += 1
+            torch.cuda.synchronize(self.device)
+            if self.error():
+                raise RuntimeError(f"barrier time-out during self-test ({what} {dtype} n={n} call {c})")
+            want = sum(data(n, q, c) for q in range(W)).to(dtype)
+            if not torch.equal(x, want):
+                bad = int((x != want).sum())
+                raise RuntimeError(f"{what} {dtype} n={n} call {c}: {bad} wrong elements")
+
+        stale = str(r) in os.environ.get("PDE_PEER_DEBUG_STALE", "").split(",")
         for dtype in (torch.float32, torch.bfloat16):
             for n in sizes:
                 if n <= 0 or n * (4 if dtype == torch.float32 else 2) > self.capacity_bytes:
                     continue
-                base = (torch.arange(n, device=self.device, dtype=torch.float32) % 13) - 6
+                reps = 8 if n == 4099 else 2          # 8 consecutive calls: 4 per stage parity
                 for algo in (ONE_SHOT, TWO_SHOT):
-                    x = (base * (r + 1)).to(dtype)
-                    self.all_reduce_(x, algo)
-                    torch.cuda.synchronize(self.device)
-                    if self.error():
-                        raise RuntimeError(f"barrier time-out during self-test ({algo} {dtype} n={n})")
-                    want = (base * (W * (W + 1) // 2)).to(dtype)
-                    if not torch.equal(x, want):
-                        bad = int((x != want).sum())
-                        raise RuntimeError(f"{algo} {dtype} n={n}: {bad} wrong elements")
+                    for _ in range(reps):
+                        if stale and call[0] == 5:
+                            self.native.debug_skip_stage(1)
+                        x = data(n, r, call[0]).to(dtype)
+                        self.all_reduce_(x, algo)
+                        check(x, n, dtype, algo)
+        s = torch.cuda.current_stream(self.device)
+        for n in (5, 4099, min(cap_el, 70001)):
+            for two in (0, 1):
+                for _ in range(8):
+                    x = data(n, r, call[0])
+                    self.native.device_probe_f32(x.data_ptr(), x.data_ptr(), n, 1.0, two, s.cuda_stream)
+                    check(x, n, torch.float32, "device-path two-shot" if two else "device-path one-shot")
         if self.error():
             raise RuntimeError("barrier time-out during self-test")
 

@@ -30,13 +30,13 @@ def free_port(host: str = "127.0.0.1") -> int:
         return s.getsockname()[1]
 
 
-def _spawn(cmd, env, log_dir, rank):
+def _spawn(cmd, env, log_dir, rank, stdout=None):
     out = None
     if log_dir:
         os.makedirs(log_dir, exist_ok=True)
         out = open(os.path.join(log_dir, f"rank{rank}.log"), "w")
     # own process group per rank so a kill takes the rank's children with it
-    return subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
+    return subprocess.Popen(cmd, env=env, stdout=out or stdout, stderr=subprocess.STDOUT if out else None,
                             start_new_session=True), out
 
 
@@ -60,8 +60,9 @@ def _terminate(procs, grace: float):
 
 
 def run_gang(cmd, nproc, master_addr, master_port, node_rank=0, nnodes=1, log_dir=None, extra_env=None,
-             grace=5.0, poll=0.05):
-    """Start ``nproc`` ranks of ``cmd``; returns the first failing exit code (0 if all succeed)."""
+             grace=5.0, poll=0.05, stdout=None):
+    """Start ``nproc`` ranks of ``cmd``; returns the first failing exit code (0 if all succeed).
+    ``stdout``: where the ranks' stdout goes when there is no ``log_dir`` (default: inherited)."""
     procs, files = [], []
     world = nproc * nnodes
     for local in range(nproc):
@@ -75,7 +76,7 @@ def run_gang(cmd, nproc, master_addr, master_port, node_rank=0, nnodes=1, log_di
         if nproc > 1 and "OMP_NUM_THREADS" not in (extra_env or {}) and "OMP_NUM_THREADS" not in os.environ:
             # CPU ranks share the host: split its cores instead of oversubscribing them nproc-fold
             env["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // nproc))
-        p, f = _spawn(cmd, env, log_dir, rank)
+        p, f = _spawn(cmd, env, log_dir, rank, stdout)
         procs.append(p)
         files.append(f)
     rc = 0

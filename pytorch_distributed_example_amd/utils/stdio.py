@@ -33,3 +33,17 @@ def stdout_to_stderr():
         _c_fflush()
         os.dup2(saved, 1)
         os.close(saved)
+
+
+def emit_result(obj) -> None:
+    """Print a benchmark's one JSON result line (rank 0).  Under ``bench.py``'s self-launch
+    (``PDE_BENCH_RESULT`` names a file) the line is also written there: the ranks' stdout goes to the
+    parent's stderr, and the parent relays exactly this line on its own stdout."""
+    import json
+
+    line = json.dumps(obj)
+    print(line, flush=True)
+    path = os.environ.get("PDE_BENCH_RESULT")
+    if path:
+        with open(path, "w") as f:
+            f.write(line + "\n")

@@ -192,6 +192,23 @@ def case_p2p_large(mb="8"):
     dist.destroy_process_group()
 
 
+def case_p2p_unwaited(end="barrier"):
+    """an isend whose handle is dropped (never waited) must still reach a peer that sits in
+    a blocking recv, when this rank next enters a barrier or destroy_process_group."""
+    _init("gloo")
+    n = (16 << 20) // 4                       # far above the socket buffers
+    if R == 0:
+        dist.isend(torch.arange(n, dtype=torch.float32), 1)   # handle discarded
+    elif R == 1:
+        r = torch.empty(n)
+        dist.recv(r, 0)
+        assert torch.equal(r, torch.arange(n, dtype=torch.float32))
+    if end == "barrier":
+        dist.barrier()
+    emit({"rank": R, "ok": True})
+    dist.destroy_process_group()
+
+
 def case_groups(backend="gloo"):
     _init(backend)
     dev = _dev(backend)
@@ -396,6 +413,21 @@ def case_peer_allreduce(graph="1"):
                 assert torch.all(t == want), (rep, k, t[:3])
     assert p.error() == 0
     emit({"rank": R, "sums": sums})
+    p.close()
+    dist.destroy_process_group()
+
+
+def case_peer_stale(stale_rank="-1"):
+    """The peer self-test against a deliberately stale stage buffer (PDE_PEER_DEBUG_STALE: that rank
+    skips staging one call): with per-call data the self-test must fail on every rank and disable the
+    path; without the injection it must pass (host kernel and device-side protocol)."""
+    from pytorch_distributed_example_amd.dist.peer import PeerAllReduce
+
+    dev = _shared_gpu_init()
+    g = dist.get_default_group()
+    os.environ["PDE_PEER_DEBUG_STALE"] = stale_rank
+    p = PeerAllReduce(g, dev, 1 << 20, timeout_ms=120000)
+    emit({"rank": R, "ok": bool(p.ok), "reason": p.reason})
     p.close()
     dist.destroy_process_group()
 

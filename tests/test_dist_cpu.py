@@ -66,6 +66,15 @@ def test_host_p2p_large_exchange(world):
     assert all(r and r["ok"] for r in res)
 
 
+@pytest.mark.parametrize("end", ["barrier", "destroy"])
+def test_host_isend_unwaited_still_delivered(end):
+    t0 = time.time()
+    rc, res, logs = run_ranks("p2p_unwaited", 2, end)
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res)
+    assert time.time() - t0 < 60
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_groups_and_toy_pattern(world):
     rc, res, logs = run_ranks("groups", world)
@@ -125,3 +134,40 @@ def test_bench_failure_prints_one_json_line_w2():
     out = json.loads(lines[0])
     assert out["value"] is None and out["n_gpus"] == 2 and out["error"]
     assert time.time() - t0 < 240
+
+
+def test_bench_self_launches_n_ranks_without_torchrun():
+    """Verdict r2 item 1: ``python bench.py --gpus 4`` with no launcher starts 4 rank processes itself
+    (never a silent 1-GPU run labelled otherwise) and relays exactly one JSON line carrying n_gpus 4
+    (the error line here: no GPU), with a non-zero exit code."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "4", "--warmup", "1"], cwd=root,
+                       capture_output=True, text=True, timeout=240, env=env)
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout + p.stderr
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["value"] is None and out["error"]
+    assert p.returncode != 0
+    started = {l.split()[2] for l in p.stderr.splitlines() if l.startswith("[bench] rank ")}
+    assert started == {"0/4", "1/4", "2/4", "3/4"}, p.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A launch whose WORLD_SIZE differs from --gpus prints one error line and exits 2."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "8"], cwd=root, capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert p.returncode == 2
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["value"] is None and "WORLD_SIZE=1" in out["error"] and out["n_gpus"] == 1
