@@ -79,12 +79,14 @@ def build_parser():
     return ap
 
 
-def _graph_steps(args) -> int:
-    """Steps per captured hipGraph: fewer, longer graphs mean fewer graph-to-graph transitions in the
-    timed window (--steps 20 is one replay of a 20-step graph)."""
-    if args.graph_steps > 0:
+def _graph_steps(args, n=None) -> int:
+    """Steps per captured hipGraph for a run of n steps (default --steps): fewer, longer graphs mean
+    fewer graph-to-graph transitions (~13 us each, profiles/r3_window/) -- --steps 20 is one replay
+    of a 20-step graph, --warmup 5 one replay of a 5-step graph."""
+    if args.graph_steps > 0 and n is None:
         return args.graph_steps
-    return max(d for d in range(1, min(100, max(1, args.steps)) + 1) if args.steps % d == 0)
+    n = args.steps if n is None else n
+    return max(d for d in range(1, min(100, max(1, n)) + 1) if n % d == 0)
 
 
 def _free_port() -> int:
@@ -161,9 +163,10 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     eng.set_epoch_indices(idx[: nfull * args.batch_size])   # full batches only: every timed step is B=128
 
     S = _graph_steps(args)
+    Sw = _graph_steps(args, args.warmup) if args.warmup > 0 else 1
     extra = {}
 
-    def run(n):
+    def run(n, S=S):
         if args.mode == "graph":
             for _ in range(n // S):
                 eng.replay(steps=S)             # S steps per replay
@@ -182,29 +185,46 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     if args.mode == "graph":
         # both step parities of both graphs are captured and launched once before the warm-up, so no
         # warm-up / step count can make the timed window capture or first-launch a graph
-        eng.prime_graphs((S, 1), replays=max(1, args.prime_replays))
+        eng.prime_graphs(tuple(sorted({S, Sw, 1})), replays=max(1, args.prime_replays))
     gc_off = os.environ.get("PDE_BENCH_GC") != "1"
     if gc_off:       # as timeit does: no Python GC pause between graph launches inside the window;
         gc.collect()     # collected BEFORE the warm-up, so the GPU does not idle (and clock down) for the
         gc.disable()     # collection between the last warm-up step and the timed window
     try:
-        return _timed_window(job, eng, comm, extra, run, steps, warmup)
+        return _timed_window(job, eng, comm, extra, run, steps, warmup, Sw)
     finally:
         if gc_off:
             gc.enable()
 
 
-def _timed_window(job, eng, comm, extra, run, steps, warmup):
+def _device_barrier(comm, dist):
+    """Barrier for the window brackets: an RCCL all-reduce of one element + synchronize when the group
+    has RCCL (every rank must arrive; the GPU idles for microseconds, not for a host TCP round trip
+    that lets the clocks drop before the timed window), else the host barrier."""
+    import torch
+
+    rc = comm.group.rccl if comm is not None else None
+    if rc is None:
+        dist.barrier()
+        return
+    t = torch.zeros(1, device=torch.device("cuda", rc.device))
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+
+
+def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1):
     import torch
 
     from pytorch_distributed_example_amd import dist
 
     world = job.world
-    run(warmup)
+    run(warmup, Sw)
+    # meters cover the timed steps only: zeroed on the stream (no .item() round trips: every idle
+    # microsecond before the window lets the GPU clock down, profiles/r3_window/)
+    eng.reset_meters()
     torch.cuda.synchronize()
-    eng.read_meters(reset=True)                    # meters cover the timed steps only
     if comm is not None:
-        dist.barrier()
+        _device_barrier(comm, dist)
     torch.cuda.synchronize()
     trace = os.environ.get("PDE_BENCH_TRACE") == "1"
     if trace:       # diagnostics only: GPU-clocked window and host launch time, to stderr
@@ -217,7 +237,7 @@ def _timed_window(job, eng, comm, extra, run, steps, warmup):
         ev1.record()
     torch.cuda.synchronize()
     if comm is not None:
-        dist.barrier()
+        _device_barrier(comm, dist)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if trace:

@@ -57,13 +57,34 @@ hipError_t pde_lenet_conv_fwd2(const float* Xb, int B, const float* w1, const fl
 hipError_t pde_lenet_gather(const float* X, const long long* labels, const int* idx, int n_idx, const long long* ctr,
                             int nbatches, int B, float* Xdst, long long* Ydst, int* rows_dst, hipStream_t st);
 hipError_t pde_lenet_pack_w2_v2(const float* w2, float* dst, hipStream_t st);
+// Deterministic gradient reduction / in-kernel optimizer of the v2 conv backward (lenet_v2.hip).
+struct PdeLenetBwdOpt {
+  float* slab;              // [16][25088] conv2 wgrad slabs
+  long long* c1rep;         // [16][576] int64 conv1 wgrad replicas (zeroed once; kept zero by the kernel)
+  float* c1part;            // defer mode: [16][576] float conv1 wgrad replicas (atomics)
+  unsigned* tick;           // [32] arrival counters (zeroed once)
+  float* g;                 // flat gradient buffer (canonical conv gradients written here)
+  long long c1w, c1b, c2w, c2b;
+  float* p;                 // nullptr: no in-kernel optimizer
+  float* m;
+  float* v;
+  float* Wp;
+  const long long* step;
+  long long fc_n4;
+  float lr, b1, b2, eps, wd, grad_scale;
+  int decoupled;
+  const void* peer_dev;     // fused fc-bucket all-reduce (nullptr: none)
+  float* ar_buf;
+  long long ar_n;
+  int ar_two;
+  int defer;                // 1: leave slabs / replicas for the flat optimizer to fold (no in-launch fold)
+};
 hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,
-                               const uint8_t* A2, const float* W2c, int B, float* gW1c, float* gb1c, int c1_nrep,
-                               int c1_rep_stride, float* gW2c, float* gb2c, int slab_stride, const float* row_loss,
-                               const int* row_hit, double* loss_sum, unsigned long long* correct, const float* gX,
-                               const long long* glabels, const int* gidx, int gn_idx, const long long* gctr,
-                               int gnbatches, int gstride, float* gXdst, long long* gYdst, int* grows, int dbg,
-                               hipStream_t st);
+                               const uint8_t* A2, const float* W2c, int B, const PdeLenetBwdOpt* o,
+                               const float* row_loss, const int* row_hit, double* loss_sum, unsigned long long* correct,
+                               const float* gX, const long long* glabels, const int* gidx, int gn_idx,
+                               const long long* gctr, int gnbatches, int gstride, float* gXdst, long long* gYdst,
+                               int* grows, int dbg, hipStream_t st);
 hipError_t pde_scale(float* x, long long n, float s, hipStream_t st);
 
 // ---- generic ops: csrc/kernels/generic.hip ----

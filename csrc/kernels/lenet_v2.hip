@@ -26,8 +26,14 @@
 //   the b128 A reads are conflict-free); each co-half region is padded to 72 KB = 72 LDS-DMA
 //   wave-instructions (9 per wave, a compile-time count, so the compiler's vmcnt bookkeeping stays exact).
 #include "pde_hip.h"
+
+#include <algorithm>
+#include <cstring>
+
 #include "pde_kernels.h"
 #include "pde_lenet.h"
+#include "pde_adam.h"
+#include "pde_peer_dev.h"
 
 namespace {
 
@@ -271,7 +277,69 @@ constexpr int kD_X = kD_C1 + 370;                  // [784] image
 constexpr int kD_DP1 = kD_X + kImg;                // [10][145] dP1 (ReLU-masked)
 constexpr int kD_TOT = kD_DP1 + 1450;              // 15436 floats
 constexpr int kW_TOT = kWImgs * kWImgStride + 160; // 13616 floats
-constexpr int kBwd2Lds = (kD_TOT > kW_TOT ? kD_TOT : kW_TOT) + 16;   // + meter scratch
+constexpr int kBwd2Lds = (kD_TOT > kW_TOT ? kD_TOT : kW_TOT) + 20;   // + meter scratch, flags, peer words
+constexpr int kL_FLAG = kBwd2Lds - 20;             // block-uniform flags (last-arriver decisions)
+constexpr int kL_PEER = kBwd2Lds - 18;             // two words for the peer protocol (fused all-reduce)
+
+// Deterministic gradient reduction + in-kernel optimizer (see the role comments above k_conv_bwd2).
+constexpr int kNIG = 16;                           // W image groups (= conv2 wgrad slabs)
+constexpr int kSlab = 25088;                       // floats per slab: weight [50][500] | pad | bias [50] at 25024
+constexpr int kSlabBias = 25024;
+constexpr int kC1Rep = 576;                        // int64 per conv1 replica: weight [20][25] | bias [20] at 512
+                                                   // (the layout of the conv1 slots of the flat gradient buffer)
+constexpr int kC1NRep = 16;
+constexpr float kC1Scale = 1099511627776.f;        // 2^40 fixed point for the order-free int64 sums
+constexpr double kC1InvScale = 1.0 / 1099511627776.0;
+enum { kTickTail = 16, kTickD = 17, kTickDLoaded = 18, kTicks = 32 };   // [0, 16): per-k-slice W tickets
+
+struct Bwd2Opt {
+  float* slab;                 // [16][kSlab] conv2 wgrad partials (write-through stores)
+  long long* c1rep;            // [16][kC1Rep] conv1 wgrad partials, fixed point (zero at rest; fold mode)
+  float* c1part;               // defer mode: [16][kC1Rep] conv1 wgrad replicas (atomics; zeroed by the forward)
+  unsigned* tick;              // [kTicks] arrival counters (zero at rest)
+  float* g;                    // flat gradient buffer: the folded (canonical) conv gradients land here
+  long long c1w, c1b, c2w, c2b;   // flat offsets of conv1.weight / conv1.bias / conv2.weight / conv2.bias
+  // optimizer (p == nullptr: gradients only; the caller reduces them across ranks and steps itself)
+  float* p;
+  float* m;
+  float* v;
+  float* Wp;                   // packed conv2 weight of k_conv_fwd2, rewritten with the update
+  const long long* step;       // optimizer step t (advanced by fc1 earlier in this step)
+  long long fc_n4;             // W blocks also update the flat float4 range [0, fc_n4) (the fc parameters)
+  float lr, b1, b2, eps, wd, grad_scale;
+  int decoupled;
+  // fused fc-bucket all-reduce (W > 1 "fused" schedule): W blocks [0, ar_nvb) run the xGMI peer
+  // protocol's virtual blocks over ar_buf once their own work is done
+  pde::PeerDev pd;
+  float* ar_buf;
+  long long ar_n;
+  int ar_nvb, ar_two;
+  int defer;                   // 1: no in-launch fold -- W blocks store slabs, D blocks add replicas, and the
+                               // next launch (the flat optimizer) folds both (W = 1: no seam on the chain)
+};
+
+// write-through (sc1) stores and L1-bypassing (sc1) loads for the in-kernel hand-offs
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + vmcnt(0) + barrier + one agent-scope
+// add; the last adder reads with sc1 loads)
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ long long ld_wt64(const long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One agent-scope arrival add by thread 0 after every wave drained its stores; true in every thread
+// of the block whose add completed the count.
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned count, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+  __syncthreads();
+  return *flag != 0;
+}
 
 struct Bwd2Gather {      // next-batch prefetch (nullptr X: off)
   const float* X;
@@ -291,13 +359,11 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <bool PROF>
+template <bool PROF, bool FOLD>
 __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb, const float* __restrict__ P1,
                                                    const uint8_t* __restrict__ A1, const float* __restrict__ dP2m,
                                                    const uint8_t* __restrict__ A2, const float* __restrict__ W2c,
-                                                   int B, float* __restrict__ gW1c, float* __restrict__ gb1c,
-                                                   int c1_nrep, int c1_rep_stride, float* __restrict__ gW2c,
-                                                   float* __restrict__ gb2c, int slab_stride,
+                                                   int B, Bwd2Opt op,
                                                    const float* __restrict__ row_loss, const int* __restrict__ row_hit,
                                                    double* __restrict__ loss_sum,
                                                    unsigned long long* __restrict__ correct, Bwd2Gather ga,
@@ -305,9 +371,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
   __shared__ __attribute__((aligned(16))) float smem[kBwd2Lds];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lg = l >> 4;
   PMARK(0);
-  const int nIG = slab_stride > 0 ? 16 : (B + kWImgs - 1) / kWImgs;
-  const int G = slab_stride > 0 ? (B + 15) / 16 : kWImgs;        // images per W group (<= 8)
-  const int nW = nIG * 16, nD = 2 * B, npair = min(nW, nD);
+  const int G = (B + kNIG - 1) / kNIG;             // images per W group (<= 8: B <= 128)
+  const int nW = kNIG * 16, nD = 2 * B, npair = min(nW, nD);
+  int* lflag = reinterpret_cast<int*>(smem + kL_FLAG);
   const int h = blockIdx.x;
   int role, idx;
   if (h < 2 * npair) {
@@ -339,6 +405,17 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
                         : pc < 250 ? reinterpret_cast<const float4*>(Av + (size_t)b * 50 + (pc - 200))
                                    : P1v + (size_t)b * 720 + ch * 36 + (q % 36);
       v4[j] = *src;
+    }
+    // in-kernel optimizer: this block's float4 of the fc parameters (complete since fc_bwd), loaded now
+    // so the latency hides under the MFMAs
+    const long long fci = (long long)idx * 512 + t;
+    const bool fcjob = FOLD && op.p != nullptr && fci < op.fc_n4;
+    float4 fp = make_float4(0.f, 0.f, 0.f, 0.f), fg = fp, fm = fp, fv = fp;
+    if (fcjob) {
+      fp = reinterpret_cast<const float4*>(op.p)[fci];
+      fg = reinterpret_cast<const float4*>(op.g)[fci];
+      fm = reinterpret_cast<const float4*>(op.m)[fci];
+      fv = reinterpret_cast<const float4*>(op.v)[fci];
     }
     // side jobs: meters (block 0) and the next-batch prefetch chain (its waits come after the MFMAs)
     const bool meter = (idx == 0) && row_loss && loss_sum;
@@ -421,18 +498,20 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     PMARK(2);
     float4 gx = make_float4(0.f, 0.f, 0.f, 0.f);
     if (gjob && t < 98) gx = reinterpret_cast<const float4*>(ga.X + (size_t)gsrc * kImg)[98 * ghalf + t];   // link 3
+    // conv2 wgrad partial of image group ig -> slab ig (write-through); no atomics: the last of the 16
+    // groups of this k slice folds the slabs in group order, so the gradient is bit-reproducible
+    {
+      float* sl = op.slab + (size_t)ig * kSlab;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int cor = ct * 16 + lg * 4 + r;
-      const float v = acc0[r] + acc1[r];
-      if (cor < 50) {
-        if (slab_stride > 0) {
-          const size_t rep = (size_t)ig * slab_stride;
-          if (kk < 500) gW2c[rep + cor * 500 + kk] = v;
-          else if (kk == 500) gb2c[rep + cor] = v;
-        } else {
-          if (kk < 500) atomicAdd(&gW2c[cor * 500 + kk], v);
-          else if (kk == 500) atomicAdd(&gb2c[cor], v);
+      for (int r = 0; r < 4; ++r) {
+        const int cor = ct * 16 + lg * 4 + r;
+        const float v = acc0[r] + acc1[r];
+        if (cor < 50) {
+          float* dst = kk < 500 ? sl + cor * 500 + kk : sl + kSlabBias + cor;
+          if (kk <= 500) {
+            if (!FOLD) *dst = v;           // read by the next launch: plain store
+            else st_wt(dst, v);            // read by the last-arriving block of this launch: write-through
+          }
         }
       }
     }
@@ -443,6 +522,82 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
         ga.rows_dst[grow] = gsrc;
       }
     }
+    PMARK(3);
+    if constexpr (FOLD) {
+    const long long tstep = op.p ? *op.step : 1;
+    const AdamStep as = adam_step_consts(op.lr, op.b1, op.b2, tstep);
+    if (arrive_last(op.tick + kp, kNIG, lflag)) {
+      PMARK(4);
+      // ---- last group of k slice kp: fold the 16 slabs (fixed order) -> canonical gradient (+ Adam) ----
+      if (t == 0) __hip_atomic_store(op.tick + kp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (op.p && t == 0) {
+        // every D block has its copy of W2 (the dgrad operand) in registers before W2 is overwritten
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(op.tick + kTickDLoaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nD &&
+               (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < 20000000)   // 200 ms guard (ablation runs)
+          __builtin_amdgcn_s_sleep(2);
+      }
+      __syncthreads();
+      // all loads of the fold (4 gradient items x 16 slabs per thread, + their p / m / v) issued before
+      // any use: one dependent round trip, not one per item
+      constexpr int kIt = (50 * 32 + 511) / 512;
+      float q[kIt][kNIG], pa[kIt], ma[kIt], va[kIt];
+      long long e[kIt];
+      int kk2[kIt], co2[kIt];
+#pragma unroll
+      for (int u = 0; u < kIt; ++u) {
+        const int i = t + 512 * u, co = min(i >> 5, 49), k = min(kp * 32 + (i & 31), 500);
+        co2[u] = (i < 50 * 32 && kp * 32 + (i & 31) <= 500) ? co : -1;
+        kk2[u] = k;
+        const int so = k < 500 ? co * 500 + k : kSlabBias + co;
+#pragma unroll
+        for (int r = 0; r < kNIG; ++r) q[u][r] = ld_wt(op.slab + (size_t)r * kSlab + so);
+        e[u] = k < 500 ? op.c2w + co * 500 + k : op.c2b + co;
+        if (op.p) {
+          pa[u] = op.p[e[u]];
+          ma[u] = op.m[e[u]];
+          va[u] = op.v[e[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kIt; ++u) {
+        if (co2[u] < 0) continue;
+        float gsum = q[u][0];
+#pragma unroll
+        for (int r = 1; r < kNIG; ++r) gsum += q[u][r];
+        op.g[e[u]] = gsum;
+        if (op.p) {
+          adam_elem(pa[u], ma[u], va[u], gsum * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
+                    as.step_size, as.bc2s, op.eps);
+          op.p[e[u]] = pa[u];
+          op.m[e[u]] = ma[u];
+          op.v[e[u]] = va[u];
+          if (kk2[u] < 500) op.Wp[pde_lenet_wp_index(co2[u] * 500 + kk2[u])] = pa[u];
+        }
+      }
+      if (op.p && arrive_last(op.tick + kTickTail, 16, lflag) && t == 0) {
+        __hip_atomic_store(op.tick + kTickTail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(op.tick + kTickDLoaded, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    PMARK(5);
+    // ---- fused fc-bucket all-reduce across ranks (W > 1 "fused" schedule) ----
+    if (op.ar_nvb > 0 && idx < op.ar_nvb)
+      pde::peer_ar_f32_vblock(op.pd, op.ar_buf, op.ar_buf, op.ar_n, 1.f, idx, op.ar_nvb, op.ar_two != 0,
+                              reinterpret_cast<uint32_t*>(smem + kL_PEER));
+    // ---- in-kernel optimizer: Adam on this block's float4 of the fc parameters ----
+    if (fcjob) {
+      float* pa = &fp.x; float* ga4 = &fg.x; float* ma = &fm.x; float* va = &fv.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        adam_elem(pa[j], ma[j], va[j], ga4[j] * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
+                  as.step_size, as.bc2s, op.eps);
+      reinterpret_cast<float4*>(op.p)[fci] = fp;
+      typedef float nt_f4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&fm), reinterpret_cast<nt_f4*>(op.m) + fci);
+      __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&fv), reinterpret_cast<nt_f4*>(op.v) + fci);
+    }
+    }   // FOLD
     PMARK(6);
     return;
   }
@@ -493,6 +648,12 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     reinterpret_cast<uint32_t*>(c1s)[(t / 36) * 37 + (t % 36)] = cv;    // 148-byte code rows
   }
   lds_barrier();
+  if (FOLD && op.p) {
+    // W2 (the dgrad operand) is in this block's registers: the W blocks' in-kernel Adam may now rewrite it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(op.tick + kTickDLoaded, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   PMARK(1);
   // ---- two passes of 5 input channels: dgrad -> T, col2im gather -> dP1 (ReLU mask of P1) ----
 #pragma unroll
@@ -564,12 +725,56 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
   lds_barrier();
   PMARK(5);
   if (t < 260) {
+    // conv1 wgrad|bgrad partial of this image: int64 fixed-point adds into replica (b % 16) -- integer
+    // addition is associative, so the sums are bit-identical whatever order the blocks arrive in
     const int c = t / 26, tap = t - c * 26;
     const float v = red[c * 36 + tap] + red[(16 + c) * 36 + tap] + red[(32 + c) * 36 + tap] + red[(48 + c) * 36 + tap];
     const int ch = 10 * hh + c;
-    const size_t rep = (size_t)(b % c1_nrep) * c1_rep_stride;
-    if (tap < 25) atomicAdd(&gW1c[rep + ch * 25 + tap], v);
-    else atomicAdd(&gb1c[rep + ch], v);
+    const int slot = tap < 25 ? ch * 25 + tap : 512 + ch;
+    if (!FOLD)               // float atomics into replica (b % 16) of the flat buffer, folded by the optimizer
+      atomicAdd(op.c1part + (size_t)(b % kC1NRep) * kC1Rep + slot, v);
+    else
+      atomicAdd(reinterpret_cast<unsigned long long*>(op.c1rep + (size_t)(b % kC1NRep) * kC1Rep + slot),
+                (unsigned long long)__float2ll_rn(v * kC1Scale));
+  }
+  if (FOLD && arrive_last(op.tick + kTickD, (unsigned)nD, lflag)) {
+    // ---- last D block: fold the 16 replicas (exact) -> canonical conv1 gradient (+ Adam), re-zero ----
+    if (t == 0) __hip_atomic_store(op.tick + kTickD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long tstep = op.p ? *op.step : 1;
+    const AdamStep as = adam_step_consts(op.lr, op.b1, op.b2, tstep);
+    // items: weight t (t < 500), bias t - 500 (t < 512), bias 12 + t (second slot, t < 8); all loads
+    // issued before any use: one dependent round trip
+    long long q[2][kC1NRep];
+    float pv[2], mv[2], vv[2];
+    long long e[2];
+    int slot[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int bi = u == 0 ? t - 500 : 12 + min(t, 7);                 // bias index when not a weight
+      slot[u] = (u == 0 && t < 500) ? t : 512 + min(bi, 19);
+      e[u] = (u == 0 && t < 500) ? op.c1w + t : op.c1b + min(bi, 19);
+#pragma unroll
+      for (int r = 0; r < kC1NRep; ++r) q[u][r] = ld_wt64(op.c1rep + (size_t)r * kC1Rep + slot[u]);
+      if (op.p) {
+        pv[u] = op.p[e[u]]; mv[u] = op.m[e[u]]; vv[u] = op.v[e[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && t >= 8) break;
+      long long acc = 0;
+#pragma unroll
+      for (int r = 0; r < kC1NRep; ++r) acc += q[u][r];
+      const float gsum = (float)((double)acc * kC1InvScale);
+      op.g[e[u]] = gsum;
+      if (op.p) {
+        adam_elem(pv[u], mv[u], vv[u], gsum * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
+                  as.step_size, as.bc2s, op.eps);
+        op.p[e[u]] = pv[u]; op.m[e[u]] = mv[u]; op.v[e[u]] = vv[u];
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < kC1NRep * kC1Rep; i += 512) op.c1rep[i] = 0;
   }
   PMARK(6);
 }
@@ -604,25 +809,46 @@ hipError_t pde_lenet_gather(const float* X, const long long* labels, const int* 
 }
 
 hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,
-                               const uint8_t* A2, const float* W2c, int B, float* gW1c, float* gb1c, int c1_nrep,
-                               int c1_rep_stride, float* gW2c, float* gb2c, int slab_stride, const float* row_loss,
-                               const int* row_hit, double* loss_sum, unsigned long long* correct, const float* gX,
-                               const long long* glabels, const int* gidx, int gn_idx, const long long* gctr,
-                               int gnbatches, int gstride, float* gXdst, long long* gYdst, int* grows, int dbg,
-                               hipStream_t st) {
-  if (slab_stride > 0 && B > 128) return hipErrorInvalidValue;      // 16 groups of <= 8 images
-  const int nIG = slab_stride > 0 ? 16 : (B + kWImgs - 1) / kWImgs;
-  const int nblk = nIG * 16 + 2 * B;
+                               const uint8_t* A2, const float* W2c, int B, const PdeLenetBwdOpt* o,
+                               const float* row_loss, const int* row_hit, double* loss_sum, unsigned long long* correct,
+                               const float* gX, const long long* glabels, const int* gidx, int gn_idx,
+                               const long long* gctr, int gnbatches, int gstride, float* gXdst, long long* gYdst,
+                               int* grows, int dbg, hipStream_t st) {
+  if (B < 1 || B > 128) return hipErrorInvalidValue;                  // 16 image groups of <= 8 images
+  if (o->fc_n4 > (long long)kNIG * 16 * 512) return hipErrorInvalidValue;   // one float4 per W thread
+  const int nblk = kNIG * 16 + 2 * B;
   Bwd2Gather ga{gX, glabels, gidx, gn_idx, gctr, gnbatches, gstride, gXdst, gYdst, grows};
+  Bwd2Opt op{};
+  op.slab = o->slab;
+  op.c1rep = o->c1rep;
+  op.c1part = o->c1part;
+  op.tick = o->tick;
+  op.g = o->g;
+  op.c1w = o->c1w; op.c1b = o->c1b; op.c2w = o->c2w; op.c2b = o->c2b;
+  op.p = o->p; op.m = o->m; op.v = o->v; op.Wp = o->Wp; op.step = o->step; op.fc_n4 = o->p ? o->fc_n4 : 0;
+  op.lr = o->lr; op.b1 = o->b1; op.b2 = o->b2; op.eps = o->eps; op.wd = o->wd; op.grad_scale = o->grad_scale;
+  op.decoupled = o->decoupled;
+  op.defer = o->defer;
+  if (o->peer_dev != nullptr && o->ar_buf != nullptr && o->ar_n > 0) {
+    std::memcpy(&op.pd, o->peer_dev, sizeof(op.pd));
+    op.ar_buf = o->ar_buf;
+    op.ar_n = o->ar_n;
+    op.ar_two = o->ar_two;
+    const long long n4 = o->ar_n / 4, work = o->ar_two ? (n4 + op.pd.world - 1) / op.pd.world : n4;
+    op.ar_nvb = (int)std::min<long long>(32, std::max<long long>(1, (work + 511) / 512));
+  }
   unsigned long long* prof = pde_lenet_prof_slot(4);
-  if (prof)
-    hipLaunchKernelGGL(k_conv_bwd2<true>, dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
-                       c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, gW2c, gb2c, slab_stride, row_loss, row_hit, loss_sum,
-                       correct, ga, dbg, prof);
-  else
-    hipLaunchKernelGGL(k_conv_bwd2<false>, dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, gW1c, gb1c,
-                       c1_nrep < 1 ? 1 : c1_nrep, c1_rep_stride, gW2c, gb2c, slab_stride, row_loss, row_hit, loss_sum,
-                       correct, ga, dbg, nullptr);
+#define PDE_BWD2_LAUNCH(P, F)                                                                                  \
+  hipLaunchKernelGGL((k_conv_bwd2<P, F>), dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, op, row_loss, \
+                     row_hit, loss_sum, correct, ga, dbg, P ? prof : nullptr)
+  if (prof) {
+    if (op.defer) PDE_BWD2_LAUNCH(true, false);
+    else PDE_BWD2_LAUNCH(true, true);
+  } else {
+    if (op.defer) PDE_BWD2_LAUNCH(false, false);
+    else PDE_BWD2_LAUNCH(false, true);
+  }
+#undef PDE_BWD2_LAUNCH
   return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 #include "pde_kernels.h"
 #include "pde_lenet.h"
 #include "pde_peer_dev.h"
+#include "pde_adam.h"
 
 #include <algorithm>
 #include <cstring>
@@ -164,18 +165,6 @@ __device__ __forceinline__ void wait_epoch(const long long* epoch, long long t, 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-}
-
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr, float lr, float wd, int decoupled,
-                                          float omb1, float omb2, float b2, float step_size, float bc2s, float eps) {
-  if (wd != 0.f) {
-    if (decoupled) p = p * (1.f - lr * wd);
-    else gr = gr + wd * p;
-  }
-  m = m + omb1 * (gr - m);
-  v = v * b2 + omb2 * gr * gr;
-  const float denom = sqrtf(v) / bc2s + eps;
-  p = p - step_size * (m / denom);
 }
 
 template <bool PROF>

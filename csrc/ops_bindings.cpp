@@ -8,6 +8,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
 
+#include <cmath>
 #include <optional>
 
 #include "pde_kernels.h"
@@ -328,27 +329,68 @@ void lenet_gather(const at::Tensor& X, const at::Tensor& labels, const OptT& idx
 }
 
 void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& dP2m,
-                     const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& gW1c,
-                     const at::Tensor& gb1c, int64_t c1_nrep, int64_t c1_rep_stride, const at::Tensor& gW2c,
-                     const at::Tensor& gb2c, int64_t slab_stride, const OptT& row_loss, const OptT& row_hit,
+                     const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& slab,
+                     const at::Tensor& c1rep, const at::Tensor& c1part, const at::Tensor& tick, const at::Tensor& g, int64_t c1w, int64_t c1b,
+                     int64_t c2w, int64_t c2b, const OptT& p, const OptT& m, const OptT& v, const OptT& Wp,
+                     const OptT& step, int64_t fc_n, double lr, double b1, double b2, double eps, double wd,
+                     bool decoupled, double grad_scale, const OptT& row_loss, const OptT& row_hit,
                      const OptT& loss_sum, const OptT& correct, const OptT& gX, const OptT& glabels, const OptT& gidx,
                      const OptT& gctr, int64_t gnbatches, int64_t gstride, const OptT& gXdst, const OptT& gYdst,
-                     const OptT& grows, int64_t dbg) {
-  TORCH_CHECK(B >= 1 && B <= 512, "conv_bwd2: batch must be in [1, 512]");
-  TORCH_CHECK(slab_stride == 0 || B <= 128, "conv_bwd2: gradient slabs need B <= 128");
+                     const OptT& grows, const OptT& peer_dev, const OptT& ar_buf, int64_t ar_two, int64_t defer,
+                     int64_t dbg) {
+  TORCH_CHECK(B >= 1 && B <= 128, "conv_bwd2: batch must be in [1, 128] (16 image groups of <= 8 images)");
   check_cuda(Xb, "Xb", F32, B * 784);
   check_cuda(P1, "P1", F32, B * 2880);
   check_cuda(A1, "A1", U8, B * 2880);
   check_cuda(dP2m, "dP2m", F32, B * 800);
   check_cuda(A2, "A2", U8, B * 800);
   check_cuda(W2c, "conv2.weight", F32, 25000);
-  const int64_t nrep = std::max<int64_t>(1, c1_nrep);
-  check_cuda(gW1c, "conv1 grad", F32, (nrep - 1) * c1_rep_stride + 500);
-  check_cuda(gb1c, "conv1 bias grad", F32, (nrep - 1) * c1_rep_stride + 20);
-  check_cuda(gW2c, "conv2 grad", F32, slab_stride > 0 ? 15 * slab_stride + 25000 : 25000);
-  check_cuda(gb2c, "conv2 bias grad", F32, slab_stride > 0 ? 15 * slab_stride + 50 : 50);
-  for (const at::Tensor* t : {&Xb, &P1, &dP2m})
+  check_cuda(slab, "slab", F32, 15 * 25088 + 25074);
+  check_cuda(c1rep, "c1rep", I64, 16 * 576);
+  check_cuda(c1part, "c1part", F32, 16 * 576);
+  check_cuda(tick, "tick", I32, 32);
+  check_cuda(g, "grads", F32);
+  const int64_t n = g.numel();
+  TORCH_CHECK(c1w >= 0 && c1w + 500 <= n && c1b >= 0 && c1b + 20 <= n && c2w >= 0 && c2w + 25000 <= n && c2b >= 0 &&
+                  c2b + 50 <= n, "conv_bwd2: conv gradient slots outside the flat buffer");
+  for (const at::Tensor* t : {&Xb, &P1, &dP2m, &g})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv_bwd2 operands must be 16-B aligned");
+  PdeLenetBwdOpt o{};
+  o.slab = ptr<float>(slab);
+  o.c1rep = ptr<long long>(c1rep);
+  o.c1part = ptr<float>(c1part);
+  o.tick = reinterpret_cast<unsigned*>(tick.data_ptr<int32_t>());
+  o.g = ptr<float>(g);
+  o.c1w = c1w; o.c1b = c1b; o.c2w = c2w; o.c2b = c2b;
+  if (p.has_value()) {
+    TORCH_CHECK(m.has_value() && v.has_value() && Wp.has_value() && step.has_value(),
+                "conv_bwd2 in-kernel Adam needs p, m, v, Wp and the step counter");
+    for (const OptT* t : {&p, &m, &v}) {
+      check_cuda(**t, "p/m/v", F32, n);
+      TORCH_CHECK(reinterpret_cast<uintptr_t>((*t)->data_ptr()) % 16 == 0, "p/m/v must be 16-B aligned");
+    }
+    TORCH_CHECK(fc_n >= 0 && fc_n % 4 == 0 && fc_n <= n && fc_n <= 16 * 16 * 512 * 4, "conv_bwd2: bad fc range");
+    o.p = ptr<float>(*p);
+    o.m = ptr<float>(*m);
+    o.v = ptr<float>(*v);
+    o.Wp = optr<float>(Wp, "Wp", F32, kPdeWpFloats);
+    o.step = optr<long long>(step, "step", I64, 1);
+    o.fc_n4 = fc_n / 4;
+  }
+  o.lr = (float)lr; o.b1 = (float)b1; o.b2 = (float)b2; o.eps = (float)eps; o.wd = (float)wd;
+  o.grad_scale = (float)grad_scale;
+  o.decoupled = decoupled ? 1 : 0;
+  o.defer = defer ? 1 : 0;
+  TORCH_CHECK(!(defer && p.has_value()), "conv_bwd2: the in-launch optimizer needs the in-launch fold (defer=0)");
+  if (peer_dev.has_value()) {
+    TORCH_CHECK(peer_dev->numel() == (int64_t)sizeof(pde::PeerDev), "bad peer device args");
+    check_cuda(*ar_buf, "ar_buf", F32);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(ar_buf->data_ptr()) % 16 == 0, "ar_buf must be 16-B aligned");
+    o.peer_dev = peer_dev->data_ptr();
+    o.ar_buf = ptr<float>(*ar_buf);
+    o.ar_n = ar_buf->numel();
+    o.ar_two = (int)ar_two;
+  }
   const bool meters = row_loss.has_value() && row_hit.has_value() && loss_sum.has_value() && correct.has_value();
   const bool gather = gX.has_value();
   if (gather) {
@@ -358,11 +400,9 @@ void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tenso
     check_cuda(*gX, "gX", F32);
     check_cuda(*gXdst, "gXdst", F32, B * 784);
     check_cuda(*gYdst, "gYdst", I64, B);
-    check_cuda(*grows, "grows", I32, B);
   }
   hip_check(pde_lenet_conv_bwd2(ptr<float>(Xb), ptr<float>(P1), ptr<uint8_t>(A1), ptr<float>(dP2m), ptr<uint8_t>(A2),
-                                ptr<float>(W2c), (int)B, ptr<float>(gW1c), ptr<float>(gb1c), (int)nrep,
-                                (int)c1_rep_stride, ptr<float>(gW2c), ptr<float>(gb2c), (int)slab_stride,
+                                ptr<float>(W2c), (int)B, &o,
                                 meters ? ptr<float>(*row_loss) : nullptr, meters ? ptr<int>(*row_hit) : nullptr,
                                 meters ? ptr<double>(*loss_sum) : nullptr,
                                 meters ? reinterpret_cast<unsigned long long*>(correct->data_ptr<int64_t>()) : nullptr,
@@ -568,12 +608,17 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_conv_fwd2", &lenet_conv_fwd2, py::arg("Xb"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wp"),
         py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("zero") = py::none());
   m.def("lenet_conv_bwd2", &lenet_conv_bwd2, py::arg("Xb"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
-        py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("gW1c"), py::arg("gb1c"), py::arg("c1_nrep"),
-        py::arg("c1_rep_stride"), py::arg("gW2c"), py::arg("gb2c"), py::arg("slab_stride"),
+        py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("slab"), py::arg("c1rep"), py::arg("c1part"), py::arg("tick"),
+        py::arg("g"),
+        py::arg("c1w"), py::arg("c1b"), py::arg("c2w"), py::arg("c2b"), py::arg("p") = py::none(),
+        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("Wp") = py::none(), py::arg("step") = py::none(),
+        py::arg("fc_n") = 0, py::arg("lr") = 1e-3, py::arg("b1") = 0.9, py::arg("b2") = 0.999, py::arg("eps") = 1e-8,
+        py::arg("wd") = 0.0, py::arg("decoupled") = false, py::arg("grad_scale") = 1.0,
         py::arg("row_loss") = py::none(), py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(),
         py::arg("correct") = py::none(), py::arg("gX") = py::none(), py::arg("glabels") = py::none(),
         py::arg("gidx") = py::none(), py::arg("gctr") = py::none(), py::arg("gnbatches") = 1, py::arg("gstride") = 0,
         py::arg("gXdst") = py::none(), py::arg("gYdst") = py::none(), py::arg("grows") = py::none(),
+        py::arg("peer_dev") = py::none(), py::arg("ar_buf") = py::none(), py::arg("ar_two") = 0, py::arg("defer") = 0,
         py::arg("dbg") = 0);
   m.def("lenet_gather", &lenet_gather, py::arg("X"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
         py::arg("nbatches"), py::arg("B"), py::arg("Xdst"), py::arg("Ydst"), py::arg("rows_dst"));

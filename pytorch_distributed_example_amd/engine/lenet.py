@@ -33,11 +33,12 @@ from ..ops.lenet_fused import pack_conv2_weight
 from ..parallel.flat import FlatLayout
 
 FC_BUCKET = ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"]
-CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv1.grad_replicas", "conv2.weight", "conv2.bias"]
+CONV_BUCKET = ["conv1.weight", "conv1.bias", "conv1.grad_replicas", "conv2.weight", "conv2.bias"]   # v1
+CONV_BUCKET_V2 = ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"]
 C1_NREP = 16          # conv1 gradient replicas (atomic contention: 128 images -> 8 adders per address)
-C1_STRIDE = 576       # conv1.weight (500 -> 512 slot) + conv1.bias (20 -> 64 slot)
-C2_NREP = 16          # conv2 wgrad slabs of the v2 step (one per 8-image group, folded by the optimizer)
-C2_STRIDE = 25088     # conv2.weight (25000 -> 25024 slot) + conv2.bias (50 -> 64 slot)
+C1_STRIDE = 576       # conv1.weight (500 -> 512 slot) + conv1.bias (20 -> 64 slot); v2: int64 [500 | 20] + pad
+C2_NREP = 16          # conv2 wgrad slabs of the v2 step (one per 8-image group, folded inside the launch)
+C2_STRIDE = 25088     # slab: conv2.weight [25000] | pad | conv2.bias [50] at 25024
 
 
 class LeNetTrainStep:
@@ -69,41 +70,69 @@ class LeNetTrainStep:
         self.K = kernels()
         dev = self.device
         # v2 step (csrc/kernels/lenet_v2.hip): prefetched batches, LDS-DMA weight staging, 8-wave conv
-        # forward, co-resident conv backward.  W = 1 (no comm path): the conv2 weight gradient is
-        # written as 16 deterministic per-image-group slabs folded by the optimizer; with a comm path
-        # the slabs would multiply the all-reduced bytes, so it is accumulated with float atomics.
-        self.v2 = (os.environ.get("PDE_LENET_V2", "1") != "0") if v2 is None else bool(v2)
-        self.slabs = self.v2 and not self.comm_on and self.B <= 128
-        extra = {"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,)}
-        conv_bucket = list(CONV_BUCKET)
-        if self.slabs:
-            extra["conv2.grad_replicas"] = ((C2_NREP - 1) * C2_STRIDE,)
-            conv_bucket.append("conv2.grad_replicas")
-        self.layout = FlatLayout([(n, tuple(p.shape)) for n, p in net.named_parameters()], [FC_BUCKET, conv_bucket],
-                                 extra_shapes=extra)
+        # forward, co-resident conv backward that reduces its weight gradients deterministically inside
+        # the launch (conv2: 16 per-image-group slabs folded in group order by the last-arriving block
+        # of each k slice; conv1: order-free int64 fixed-point sums) into the canonical gradient slots,
+        # so the all-reduced conv bucket is exactly the conv parameters.  At W = 1 with Adam the same
+        # launch also runs the optimizer (no separate Adam kernel: the folding blocks update the conv
+        # parameters, every W block one float4 of the fc parameters).  v1 (lenet.hip) for B > 128.
+        self.v2 = ((os.environ.get("PDE_LENET_V2", "1") != "0") if v2 is None else bool(v2)) and self.B <= 128
+        # where the conv weight gradients are reduced (v2), all deterministic:
+        #   "defer" (W = 1 default): the conv backward stores its partials (16 conv2 slabs, 16 int64 conv1
+        #           replicas) and the flat optimizer's fold blocks reduce them -- no seam on the chain;
+        #   "fold"  (W > 1): the last-arriving blocks of the conv backward fold them into the canonical
+        #           slots inside the launch, so the all-reduced conv bucket is just the conv parameters;
+        #   "opt"   (W = 1, Adam): "fold" plus the whole optimizer step inside the same launch.
+        # PDE_LENET_BWD_MODE overrides the W = 1 choice (A/B runs).
+        mode = os.environ.get("PDE_LENET_BWD_MODE", "defer")
+        if self.comm_on:
+            mode = "fold"
+        elif mode == "opt" and optimizer != "adam":
+            mode = "defer"
+        self.bwd_mode = mode if self.v2 else "v1"
+        self.opt_in_bwd = self.bwd_mode == "opt"
+        dev = self.device
+        named = [(n, tuple(p.shape)) for n, p in net.named_parameters()]
+        if self.bwd_mode == "defer":
+            # gradient replicas in the flat buffer (replica 0 = the canonical slot), folded in fixed order
+            # by the optimizer's fold blocks: conv1 as 16 atomic-add replicas, conv2 as 16 image-group slabs
+            self.layout = FlatLayout(named, [FC_BUCKET, CONV_BUCKET + ["conv2.grad_replicas"]],
+                                     extra_shapes={"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,),
+                                                   "conv2.grad_replicas": ((C2_NREP - 1) * C2_STRIDE,)})
+        elif self.v2:
+            self.layout = FlatLayout(named, [FC_BUCKET, CONV_BUCKET_V2])
+        else:
+            self.layout = FlatLayout(named, [FC_BUCKET, CONV_BUCKET],
+                                     extra_shapes={"conv1.grad_replicas": ((C1_NREP - 1) * C1_STRIDE,)})
         self.params, self.grads = self.layout.bind(net)
         V = self.layout.view
         self.p = {n: V(self.params, n) for n in self.layout.param_names}
         self.g = {n: V(self.grads, n) for n in self.layout.param_names}
-        c1 = self.layout.slots["conv1.weight"].offset
-        assert self.layout.slots["conv1.bias"].offset == c1 + 512
-        assert self.layout.slots["conv1.grad_replicas"].offset == c1 + C1_STRIDE
+        self.off = {n: self.layout.slots[n].offset for n in self.layout.param_names}
+        c1 = self.off["conv1.weight"]
         self.c1_off = c1
-        self.g_c1w_rep = self.grads[c1: c1 + C1_NREP * C1_STRIDE]
-        self.g_c1b_rep = self.grads[c1 + 512: c1 + C1_NREP * C1_STRIDE]
-        c2 = self.layout.slots["conv2.weight"].offset
-        assert self.layout.slots["conv2.bias"].offset == c2 + 25024
-        self.c2_off = c2
-        if self.slabs:
-            assert self.layout.slots["conv2.grad_replicas"].offset == c2 + C2_STRIDE
-            self.g_c2w_rep = self.grads[c2: c2 + C2_NREP * C2_STRIDE]
-            self.g_c2b_rep = self.grads[c2 + 25024: c2 + C2_NREP * C2_STRIDE]
-            self.zero_view = self.grads[c1: c1 + C1_NREP * C1_STRIDE]    # only the atomic targets
-        else:
-            self.g_c2w_rep = self.grads[c2: c2 + 25000]
-            self.g_c2b_rep = self.grads[c2 + 25024: c2 + 25024 + 50]
+        self.c2_off = self.off["conv2.weight"]
         self.bucket_grads = [self.layout.bucket_view(self.grads, i) for i in range(2)]
-        if not self.slabs:
+        o = self.off
+        assert o["conv1.bias"] == c1 + 512 and o["conv2.bias"] == self.c2_off + 25024
+        if self.v2:
+            self.c1rep = torch.zeros(C1_NREP * C1_STRIDE, device=dev, dtype=torch.int64)   # kept zero by the kernel
+            self.tick = torch.zeros(32, device=dev, dtype=torch.int32)                      # arrival counters
+        if self.bwd_mode == "defer":
+            assert self.layout.slots["conv1.grad_replicas"].offset == c1 + C1_STRIDE
+            assert self.layout.slots["conv2.grad_replicas"].offset == self.c2_off + C2_STRIDE
+            self.c1part = self.grads[c1: c1 + C1_NREP * C1_STRIDE]
+            self.slab = self.grads[self.c2_off: self.c2_off + C2_NREP * C2_STRIDE]
+            self.zero_view = self.c1part              # zeroed by the conv forward (atomic targets)
+        elif self.v2:
+            assert o["conv2.weight"] == c1 + C1_STRIDE
+            self.slab = torch.zeros(C2_NREP * C2_STRIDE, device=dev, dtype=torch.float32)
+            self.c1part = torch.zeros(C1_NREP * C1_STRIDE, device=dev, dtype=torch.float32)   # unused in fold mode
+            self.zero_view = None
+        else:
+            assert self.layout.slots["conv1.grad_replicas"].offset == c1 + C1_STRIDE
+            self.g_c1w_rep = self.grads[c1: c1 + C1_NREP * C1_STRIDE]
+            self.g_c1b_rep = self.grads[c1 + 512: c1 + C1_NREP * C1_STRIDE]
             self.zero_view = self.bucket_grads[1]
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params) if optimizer == "adam" else self.m
@@ -177,21 +206,25 @@ class LeNetTrainStep:
                                 self.Yb[self.q], self.rowsb[self.q])
 
     # ------------------------------------------------------------------ the step
-    def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None):
+    def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None, B: Optional[int] = None):
         """Fused optimizer update of the flat range [lo, hi) (one bucket or everything).  The conv
-        range carries the conv2 weight repack (Wt2) and the conv1 gradient-replica fold.
+        range carries the conv2 weight repack (Wp / Wt2) and, in the v1 layout, the conv1
+        gradient-replica fold (v2 writes canonical gradients, nothing to fold).
         ``fuse_ar`` ('adam1' / 'adam2'): side blocks of the Adam kernel all-reduce the conv bucket
         (one- / two-shot peer protocol) while the other blocks update the fc parameters."""
         K, sl = self.K, slice(lo, hi)
+        B = B or self.B
         pack_off = self.pack_off - lo if conv else -1
-        fold_off = self.c1_off - lo if conv else -1
-        f2 = dict(fold2_off=self.c2_off - lo, fold2_len=C2_STRIDE, fold2_nrep=C2_NREP,
-                  fold2_stride=C2_STRIDE) if (conv and self.slabs) else {}
-        pack = self.Wt2 if conv else None
+        pack, mode = (self.Wp, 2) if self.v2 else (self.Wt2, 1)
+        if not conv:
+            pack = None
+        folds = {}
+        if conv and self.bwd_mode == "v1":        # in-layout float conv1 replicas
+            folds = dict(fold_off=self.c1_off - lo, fold_len=C1_STRIDE, fold_nrep=C1_NREP, fold_stride=C1_STRIDE)
+        elif conv and self.bwd_mode == "defer":   # conv2 slabs + int64 conv1 replicas of the conv backward
+            folds = dict(fold_off=self.c1_off - lo, fold_len=C1_STRIDE, fold_nrep=C1_NREP, fold_stride=C1_STRIDE,
+                         fold2_off=self.c2_off - lo, fold2_len=C2_STRIDE, fold2_nrep=C2_NREP, fold2_stride=C2_STRIDE)
         scale = 1.0 / self.world
-        mode = 1
-        if conv and self.v2:
-            pack, mode = self.Wp, 2
         if self.optimizer == "adam":
             far = {}
             if fuse_ar is not None:
@@ -199,11 +232,32 @@ class LeNetTrainStep:
                            ar_epoch=self.ar_epoch, ar_two=int(fuse_ar == "adam2"))
             K.adam_flat(self.params[sl], self.grads[sl], self.m[sl], self.v[sl], self.lr, self.betas[0],
                         self.betas[1], self.eps, self.wd, False, scale, self.counters, self.arrive, -1, pack_off,
-                        pack, fold_off, C1_STRIDE, C1_NREP, C1_STRIDE, pack_mode=mode, **f2, **far)
+                        pack, pack_mode=mode, **folds, **far)
         else:
             K.sgd_flat(self.params[sl], self.grads[sl], self.m[sl], self.lr, self.momentum, 0.0, self.wd, False,
-                       scale, self.counters, self.arrive, -1, pack_off, pack, fold_off, C1_STRIDE, C1_NREP,
-                       C1_STRIDE, pack_mode=mode, **f2)
+                       scale, self.counters, self.arrive, -1, pack_off, pack, pack_mode=mode, **folds)
+
+    def _conv_bwd2(self, B: int, q: int, fused_fc_route: Optional[str] = None):
+        """The v2 conv backward: deterministic in-launch gradient reduction, the next batch's prefetch,
+        the meters, and (W = 1, Adam) the whole optimizer step; ``fused_fc_route`` ('peer1' / 'peer2'):
+        its W blocks also all-reduce the fc bucket across ranks once their own work is done."""
+        p = self.p
+        kw = dict(row_loss=self.row_loss, row_hit=self.row_hit, loss_sum=self.loss_sum, correct=self.correct,
+                  gX=self.X, glabels=self.Y, gidx=self.idx, gctr=self.counters[1:], gnbatches=self.nbatches,
+                  gstride=self.B, gXdst=self.Xb[1 - q], gYdst=self.Yb[1 - q], grows=self.rowsb[1 - q],
+                  dbg=self.bwd_dbg)
+        if self.opt_in_bwd:
+            kw.update(p=self.params, m=self.m, v=self.v, Wp=self.Wp, step=self.counters,
+                      fc_n=self.bucket_ranges[0][1], lr=self.lr, b1=self.betas[0], b2=self.betas[1], eps=self.eps,
+                      wd=self.wd, decoupled=False, grad_scale=1.0 / self.world)
+        if fused_fc_route is not None:
+            kw.update(peer_dev=self._peer_device_args(), ar_buf=self.bucket_grads[0],
+                      ar_two=int(fused_fc_route == "peer2"))
+        kw["defer"] = int(self.bwd_mode == "defer")
+        o = self.off
+        self.K.lenet_conv_bwd2(self.Xb[q], self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B, self.slab,
+                               self.c1rep, self.c1part, self.tick, self.grads, o["conv1.weight"], o["conv1.bias"],
+                               o["conv2.weight"], o["conv2.bias"], **kw)
 
     def _launch(self, B: int):
         """One step on the current stream: conv_fwd -> fc1 -> head -> fc_bwd -> conv_bwd -> opt.
@@ -244,35 +298,29 @@ class LeNetTrainStep:
         K.lenet_fc1_fwd(self.P2, B, p["fc1.weight"], p["fc1.bias"], self.H1, self.counters)   # bumps counters
         K.lenet_head(self.H1, B, p["fc2.weight"], p["fc2.bias"], labels, 1.0 / B, None, self.dZ2, self.dZ1,
                      self.row_loss, self.row_hit, None, None)
-        fused = self.comm_on and self.mode == "fused"
         if self.v2:
             self.q = 1 - q
-            if fused:       # the first-generation conv backward (peer side blocks) has no prefetch role
-                K.lenet_gather(self.X, self.Y, self.idx, self.counters[1:], self.nbatches, self.B, self.Xb[1 - q],
-                               self.Yb[1 - q], self.rowsb[1 - q])
+        fused = self.comm_on and self.mode == "fused"
         # the loss / accuracy meters are folded by an extra block of conv_bwd (off fc_bwd's chain)
         fc_args = (self.P2, self.H1, self.dZ1, self.dZ2, p["fc1.weight"], B, self.dP2m, g["fc1.weight"],
                    g["fc1.bias"], g["fc2.weight"], g["fc2.bias"], None, None, None, None)
-        conv_args = (self.X, rows, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
-                     self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE,
-                     self.row_loss, self.row_hit, self.loss_sum, self.correct)
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)
-        if self.v2 and not fused:
-            # conv backward v2; D blocks also prefetch the next batch (counters[1] was advanced by fc1)
-            # into the other parity's buffers and fold the meters
-            conv_bwd = lambda: K.lenet_conv_bwd2(
-                self.Xb[q], self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B, self.g_c1w_rep,
-                self.g_c1b_rep, C1_NREP, C1_STRIDE, self.g_c2w_rep, self.g_c2b_rep, C2_STRIDE if self.slabs else 0,
-                self.row_loss, self.row_hit, self.loss_sum, self.correct, self.X, self.Y, self.idx,
-                self.counters[1:], self.nbatches, self.B, self.Xb[1 - q], self.Yb[1 - q], self.rowsb[1 - q],
-                self.bwd_dbg)
+        if self.v2:
+            conv_bwd = lambda: self._conv_bwd2(B, q)
         else:
+            conv_args = (self.X, rows, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
+                         self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE,
+                         self.row_loss, self.row_hit, self.loss_sum, self.correct)
             conv_bwd = lambda: K.lenet_conv_bwd(*conv_args)
         if fused:
             fc_route = self.comm.routes.get(self.bucket_grads[0].numel(), "peer2")
-            K.lenet_conv_bwd(*conv_args, 0, self._peer_device_args(), self.bucket_grads[0], int(fc_route == "peer2"))
+            if self.v2:
+                self._conv_bwd2(B, q, fused_fc_route=fc_route)
+            else:
+                K.lenet_conv_bwd(*conv_args, 0, self._peer_device_args(), self.bucket_grads[0],
+                                 int(fc_route == "peer2"))
             conv_route = self.comm.routes.get(self.bucket_grads[1].numel(), "rccl")
             if conv_route in ("adam1", "adam2") and self.optimizer == "adam":
                 self._opt(0, self.params.numel(), True, fuse_ar=conv_route)
@@ -287,7 +335,8 @@ class LeNetTrainStep:
                 self.comm.all_reduce_(self.bucket_grads[0])
         conv_bwd()
         if not self.comm_on:
-            self._opt(0, self.params.numel(), True)
+            if not self.opt_in_bwd:
+                self._opt(0, self.params.numel(), True, B=B)
             return
         if self.mode == "serial":
             self.comm.all_reduce_(self.grads)
@@ -403,6 +452,12 @@ class LeNetTrainStep:
             else:
                 self.step(Bb)
         self.samples += self.nfull * self.B + self.tail
+
+    def reset_meters(self):
+        """Zero the device meters without a host round trip (enqueued on the current stream)."""
+        self.loss_sum.zero_()
+        self.correct.zero_()
+        self.samples = 0
 
     def read_meters(self, reset: bool = True):
         loss = float(self.loss_sum.item())

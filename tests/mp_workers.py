@@ -349,7 +349,8 @@ def case_engine_comm(steps="3", mode="eager"):
         for _ in range(int(steps)):
             eng.step()
     torch.cuda.synchronize()
-    emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()]})
+    bits = [int(p.detach().contiguous().view(torch.int32).to(torch.int64).sum().item()) for p in net.parameters()]
+    emit({"rank": R, "params": [p.detach().double().sum().item() for p in net.parameters()], "bits": bits})
     dist.destroy_process_group()
 
 

@@ -276,3 +276,50 @@ def test_engine_v2_tracks_v1():
         res.append((torch.cat([p.detach().reshape(-1) for p in net.parameters()]), eng.read_meters()))
     _mostly_close(res[1][0], res[0][0], 2e-6, 6 * 2e-3, "v2 vs v1 params after 6 steps")
     assert abs(res[1][1][0] - res[0][1][0]) <= 1e-3 * abs(res[0][1][0]) + 1e-3
+
+
+@pytest.mark.parametrize("mode", ["fold", "opt"])
+def test_engine_v2_bit_reproducible(mode, monkeypatch):
+    """Verdict r2 item 6: with the in-launch reduction (the W > 1 path: "fold"; "opt" = plus the
+    optimizer) the conv weight gradients are reduced in a fixed order -- conv2: 16 slabs summed in group
+    order by the last-arriving block; conv1: int64 fixed-point sums, order-free -- so two identical runs
+    give bit-identical parameters, gradients and moments.  (The W = 1 default "defer" keeps conv1's
+    float atomics into 16 replicas: fastest, reproducible to rounding only.)"""
+    monkeypatch.setenv("PDE_LENET_BWD_MODE", mode)
+    B, n = 128, 8 * 128
+    x, y = _batch(n, seed=31)
+    res = []
+    for _ in range(2):
+        net = build_net(seed=12, device=DEV)
+        eng = LeNetTrainStep(net, batch_size=B)
+        assert eng.bwd_mode == mode
+        eng.bind_dataset(x.to(DEV), y.to(DEV))
+        eng.set_epoch_indices(torch.randperm(n, generator=torch.Generator().manual_seed(5)).to(torch.int32))
+        for _ in range(3):
+            eng.step()
+        eng.replay(steps=4)
+        eng.replay(steps=1)
+        torch.cuda.synchronize()
+        res.append((eng.params.clone(), eng.grads.clone(), eng.m.clone(), eng.v.clone()))
+    for a, b, what in zip(res[0], res[1], ("params", "grads", "exp_avg", "exp_avg_sq")):
+        assert torch.equal(a, b), f"{what} differ between identical runs: {(a != b).sum().item()} elements"
+
+
+def test_engine_bwd_modes_agree(monkeypatch):
+    """The three places the conv gradients are reduced (and the optimizer runs) give the same training:
+    identical canonical gradients, the same Adam math."""
+    B, n = 128, 6 * 128
+    x, y = _batch(n, seed=33)
+    res = []
+    for mode in ("defer", "fold", "opt"):
+        monkeypatch.setenv("PDE_LENET_BWD_MODE", mode)
+        net = build_net(seed=13, device=DEV)
+        eng = LeNetTrainStep(net, batch_size=B)
+        eng.bind_dataset(x.to(DEV), y.to(DEV))
+        eng.set_epoch_indices(torch.arange(n, dtype=torch.int32))
+        for _ in range(6):
+            eng.step()
+        torch.cuda.synchronize()
+        res.append(torch.cat([p.detach().reshape(-1) for p in net.parameters()]))   # layouts differ by mode
+    _mostly_close(res[1], res[0], 1e-7, 2e-5, "fold vs defer")
+    _mostly_close(res[2], res[0], 1e-7, 2e-5, "opt vs defer")

@@ -160,6 +160,17 @@ def test_ddp_nccl_world1():
     assert rc == 0, logs
 
 
+def test_engine_comm_world1_bit_reproducible():
+    """Verdict r2 item 6: two identical W=1 runs of the communication path (RCCL initialised, the
+    conv gradients reduced in-launch without atomics) end with bit-identical parameters."""
+    runs = []
+    for _ in range(2):
+        rc, res, logs = _mp("engine_comm", "4", "graph")
+        assert rc == 0, logs
+        runs.append(res[0]["bits"])
+    assert runs[0] == runs[1]
+
+
 @pytest.mark.parametrize("mode", ["eager", "graph"])
 def test_engine_comm_world1_matches_no_comm(mode):
     rc, res, logs = _mp("engine_comm", "3", mode)
