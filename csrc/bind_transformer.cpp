@@ -157,10 +157,22 @@ void colsum_bf16(const at::Tensor& x, const at::Tensor& part, const at::Tensor& 
             "colsum_bf16");
 }
 
-void sum_f32(const at::Tensor& x, const at::Tensor& out) {
+void sum_f32(const at::Tensor& x, const at::Tensor& out, double scale) {
   check_cuda(x, "x", F32);
   check_cuda(out, "out", F32, 1);
-  hip_check(pde_sum_f32(ptr<float>(x), (int)x.numel(), ptr<float>(out), cur_stream()), "sum_f32");
+  hip_check(pde_sum_f32(ptr<float>(x), (int)x.numel(), ptr<float>(out), (float)scale, cur_stream()), "sum_f32");
+}
+
+void token_batch(const at::Tensor& pool, const at::Tensor& rows, const at::Tensor& x, const at::Tensor& y) {
+  check_cuda(pool, "pool", I64);
+  check_cuda(rows, "rows", I64);
+  TORCH_CHECK(pool.dim() == 2 && pool.size(1) >= 2, "token_batch: pool must be [P, T+1]");
+  const int64_t B = rows.numel(), T = pool.size(1) - 1;
+  check_cuda(x, "x", I64, B * T);
+  check_cuda(y, "y", I64, B * T);
+  hip_check(pde_token_batch(ptr<int64_t>(pool), ptr<int64_t>(rows), (int)B, (int)T, ptr<int64_t>(x), ptr<int64_t>(y),
+                            cur_stream()),
+            "token_batch");
 }
 
 // q/k/v: views into a [B, T, ld] bf16 buffer (column offset = section start); o: [B, T, H*64]
@@ -211,7 +223,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
 // A(m,k) = A[m*lda+k] (ta=0) or A[k*lda+m] (ta=1), B(k,n) = B[n*ldb+k] (tb=0) or B[k*ldb+n] (tb=1).
 void gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t ta, int64_t tb, int64_t epi,
           int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t splits, int64_t cfg,
-          const OptT& C2, const OptT& bias, const OptT& aux, const OptT& colsum) {
+          const OptT& C2, const OptT& bias, const OptT& aux, const OptT& colsum, const OptT& scale) {
   check_cuda(A, "A", BF16, (ta ? K : M - 1) * lda + (ta ? 0 : K));
   check_cuda(B, "B", BF16, (tb ? K : N - 1) * ldb + (tb ? 0 : K));
   TORCH_CHECK(ta ? lda >= M : lda >= K, "gemm: lda too small");
@@ -226,20 +238,23 @@ void gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t
   float* cs = optr<float>(colsum, "colsum", F32, (int64_t)S * M);
   TORCH_CHECK(epi != 1 || c2 != nullptr, "gemm: the GELU epilogue needs C2 (activation output)");
   TORCH_CHECK(epi != 2 || xp != nullptr, "gemm: the GELU-backward epilogue needs aux (pre-activation)");
+  const float* sp = optr<float>(scale, "scale", F32, 1);
+  TORCH_CHECK(sp == nullptr || epi == 0, "gemm: a device scale needs the plain bf16 epilogue");
   hip_check(pde_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), c2, bp, xp, cs, (int)ta, (int)tb, (int)epi, (int)M,
-                     (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)splits, (int)cfg, cur_stream()),
+                     (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, (int)splits, (int)cfg, sp, cur_stream()),
             "gemm");
 }
 
 // dw = sum of the S fp32 slabs of part; db = sum of the S bias-gradient partials cs (part / dw may
 // be None: db only)
 void gemm_reduce(const OptT& part, int64_t S, int64_t M, int64_t N, const OptT& dw, const OptT& cs,
-                 const OptT& db) {
+                 const OptT& db, const OptT& scale) {
   const float* p = optr<float>(part, "part", F32, S * M * N);
   void* w = optr<void>(dw, "dw", BF16, M * N);
   const float* c = optr<float>(cs, "cs", F32, S * M);
   void* d = optr<void>(db, "db", BF16, M);
-  hip_check(pde_gemm_reduce(p, (int)S, (int)M, (int)N, w, c, d, cur_stream()), "gemm_reduce");
+  hip_check(pde_gemm_reduce(p, (int)S, (int)M, (int)N, w, c, d, optr<float>(scale, "scale", F32, 1), cur_stream()),
+            "gemm_reduce");
 }
 
 std::vector<int64_t> gemm_tile(int64_t cfg) {
@@ -263,9 +278,9 @@ void register_transformer(pybind11::module& m) {
   m.def("gemm_bf16", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("ta"), py::arg("tb"), py::arg("epi"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("splits") = 1,
         py::arg("cfg") = 0, py::arg("C2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("colsum") = py::none());
+        py::arg("colsum") = py::none(), py::arg("scale") = py::none());
   m.def("gemm_reduce", &gemm_reduce, py::arg("part"), py::arg("S"), py::arg("M"), py::arg("N"), py::arg("dw"),
-        py::arg("cs") = py::none(), py::arg("db") = py::none());
+        py::arg("cs") = py::none(), py::arg("db") = py::none(), py::arg("scale") = py::none());
   m.def("gemm_tile", &gemm_tile);
   m.def("gemm_splits", &gemm_splits);
   m.def("gemm_num_cfgs", &gemm_num_cfgs);
@@ -281,7 +296,8 @@ void register_transformer(pybind11::module& m) {
         py::arg("step"), py::arg("decay_blk") = py::none(), py::arg("clip_sumsq") = py::none(),
         py::arg("max_norm") = 1.0, py::arg("step_dev") = py::none());
   m.def("f32_to_bf16", &f32_to_bf16);
-  m.def("sum_f32", &sum_f32);
+  m.def("sum_f32", &sum_f32, py::arg("x"), py::arg("out"), py::arg("scale") = 1.0);
+  m.def("token_batch", &token_batch);
   m.def("colsum_bf16_splits", &colsum_bf16_splits);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("attn_fwd", &attn_fwd);

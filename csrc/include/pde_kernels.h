@@ -57,7 +57,7 @@ hipError_t pde_lenet_conv_fwd2(const float* Xb, int B, const float* w1, const fl
 hipError_t pde_lenet_gather(const float* X, const long long* labels, const int* idx, int n_idx, const long long* ctr,
                             int nbatches, int B, float* Xdst, long long* Ydst, int* rows_dst, hipStream_t st);
 hipError_t pde_lenet_pack_w2_v2(const float* w2, float* dst, hipStream_t st);
-// Deterministic gradient reduction / in-kernel optimizer of the v2 conv backward (lenet_v2.hip).
+// Gradient reduction of the v2 conv backward (lenet_v2.hip): deferred to the optimizer, or in-launch.
 struct PdeLenetBwdOpt {
   float* slab;              // [16][25088] conv2 wgrad slabs
   long long* c1rep;         // [16][576] int64 conv1 wgrad replicas (zeroed once; kept zero by the kernel)
@@ -65,14 +65,6 @@ struct PdeLenetBwdOpt {
   unsigned* tick;           // [32] arrival counters (zeroed once)
   float* g;                 // flat gradient buffer (canonical conv gradients written here)
   long long c1w, c1b, c2w, c2b;
-  float* p;                 // nullptr: no in-kernel optimizer
-  float* m;
-  float* v;
-  float* Wp;
-  const long long* step;
-  long long fc_n4;
-  float lr, b1, b2, eps, wd, grad_scale;
-  int decoupled;
   const void* peer_dev;     // fused fc-bucket all-reduce (nullptr: none)
   float* ar_buf;
   long long ar_n;
@@ -130,7 +122,9 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
                             const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, const float* step_dev,
                             hipStream_t st);
 hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
-hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st);
+hipError_t pde_sum_f32(const float* x, int n, float* out, float scale, hipStream_t st);
+hipError_t pde_token_batch(const int64_t* pool, const int64_t* rows, int B, int T, int64_t* x, int64_t* y,
+                           hipStream_t st);
 int pde_colsum_bf16_splits(int C);
 hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, hipStream_t st);
 
@@ -166,9 +160,9 @@ int pde_gemm_splits(int K, int splits);
 void pde_gemm_set_dbg(int d);
 hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
                     int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
-                    hipStream_t st);
+                    const float* scale, hipStream_t st);
 hipError_t pde_gemm_reduce(const float* part, int S, int M, int N, void* dw, const float* cs, void* db,
-                           hipStream_t st);
+                           const float* scale, hipStream_t st);
 
 // ---- attention (attention.hip) ----
 void pde_attn_set_variant(int v);

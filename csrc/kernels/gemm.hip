@@ -55,6 +55,7 @@ struct GemmArgs {
   const bf16_t* bias;    // [N] or null (kBf16 / kGelu)
   const bf16_t* aux;     // kGeluBwd: pre-activation [M][ldc]
   float* colsum;         // [splits][M] bias-gradient partials (CS) or null
+  const float* scale;    // kBf16: device scalar multiplying the result (e.g. a loss gradient) or null
   uint32_t a_bytes, b_bytes;
   int M, N, K, lda, ldb, ldc;
   int mtiles, ntiles, kper;
@@ -124,6 +125,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
     }
   } else {
     const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+    const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;   // uniform scalar load
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -134,8 +136,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int ml = wm * WTM + 32 * i + lr;
-          const float v[4] = {acc[i][j][4 * g] + bv[0], acc[i][j][4 * g + 1] + bv[1], acc[i][j][4 * g + 2] + bv[2],
-                              acc[i][j][4 * g + 3] + bv[3]};
+          const float v[4] = {(acc[i][j][4 * g] + bv[0]) * sc, (acc[i][j][4 * g + 1] + bv[1]) * sc,
+                              (acc[i][j][4 * g + 2] + bv[2]) * sc, (acc[i][j][4 * g + 3] + bv[3]) * sc};
           *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
         }
       }
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm2(GemmArgs a) {
 // bias-gradient partials [S][M] into db (bf16) the same way
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int S, int64_t mn,
                                                      bf16_t* __restrict__ dw, int nb_main, const float* __restrict__ cs,
-                                                     int M, bf16_t* __restrict__ db) {
+                                                     int M, bf16_t* __restrict__ db, const float* __restrict__ scale) {
   if ((int)blockIdx.x < nb_main) {
     const int64_t i = (blockIdx.x * 256ll + threadIdx.x) * 4;
     if (i >= mn) return;
@@ -606,7 +608,8 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ p
       const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * mn + i);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    const float f[4] = {s.x, s.y, s.z, s.w};
+    const float sc = scale ? *scale : 1.f;
+    const float f[4] = {s.x * sc, s.y * sc, s.z * sc, s.w * sc};
     *reinterpret_cast<uint2*>(dw + i) = pack4(f);
   } else {
     const int m = ((int)blockIdx.x - nb_main) * 256 + threadIdx.x;
@@ -706,7 +709,7 @@ void pde_gemm_set_dbg(int d) { g_gemm_dbg = d; }
 
 hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
                     int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
-                    hipStream_t st) {
+                    const float* scale, hipStream_t st) {
   // a K-contiguous operand is staged in 8-element chunks: K % 8 == 0 unless both operands are transposed
   if (M <= 0 || N <= 0 || K <= 0 || (K % 8 && !(ta && tb)) || N % 8 || lda % 8 || ldb % 8 || ldc % 8 ||
       splits < 1)
@@ -714,6 +717,7 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   if ((ta && M % 8) || cfg < 0 || cfg >= kNumCfg) return hipErrorInvalidValue;
   if (splits > 1 && epi != kSlab) return hipErrorInvalidValue;
   if (colsum && !(ta && tb)) return hipErrorInvalidValue;
+  if (scale && epi != kBf16) return hipErrorInvalidValue;
   const size_t a_bytes = (size_t)(ta ? K : M) * lda * 2, b_bytes = (size_t)(tb ? K : N) * ldb * 2;
   if (a_bytes >= kOOB || b_bytes >= kOOB) return hipErrorInvalidValue;   // 32-bit buffer offsets
   GemmArgs a{};
@@ -724,6 +728,7 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   a.bias = (const bf16_t*)bias;
   a.aux = (const bf16_t*)aux;
   a.colsum = colsum;
+  a.scale = scale;
   a.a_bytes = (uint32_t)a_bytes;
   a.b_bytes = (uint32_t)b_bytes;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
@@ -757,7 +762,7 @@ int pde_gemm_splits(int K, int splits) {
 }
 
 hipError_t pde_gemm_reduce(const float* part, int S, int M, int N, void* dw, const float* cs, void* db,
-                           hipStream_t st) {
+                           const float* scale, hipStream_t st) {
   const int64_t mn = (int64_t)M * N;
   if (mn % 4 || S < 1 || (cs == nullptr) != (db == nullptr) || (part == nullptr) != (dw == nullptr))
     return hipErrorInvalidValue;
@@ -765,7 +770,7 @@ hipError_t pde_gemm_reduce(const float* part, int S, int M, int N, void* dw, con
   if (nb_main == 0 && !cs) return hipSuccess;
   const int nb_db = cs ? (M + 255) / 256 : 0;
   hipLaunchKernelGGL(k_gemm_reduce, dim3(nb_main + nb_db), dim3(256), 0, st, part, S, mn, (bf16_t*)dw, nb_main, cs, M,
-                     (bf16_t*)db);
+                     (bf16_t*)db, scale);
   return hipGetLastError();
 }
 

@@ -32,7 +32,6 @@
 
 #include "pde_kernels.h"
 #include "pde_lenet.h"
-#include "pde_adam.h"
 #include "pde_peer_dev.h"
 
 namespace {
@@ -290,7 +289,7 @@ constexpr int kC1Rep = 576;                        // int64 per conv1 replica: w
 constexpr int kC1NRep = 16;
 constexpr float kC1Scale = 1099511627776.f;        // 2^40 fixed point for the order-free int64 sums
 constexpr double kC1InvScale = 1.0 / 1099511627776.0;
-enum { kTickTail = 16, kTickD = 17, kTickDLoaded = 18, kTicks = 32 };   // [0, 16): per-k-slice W tickets
+enum { kTickD = 16, kTicks = 32 };        // [0, 16): per-k-slice W tickets, [16]: D blocks
 
 struct Bwd2Opt {
   float* slab;                 // [16][kSlab] conv2 wgrad partials (write-through stores)
@@ -299,15 +298,6 @@ struct Bwd2Opt {
   unsigned* tick;              // [kTicks] arrival counters (zero at rest)
   float* g;                    // flat gradient buffer: the folded (canonical) conv gradients land here
   long long c1w, c1b, c2w, c2b;   // flat offsets of conv1.weight / conv1.bias / conv2.weight / conv2.bias
-  // optimizer (p == nullptr: gradients only; the caller reduces them across ranks and steps itself)
-  float* p;
-  float* m;
-  float* v;
-  float* Wp;                   // packed conv2 weight of k_conv_fwd2, rewritten with the update
-  const long long* step;       // optimizer step t (advanced by fc1 earlier in this step)
-  long long fc_n4;             // W blocks also update the flat float4 range [0, fc_n4) (the fc parameters)
-  float lr, b1, b2, eps, wd, grad_scale;
-  int decoupled;
   // fused fc-bucket all-reduce (W > 1 "fused" schedule): W blocks [0, ar_nvb) run the xGMI peer
   // protocol's virtual blocks over ar_buf once their own work is done
   pde::PeerDev pd;
@@ -405,17 +395,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
                         : pc < 250 ? reinterpret_cast<const float4*>(Av + (size_t)b * 50 + (pc - 200))
                                    : P1v + (size_t)b * 720 + ch * 36 + (q % 36);
       v4[j] = *src;
-    }
-    // in-kernel optimizer: this block's float4 of the fc parameters (complete since fc_bwd), loaded now
-    // so the latency hides under the MFMAs
-    const long long fci = (long long)idx * 512 + t;
-    const bool fcjob = FOLD && op.p != nullptr && fci < op.fc_n4;
-    float4 fp = make_float4(0.f, 0.f, 0.f, 0.f), fg = fp, fm = fp, fv = fp;
-    if (fcjob) {
-      fp = reinterpret_cast<const float4*>(op.p)[fci];
-      fg = reinterpret_cast<const float4*>(op.g)[fci];
-      fm = reinterpret_cast<const float4*>(op.m)[fci];
-      fv = reinterpret_cast<const float4*>(op.v)[fci];
     }
     // side jobs: meters (block 0) and the next-batch prefetch chain (its waits come after the MFMAs)
     const bool meter = (idx == 0) && row_loss && loss_sum;
@@ -524,40 +503,25 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     }
     PMARK(3);
     if constexpr (FOLD) {
-    const long long tstep = op.p ? *op.step : 1;
-    const AdamStep as = adam_step_consts(op.lr, op.b1, op.b2, tstep);
     if (arrive_last(op.tick + kp, kNIG, lflag)) {
       PMARK(4);
-      // ---- last group of k slice kp: fold the 16 slabs (fixed order) -> canonical gradient (+ Adam) ----
+      // ---- last group of k slice kp: fold the 16 slabs (fixed order) -> canonical gradient ----
       if (t == 0) __hip_atomic_store(op.tick + kp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (op.p && t == 0) {
-        // every D block has its copy of W2 (the dgrad operand) in registers before W2 is overwritten
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(op.tick + kTickDLoaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nD &&
-               (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < 20000000)   // 200 ms guard (ablation runs)
-          __builtin_amdgcn_s_sleep(2);
-      }
       __syncthreads();
-      // all loads of the fold (4 gradient items x 16 slabs per thread, + their p / m / v) issued before
-      // any use: one dependent round trip, not one per item
+      // all loads of the fold (4 gradient items x 16 slabs per thread) issued before any use: one
+      // dependent round trip, not one per item
       constexpr int kIt = (50 * 32 + 511) / 512;
-      float q[kIt][kNIG], pa[kIt], ma[kIt], va[kIt];
+      float q[kIt][kNIG];
       long long e[kIt];
-      int kk2[kIt], co2[kIt];
+      int co2[kIt];
 #pragma unroll
       for (int u = 0; u < kIt; ++u) {
         const int i = t + 512 * u, co = min(i >> 5, 49), k = min(kp * 32 + (i & 31), 500);
         co2[u] = (i < 50 * 32 && kp * 32 + (i & 31) <= 500) ? co : -1;
-        kk2[u] = k;
         const int so = k < 500 ? co * 500 + k : kSlabBias + co;
 #pragma unroll
         for (int r = 0; r < kNIG; ++r) q[u][r] = ld_wt(op.slab + (size_t)r * kSlab + so);
         e[u] = k < 500 ? op.c2w + co * 500 + k : op.c2b + co;
-        if (op.p) {
-          pa[u] = op.p[e[u]];
-          ma[u] = op.m[e[u]];
-          va[u] = op.v[e[u]];
-        }
       }
 #pragma unroll
       for (int u = 0; u < kIt; ++u) {
@@ -566,18 +530,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
 #pragma unroll
         for (int r = 1; r < kNIG; ++r) gsum += q[u][r];
         op.g[e[u]] = gsum;
-        if (op.p) {
-          adam_elem(pa[u], ma[u], va[u], gsum * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
-                    as.step_size, as.bc2s, op.eps);
-          op.p[e[u]] = pa[u];
-          op.m[e[u]] = ma[u];
-          op.v[e[u]] = va[u];
-          if (kk2[u] < 500) op.Wp[pde_lenet_wp_index(co2[u] * 500 + kk2[u])] = pa[u];
-        }
-      }
-      if (op.p && arrive_last(op.tick + kTickTail, 16, lflag) && t == 0) {
-        __hip_atomic_store(op.tick + kTickTail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(op.tick + kTickDLoaded, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     PMARK(5);
@@ -585,18 +537,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     if (op.ar_nvb > 0 && idx < op.ar_nvb)
       pde::peer_ar_f32_vblock(op.pd, op.ar_buf, op.ar_buf, op.ar_n, 1.f, idx, op.ar_nvb, op.ar_two != 0,
                               reinterpret_cast<uint32_t*>(smem + kL_PEER));
-    // ---- in-kernel optimizer: Adam on this block's float4 of the fc parameters ----
-    if (fcjob) {
-      float* pa = &fp.x; float* ga4 = &fg.x; float* ma = &fm.x; float* va = &fv.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        adam_elem(pa[j], ma[j], va[j], ga4[j] * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
-                  as.step_size, as.bc2s, op.eps);
-      reinterpret_cast<float4*>(op.p)[fci] = fp;
-      typedef float nt_f4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&fm), reinterpret_cast<nt_f4*>(op.m) + fci);
-      __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&fv), reinterpret_cast<nt_f4*>(op.v) + fci);
-    }
     }   // FOLD
     PMARK(6);
     return;
@@ -648,14 +588,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     reinterpret_cast<uint32_t*>(c1s)[(t / 36) * 37 + (t % 36)] = cv;    // 148-byte code rows
   }
   lds_barrier();
-  if (FOLD && op.p) {
-    // W2 (the dgrad operand) is in this block's registers: the W blocks' in-kernel Adam may now rewrite it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(op.tick + kTickDLoaded, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   PMARK(1);
-  // ---- two passes of 5 input channels: dgrad -> T, col2im gather -> dP1 (ReLU mask of P1) ----
+  // ---- two passes of 5 input channels: dgrad T[125 k'][64 px] = W2^T dY2 on v_mfma_f32_32x32x2_f32,
+  // then col2im dP1[ci][ih][iw] = sum_{kh,kw} T[ci,kh,kw][ih-kh][iw-kw] ----
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     {
@@ -669,6 +604,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     }
     lds_barrier();
     if (p == 0) PMARK(2);
+    // col2im as a gather (fixed summation order) + ReLU mask of P1.  (Measured and rejected: each lane
+    // adding its 16 T values into dP1 with LDS atomics straight from the accumulator, no T image and
+    // no gather pass -- ds_add_f32 made the step 91 us instead of 55.5, profiles/r3_lenet/.)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int o = t + 512 * r;
@@ -725,8 +663,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
   lds_barrier();
   PMARK(5);
   if (t < 260) {
-    // conv1 wgrad|bgrad partial of this image: int64 fixed-point adds into replica (b % 16) -- integer
-    // addition is associative, so the sums are bit-identical whatever order the blocks arrive in
+    // conv1 wgrad|bgrad partial of this image into replica (b % 16): FOLD -- int64 fixed-point adds
+    // (integer addition is associative: bit-identical sums whatever order the blocks arrive in)
     const int c = t / 26, tap = t - c * 26;
     const float v = red[c * 36 + tap] + red[(16 + c) * 36 + tap] + red[(32 + c) * 36 + tap] + red[(48 + c) * 36 + tap];
     const int ch = 10 * hh + c;
@@ -738,14 +676,11 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
                 (unsigned long long)__float2ll_rn(v * kC1Scale));
   }
   if (FOLD && arrive_last(op.tick + kTickD, (unsigned)nD, lflag)) {
-    // ---- last D block: fold the 16 replicas (exact) -> canonical conv1 gradient (+ Adam), re-zero ----
+    // ---- last D block: fold the 16 replicas (exact) -> canonical conv1 gradient, re-zero ----
     if (t == 0) __hip_atomic_store(op.tick + kTickD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long tstep = op.p ? *op.step : 1;
-    const AdamStep as = adam_step_consts(op.lr, op.b1, op.b2, tstep);
     // items: weight t (t < 500), bias t - 500 (t < 512), bias 12 + t (second slot, t < 8); all loads
     // issued before any use: one dependent round trip
     long long q[2][kC1NRep];
-    float pv[2], mv[2], vv[2];
     long long e[2];
     int slot[2];
 #pragma unroll
@@ -755,9 +690,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
       e[u] = (u == 0 && t < 500) ? op.c1w + t : op.c1b + min(bi, 19);
 #pragma unroll
       for (int r = 0; r < kC1NRep; ++r) q[u][r] = ld_wt64(op.c1rep + (size_t)r * kC1Rep + slot[u]);
-      if (op.p) {
-        pv[u] = op.p[e[u]]; mv[u] = op.m[e[u]]; vv[u] = op.v[e[u]];
-      }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -767,11 +699,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
       for (int r = 0; r < kC1NRep; ++r) acc += q[u][r];
       const float gsum = (float)((double)acc * kC1InvScale);
       op.g[e[u]] = gsum;
-      if (op.p) {
-        adam_elem(pv[u], mv[u], vv[u], gsum * op.grad_scale, op.lr, op.wd, op.decoupled, as.omb1, as.omb2, op.b2,
-                  as.step_size, as.bc2s, op.eps);
-        op.p[e[u]] = pv[u]; op.m[e[u]] = mv[u]; op.v[e[u]] = vv[u];
-      }
     }
     __syncthreads();
     for (int i = t; i < kC1NRep * kC1Rep; i += 512) op.c1rep[i] = 0;
@@ -815,7 +742,6 @@ hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* 
                                const long long* gctr, int gnbatches, int gstride, float* gXdst, long long* gYdst,
                                int* grows, int dbg, hipStream_t st) {
   if (B < 1 || B > 128) return hipErrorInvalidValue;                  // 16 image groups of <= 8 images
-  if (o->fc_n4 > (long long)kNIG * 16 * 512) return hipErrorInvalidValue;   // one float4 per W thread
   const int nblk = kNIG * 16 + 2 * B;
   Bwd2Gather ga{gX, glabels, gidx, gn_idx, gctr, gnbatches, gstride, gXdst, gYdst, grows};
   Bwd2Opt op{};
@@ -825,9 +751,6 @@ hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* 
   op.tick = o->tick;
   op.g = o->g;
   op.c1w = o->c1w; op.c1b = o->c1b; op.c2w = o->c2w; op.c2b = o->c2b;
-  op.p = o->p; op.m = o->m; op.v = o->v; op.Wp = o->Wp; op.step = o->step; op.fc_n4 = o->p ? o->fc_n4 : 0;
-  op.lr = o->lr; op.b1 = o->b1; op.b2 = o->b2; op.eps = o->eps; op.wd = o->wd; op.grad_scale = o->grad_scale;
-  op.decoupled = o->decoupled;
   op.defer = o->defer;
   if (o->peer_dev != nullptr && o->ar_buf != nullptr && o->ar_n > 0) {
     std::memcpy(&op.pd, o->peer_dev, sizeof(op.pd));

@@ -676,7 +676,8 @@ __global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__
 }
 
 // out[0] = sum(x[0..n)) (one 1024-thread block; n up to a few 1e5 -- loss rows)
-__global__ __launch_bounds__(1024) void k_sum_f32(const float* __restrict__ x, int n, float* __restrict__ out) {
+__global__ __launch_bounds__(1024) void k_sum_f32(const float* __restrict__ x, int n, float* __restrict__ out,
+                                                  float scale) {
   __shared__ float sh[16];
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
@@ -686,7 +687,19 @@ __global__ __launch_bounds__(1024) void k_sum_f32(const float* __restrict__ x, i
   if (threadIdx.x < 64) {
     float t = threadIdx.x < 16 ? sh[threadIdx.x] : 0.f;
     t = wave_sum(t);
-    if (threadIdx.x == 0) out[0] = t;
+    if (threadIdx.x == 0) out[0] = t * scale;
+  }
+}
+
+// Next-token batch of a [P][T+1] token pool: x[b] = pool[rows[b]][0:T], y[b] = pool[rows[b]][1:T+1]
+// (contiguous model inputs / targets straight from the sampler's rows, one pass, no index_select)
+__global__ __launch_bounds__(256) void k_token_batch(const int64_t* __restrict__ pool, const int64_t* __restrict__ rows,
+                                                     int T, int64_t* __restrict__ x, int64_t* __restrict__ y) {
+  const int b = blockIdx.y;
+  const int64_t* src = pool + rows[b] * (int64_t)(T + 1);
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
+    x[(int64_t)b * T + t] = src[t];
+    y[(int64_t)b * T + t] = src[t + 1];
   }
 }
 
@@ -825,8 +838,14 @@ hipError_t pde_colsum_bf16(const void* x, int N, int C, float* part, void* out, 
   return hipGetLastError();
 }
 
-hipError_t pde_sum_f32(const float* x, int n, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_sum_f32, dim3(1), dim3(1024), 0, st, x, n, out);
+hipError_t pde_sum_f32(const float* x, int n, float* out, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_f32, dim3(1), dim3(1024), 0, st, x, n, out, scale);
+  return hipGetLastError();
+}
+
+hipError_t pde_token_batch(const int64_t* pool, const int64_t* rows, int B, int T, int64_t* x, int64_t* y,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_token_batch, dim3((T + 255) / 256, B), dim3(256), 0, st, pool, rows, T, x, y);
   return hipGetLastError();
 }
 

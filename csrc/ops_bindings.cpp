@@ -331,9 +331,7 @@ void lenet_gather(const at::Tensor& X, const at::Tensor& labels, const OptT& idx
 void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& dP2m,
                      const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& slab,
                      const at::Tensor& c1rep, const at::Tensor& c1part, const at::Tensor& tick, const at::Tensor& g, int64_t c1w, int64_t c1b,
-                     int64_t c2w, int64_t c2b, const OptT& p, const OptT& m, const OptT& v, const OptT& Wp,
-                     const OptT& step, int64_t fc_n, double lr, double b1, double b2, double eps, double wd,
-                     bool decoupled, double grad_scale, const OptT& row_loss, const OptT& row_hit,
+                     int64_t c2w, int64_t c2b, const OptT& row_loss, const OptT& row_hit,
                      const OptT& loss_sum, const OptT& correct, const OptT& gX, const OptT& glabels, const OptT& gidx,
                      const OptT& gctr, int64_t gnbatches, int64_t gstride, const OptT& gXdst, const OptT& gYdst,
                      const OptT& grows, const OptT& peer_dev, const OptT& ar_buf, int64_t ar_two, int64_t defer,
@@ -362,26 +360,7 @@ void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tenso
   o.tick = reinterpret_cast<unsigned*>(tick.data_ptr<int32_t>());
   o.g = ptr<float>(g);
   o.c1w = c1w; o.c1b = c1b; o.c2w = c2w; o.c2b = c2b;
-  if (p.has_value()) {
-    TORCH_CHECK(m.has_value() && v.has_value() && Wp.has_value() && step.has_value(),
-                "conv_bwd2 in-kernel Adam needs p, m, v, Wp and the step counter");
-    for (const OptT* t : {&p, &m, &v}) {
-      check_cuda(**t, "p/m/v", F32, n);
-      TORCH_CHECK(reinterpret_cast<uintptr_t>((*t)->data_ptr()) % 16 == 0, "p/m/v must be 16-B aligned");
-    }
-    TORCH_CHECK(fc_n >= 0 && fc_n % 4 == 0 && fc_n <= n && fc_n <= 16 * 16 * 512 * 4, "conv_bwd2: bad fc range");
-    o.p = ptr<float>(*p);
-    o.m = ptr<float>(*m);
-    o.v = ptr<float>(*v);
-    o.Wp = optr<float>(Wp, "Wp", F32, kPdeWpFloats);
-    o.step = optr<long long>(step, "step", I64, 1);
-    o.fc_n4 = fc_n / 4;
-  }
-  o.lr = (float)lr; o.b1 = (float)b1; o.b2 = (float)b2; o.eps = (float)eps; o.wd = (float)wd;
-  o.grad_scale = (float)grad_scale;
-  o.decoupled = decoupled ? 1 : 0;
   o.defer = defer ? 1 : 0;
-  TORCH_CHECK(!(defer && p.has_value()), "conv_bwd2: the in-launch optimizer needs the in-launch fold (defer=0)");
   if (peer_dev.has_value()) {
     TORCH_CHECK(peer_dev->numel() == (int64_t)sizeof(pde::PeerDev), "bad peer device args");
     check_cuda(*ar_buf, "ar_buf", F32);
@@ -610,11 +589,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_conv_bwd2", &lenet_conv_bwd2, py::arg("Xb"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("slab"), py::arg("c1rep"), py::arg("c1part"), py::arg("tick"),
         py::arg("g"),
-        py::arg("c1w"), py::arg("c1b"), py::arg("c2w"), py::arg("c2b"), py::arg("p") = py::none(),
-        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("Wp") = py::none(), py::arg("step") = py::none(),
-        py::arg("fc_n") = 0, py::arg("lr") = 1e-3, py::arg("b1") = 0.9, py::arg("b2") = 0.999, py::arg("eps") = 1e-8,
-        py::arg("wd") = 0.0, py::arg("decoupled") = false, py::arg("grad_scale") = 1.0,
-        py::arg("row_loss") = py::none(), py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(),
+        py::arg("c1w"), py::arg("c1b"), py::arg("c2w"), py::arg("c2b"), py::arg("row_loss") = py::none(), py::arg("row_hit") = py::none(), py::arg("loss_sum") = py::none(),
         py::arg("correct") = py::none(), py::arg("gX") = py::none(), py::arg("glabels") = py::none(),
         py::arg("gidx") = py::none(), py::arg("gctr") = py::none(), py::arg("gnbatches") = 1, py::arg("gstride") = 0,
         py::arg("gXdst") = py::none(), py::arg("gYdst") = py::none(), py::arg("grows") = py::none(),

@@ -77,20 +77,18 @@ class LeNetTrainStep:
         # launch also runs the optimizer (no separate Adam kernel: the folding blocks update the conv
         # parameters, every W block one float4 of the fc parameters).  v1 (lenet.hip) for B > 128.
         self.v2 = ((os.environ.get("PDE_LENET_V2", "1") != "0") if v2 is None else bool(v2)) and self.B <= 128
-        # where the conv weight gradients are reduced (v2), all deterministic:
-        #   "defer" (W = 1 default): the conv backward stores its partials (16 conv2 slabs, 16 int64 conv1
-        #           replicas) and the flat optimizer's fold blocks reduce them -- no seam on the chain;
-        #   "fold"  (W > 1): the last-arriving blocks of the conv backward fold them into the canonical
-        #           slots inside the launch, so the all-reduced conv bucket is just the conv parameters;
-        #   "opt"   (W = 1, Adam): "fold" plus the whole optimizer step inside the same launch.
-        # PDE_LENET_BWD_MODE overrides the W = 1 choice (A/B runs).
+        # where the conv weight gradients are reduced (v2):
+        #   "defer" (W = 1): the conv backward leaves 16 conv2 slabs (plain stores) and 16 conv1 replicas
+        #           (float atomics) in the flat buffer; the optimizer's fold blocks sum them in fixed order
+        #           -- no reduction seam on the chain (measured: an in-launch fold + Adam is 2-3 us slower);
+        #   "fold"  (comm path): the last-arriving blocks of the conv backward fold them inside the launch,
+        #           conv2 slabs in group order and conv1 as int64 fixed-point sums (order-free), so the
+        #           all-reduced conv bucket is exactly the conv parameters and bit-reproducible.
+        # PDE_LENET_BWD_MODE=fold forces the comm-path reduction at W = 1 (A/B runs, tests).
         mode = os.environ.get("PDE_LENET_BWD_MODE", "defer")
         if self.comm_on:
             mode = "fold"
-        elif mode == "opt" and optimizer != "adam":
-            mode = "defer"
         self.bwd_mode = mode if self.v2 else "v1"
-        self.opt_in_bwd = self.bwd_mode == "opt"
         dev = self.device
         named = [(n, tuple(p.shape)) for n, p in net.named_parameters()]
         if self.bwd_mode == "defer":
@@ -206,14 +204,13 @@ class LeNetTrainStep:
                                 self.Yb[self.q], self.rowsb[self.q])
 
     # ------------------------------------------------------------------ the step
-    def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None, B: Optional[int] = None):
+    def _opt(self, lo: int, hi: int, conv: bool, fuse_ar: Optional[str] = None):
         """Fused optimizer update of the flat range [lo, hi) (one bucket or everything).  The conv
         range carries the conv2 weight repack (Wp / Wt2) and, in the v1 layout, the conv1
         gradient-replica fold (v2 writes canonical gradients, nothing to fold).
         ``fuse_ar`` ('adam1' / 'adam2'): side blocks of the Adam kernel all-reduce the conv bucket
         (one- / two-shot peer protocol) while the other blocks update the fc parameters."""
         K, sl = self.K, slice(lo, hi)
-        B = B or self.B
         pack_off = self.pack_off - lo if conv else -1
         pack, mode = (self.Wp, 2) if self.v2 else (self.Wt2, 1)
         if not conv:
@@ -238,18 +235,14 @@ class LeNetTrainStep:
                        scale, self.counters, self.arrive, -1, pack_off, pack, pack_mode=mode, **folds)
 
     def _conv_bwd2(self, B: int, q: int, fused_fc_route: Optional[str] = None):
-        """The v2 conv backward: deterministic in-launch gradient reduction, the next batch's prefetch,
-        the meters, and (W = 1, Adam) the whole optimizer step; ``fused_fc_route`` ('peer1' / 'peer2'):
-        its W blocks also all-reduce the fc bucket across ranks once their own work is done."""
+        """The v2 conv backward (+ the next batch's prefetch and the meters); ``fused_fc_route``
+        ('peer1' / 'peer2'): its W blocks also all-reduce the fc bucket across ranks once their own work
+        is done."""
         p = self.p
         kw = dict(row_loss=self.row_loss, row_hit=self.row_hit, loss_sum=self.loss_sum, correct=self.correct,
                   gX=self.X, glabels=self.Y, gidx=self.idx, gctr=self.counters[1:], gnbatches=self.nbatches,
                   gstride=self.B, gXdst=self.Xb[1 - q], gYdst=self.Yb[1 - q], grows=self.rowsb[1 - q],
                   dbg=self.bwd_dbg)
-        if self.opt_in_bwd:
-            kw.update(p=self.params, m=self.m, v=self.v, Wp=self.Wp, step=self.counters,
-                      fc_n=self.bucket_ranges[0][1], lr=self.lr, b1=self.betas[0], b2=self.betas[1], eps=self.eps,
-                      wd=self.wd, decoupled=False, grad_scale=1.0 / self.world)
         if fused_fc_route is not None:
             kw.update(peer_dev=self._peer_device_args(), ar_buf=self.bucket_grads[0],
                       ar_two=int(fused_fc_route == "peer2"))
@@ -335,8 +328,7 @@ class LeNetTrainStep:
                 self.comm.all_reduce_(self.bucket_grads[0])
         conv_bwd()
         if not self.comm_on:
-            if not self.opt_in_bwd:
-                self._opt(0, self.params.numel(), True, B=B)
+            self._opt(0, self.params.numel(), True)
             return
         if self.mode == "serial":
             self.comm.all_reduce_(self.grads)

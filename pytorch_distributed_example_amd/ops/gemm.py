@@ -113,8 +113,10 @@ def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return y
 
 
-def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
-    """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``pre`` ([M, K]) returns dx * gelu'(pre)."""
+def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
+          scale: Optional[torch.Tensor] = None):
+    """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``pre`` ([M, K]) returns dx * gelu'(pre); ``scale`` (a
+    one-element fp32 device tensor, e.g. the loss gradient) multiplies the result in the epilogue."""
     _chk(dy2, "dy")
     _chk(w, "w")
     M, Nk = dy2.shape                  # reduction over the weight's rows
@@ -124,14 +126,16 @@ def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None
     if pre is not None:
         kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=pre)
     else:
-        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c)
+        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c, scale=scale)
     return dx
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, dw: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None,
-          want_db: bool = False, cfg: Optional[int] = None, splits: Optional[int] = None):
+          want_db: bool = False, cfg: Optional[int] = None, splits: Optional[int] = None,
+          scale: Optional[torch.Tensor] = None):
     """dw [N, K] = dy2[T, N]^T . x2[T, K] (into ``dw`` when given); with ``want_db`` (or ``db``) also
-    db [N] = column sums of dy2.  Returns (dw, db or None)."""
+    db [N] = column sums of dy2.  ``scale``: one-element fp32 device tensor multiplying dw (not db).
+    Returns (dw, db or None)."""
     _chk(dy2, "dy")
     _chk(x2, "x")
     T, N = dy2.shape
@@ -146,12 +150,12 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, dw: Optional[torch.Tensor] = None
         db = torch.empty(N, device=dy2.device, dtype=torch.bfloat16)
     cs = _scratch(dy2.device, S * N, "cs") if want_db else None
     if S == 1:
-        kernels().gemm_bf16(dy2, x2, dw, 1, 1, EPI_BF16, N, K, T, N, K, K, 1, c, colsum=cs)
+        kernels().gemm_bf16(dy2, x2, dw, 1, 1, EPI_BF16, N, K, T, N, K, K, 1, c, colsum=cs, scale=scale)
         if want_db:
             kernels().gemm_reduce(None, 1, N, K, None, cs, db)     # db only
         return dw, db
     part = _scratch(dy2.device, S * N * K, "slab")
     kernels().gemm_bf16(dy2, x2, part, 1, 1, EPI_SLAB, N, K, T, N, K, K, S, c, colsum=cs)
-    kernels().gemm_reduce(part, S, N, K, dw, cs, db)
+    kernels().gemm_reduce(part, S, N, K, dw, cs, db, scale)
     return dw, db
 

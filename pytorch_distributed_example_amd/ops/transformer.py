@@ -229,6 +229,11 @@ def _emb_scratch(device, Vp, C):
 
 
 class EmbeddingFn(torch.autograd.Function):
+    """Token + position embedding.  With a tied LM head (``lm_head_loss`` over the same ``wte`` later
+    in the forward) the token-embedding gradient is accumulated straight into the LM head's weight
+    gradient -- the tied ``wte`` gradient is written once: no zero-fill, no autograd add of the two
+    paths (the LM head's backward runs first and leaves its dw in the pairing slot)."""
+
     @staticmethod
     def forward(ctx, idx, wte, wpe):
         B, T = idx.shape
@@ -238,17 +243,29 @@ class EmbeddingFn(torch.autograd.Function):
         kernels().embed_fwd(idx, wte, wpe, out, T)
         ctx.save_for_backward(idx)
         ctx.shapes = (wte.shape, wpe.shape, T)
+        ctx.tied = {}                  # filled by the LM head's backward of this forward pass, if tied
+        ctx.wpe = wpe
+        wte._pde_tied_slot = ctx.tied
         return out
 
     @staticmethod
     def backward(ctx, dx):
         (idx,) = ctx.saved_tensors
         wte_shape, wpe_shape, T = ctx.shapes
-        dwte = torch.zeros(wte_shape, device=dx.device, dtype=dx.dtype)
-        dwpe = torch.zeros(wpe_shape, device=dx.device, dtype=dx.dtype)
+        dw_tied = ctx.tied.pop("dw", None)
+        if dw_tied is not None and tuple(dw_tied.shape) == tuple(wte_shape):
+            dwte, ret_wte = dw_tied, None          # accumulate into the LM head's gradient in place
+        else:
+            dwte = torch.zeros(wte_shape, device=dx.device, dtype=dx.dtype)
+            ret_wte = dwte
+        dwpe = _grad_out(ctx.wpe)
+        if dwpe is None:
+            dwpe = torch.empty(wpe_shape, device=dx.device, dtype=dx.dtype)
+        if T < wpe_shape[0]:
+            dwpe[T:].zero_()                       # rows past the sequence get no gradient
         acc, touched = _emb_scratch(dx.device, wte_shape[0], wte_shape[1])
         kernels().embed_bwd(_c(dx), idx, dwte, dwpe, acc, touched, T, False)
-        return None, dwte, dwpe
+        return None, ret_wte, dwpe
 
 
 def embedding(idx, wte, wpe):
@@ -263,7 +280,10 @@ class LMHeadLossFn(torch.autograd.Function):
     """mean cross-entropy of logits = h @ W^T over the first V columns of W ([Vp, C], padded vocab).
 
     Forward runs the GEMM and the fused softmax-CE kernel, which overwrites the logits buffer with
-    dlogits = (softmax - onehot) / N; backward is two GEMMs from that buffer."""
+    dlogits = (softmax - onehot) / N; backward is two GEMMs from that buffer with the incoming loss
+    gradient applied in their epilogues (a device scalar: no host read, no extra kernel, graph-safe,
+    and the saved dlogits stay unscaled, so a retained graph can run backward again).  With W tied to
+    the embedding of the same forward pass, dW is left for the embedding backward to accumulate into."""
 
     @staticmethod
     def forward(ctx, h, w, targets, V):
@@ -275,27 +295,26 @@ class LMHeadLossFn(torch.autograd.Function):
         tg = _c(targets.reshape(-1).long())
         kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
         tot = torch.empty(1, device=h.device, dtype=torch.float32)
-        kernels().sum_f32(rows, tot)
+        kernels().sum_f32(rows, tot, 1.0 / N)               # mean loss, no separate divide
         ctx.save_for_backward(h2, w, logits)
         ctx.hshape = h.shape
-        return (tot / N).reshape(())
+        ctx.tied = getattr(w, "_pde_tied_slot", None)
+        if ctx.tied is not None:
+            del w._pde_tied_slot
+        return tot.reshape(())
 
     @staticmethod
     def backward(ctx, g):
         h2, w, dlogits = ctx.saved_tensors
         if not (isinstance(g, torch.Tensor) and g.numel() == 1):
             raise RuntimeError("LM head loss expects a scalar gradient")
-        # dlogits already holds d(mean loss)/dlogits for g = 1.  Eagerly, a g != 1 rescales it (host
-        # check); inside a hipGraph capture there is no host read, so g scales the two (small) outputs
-        # instead -- exact for the usual g = 1
-        post = torch.cuda.is_current_stream_capturing()
-        if not post and float(g) != 1.0:
-            dlogits.mul_(g.to(dlogits.dtype))
-        dh = G.dgrad(dlogits, w)                             # [N, C]
-        dw, _ = G.wgrad(dlogits, h2)                         # [Vp, C]
-        if post:
-            dh.mul_(g.to(dh.dtype))
-            dw.mul_(g.to(dw.dtype))
+        gs = g.reshape(1)
+        if gs.dtype != torch.float32 or not gs.is_cuda:
+            gs = gs.to(device=dlogits.device, dtype=torch.float32)
+        dh = G.dgrad(dlogits, w, scale=gs)                   # [N, C]
+        dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
+        if ctx.tied is not None:
+            ctx.tied["dw"] = dw                              # the tied embedding adds its part in place
         return dh.reshape(ctx.hshape), dw, None, None
 
 
