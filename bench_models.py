@@ -42,19 +42,25 @@ def _cap(args) -> float:
     return 25.0 if str(args.bucket_mb) == "auto" else float(args.bucket_mb)
 
 
-def _tune(ddp, step, world, args) -> dict:
-    """W > 1 with --bucket-mb auto: time whole steps per bucket cap (max over ranks), keep the fastest.
-    Reports the chosen cap, the per-cap timings and the reduction dtype in the bench JSON."""
+def _tune(ddp, step, world, args, restore=None) -> dict:
+    """W > 1 with --bucket-mb auto: time whole steps per (reduction route, bucket cap) (max over ranks),
+    keep the fastest; the trial steps' training state is restored.  Reports the chosen cap and route,
+    the per-candidate timings and the gradient bytes each rank hands to the all-reduce per step."""
     if world <= 1:
         return {"bucket_mb": None, "grad_allreduce": "none"}
     from pytorch_distributed_example_amd.parallel import tune_bucket_cap
-    out = {"grad_reduce_dtype": str(ddp.reduce_dtype or "param dtype").replace("torch.", "")}
+    out = {}
     if str(args.bucket_mb) == "auto":
-        timings, best = tune_bucket_cap(ddp, step)
+        timings, best = tune_bucket_cap(ddp, step, restore=restore)
         out.update(bucket_mb=best, bucket_sweep_ms_per_step=timings)
     else:
         out["bucket_mb"] = float(args.bucket_mb)
+    out["grad_reduce_route"] = ddp.reduce_route
+    out["grad_reduce_dtype"] = str(ddp.reduce_dtype or "param dtype").replace("torch.", "")
+    out["grad_allreduce_bytes_per_step"] = ddp.wire_bytes_per_step()
     out["n_buckets"] = len(ddp.buckets)
+    if ddp.peer_reason:
+        out["peer_reason"] = ddp.peer_reason
     return out
 
 
@@ -137,7 +143,11 @@ def bench_gpt2(args):
         next_batch()
         losses.append(eager_step(sx, sy))
 
-    extra = _tune(ddp, step, world, args)
+    step0 = opt._step
+    extra = _tune(ddp, step, world, args, restore=list(model.parameters()) + opt.state_tensors())
+    opt._step = step0
+    if getattr(opt, "capturable", False):
+        opt.state_tensors()[-1].fill_(float(step0))
     if use_graph:
         # the whole step (forward, loss, backward, grad-norm clip, AdamW with its device-side step
         # count) is captured once into a hipGraph and replayed: ~340 launches per step leave the host

@@ -84,6 +84,10 @@ hipError_t pde_gemm_f32(const float* A, const float* B, float* C, const float* b
                         int ldb, int ldc, int transA, int transB, long long sA, long long sB, long long sC, int batch,
                         float alpha, float beta, int bias_mode, int relu, int atomic, hipStream_t st);
 hipError_t pde_xent_fwd(const float* x, const long long* y, int B, int C, float* row_loss, float* lse, hipStream_t st);
+hipError_t pde_xent_fwd_bf16(const void* x, const long long* y, int B, int C, float* row_loss, float* lse,
+                             hipStream_t st);
+hipError_t pde_xent_bwd_bf16(const void* x, const long long* y, const float* lse, const float* gscale, int per_row,
+                             float mul, int B, int C, void* dx, hipStream_t st);
 hipError_t pde_xent_bwd(const float* x, const long long* y, const float* lse, const float* gscale, int per_row,
                         float mul, int B, int C, float* dx, hipStream_t st);
 hipError_t pde_log_softmax_fwd(const float* x, int B, int C, float* out, hipStream_t st);

@@ -13,6 +13,7 @@
 //   k_pool2_*     : 2x2 stride-2 max pool with argmax codes, forward / backward
 //   k_im2col / k_col2im, k_bias_grad_nchw, k_colsum
 #include "pde_hip.h"
+#include "pde_bf16.h"
 #include "pde_kernels.h"
 
 namespace {
@@ -138,36 +139,45 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 
 // ---------------------------------------------------------------------------------------------
 // cross entropy over logits [B][C] (= F.cross_entropy = nll(log_softmax)), wave per row
-__global__ __launch_bounds__(256) void k_xent_fwd(const float* __restrict__ x, const long long* __restrict__ y, int B,
+// logits of either dtype (fp32 or bf16: the bf16 ResNet head feeds its own output, no cast kernel)
+__device__ __forceinline__ float ld_logit(const float* p, size_t i) { return p[i]; }
+__device__ __forceinline__ float ld_logit(const bf16_t* p, size_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ void st_logit(float* p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st_logit(bf16_t* p, size_t i, float v) { p[i] = f2bf(v); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_xent_fwd(const T* __restrict__ x, const long long* __restrict__ y, int B,
                                                   int C, float* __restrict__ row_loss, float* __restrict__ lse_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   if (row >= B) return;
-  const float* xr = x + (size_t)row * C;
+  const size_t r0 = (size_t)row * C;
   float m = -INFINITY;
-  for (int c = l; c < C; c += 64) m = fmaxf(m, xr[c]);
+  for (int c = l; c < C; c += 64) m = fmaxf(m, ld_logit(x, r0 + c));
   m = wave_max(m);
   float s = 0.f;
-  for (int c = l; c < C; c += 64) s += expf(xr[c] - m);
+  for (int c = l; c < C; c += 64) s += expf(ld_logit(x, r0 + c) - m);
   s = wave_sum(s);
   const float lse = m + logf(s);
   if (l == 0) {
     const int yy = (int)y[row];
-    row_loss[row] = (yy >= 0 && yy < C) ? lse - xr[yy] : 0.f;
+    row_loss[row] = (yy >= 0 && yy < C) ? lse - ld_logit(x, r0 + yy) : 0.f;
     lse_out[row] = lse;
   }
 }
 
 // dx = (softmax(x) - onehot(y)) * scale_row  (scale = grad * (1/B for mean))
-__global__ __launch_bounds__(256) void k_xent_bwd(const float* __restrict__ x, const long long* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void k_xent_bwd(const T* __restrict__ x, const long long* __restrict__ y,
                                                   const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                  int per_row, float mul, int B, int C, float* __restrict__ dx) {
+                                                  int per_row, float mul, int B, int C, T* __restrict__ dx) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   if (row >= B) return;
   const float g = (per_row ? gscale[row] : gscale[0]) * mul;
   const int yy = (int)y[row];
   const float L = lse[row];
+  const size_t r0 = (size_t)row * C;
   for (int c = l; c < C; c += 64)
-    dx[(size_t)row * C + c] = (expf(x[(size_t)row * C + c] - L) - (c == yy ? 1.f : 0.f)) * g;
+    st_logit(dx, r0 + c, (expf(ld_logit(x, r0 + c) - L) - (c == yy ? 1.f : 0.f)) * g);
 }
 
 __global__ __launch_bounds__(256) void k_logsm_fwd(const float* __restrict__ x, int B, int C, float* __restrict__ out) {
@@ -346,13 +356,27 @@ hipError_t pde_gemm_f32(const float* A, const float* B, float* C, const float* b
 
 hipError_t pde_xent_fwd(const float* x, const long long* y, int B, int C, float* row_loss, float* lse,
                         hipStream_t st) {
-  hipLaunchKernelGGL(k_xent_fwd, dim3((B + 3) / 4), dim3(256), 0, st, x, y, B, C, row_loss, lse);
+  hipLaunchKernelGGL(k_xent_fwd<float>, dim3((B + 3) / 4), dim3(256), 0, st, x, y, B, C, row_loss, lse);
   return hipGetLastError();
 }
 
 hipError_t pde_xent_bwd(const float* x, const long long* y, const float* lse, const float* gscale, int per_row,
                         float mul, int B, int C, float* dx, hipStream_t st) {
-  hipLaunchKernelGGL(k_xent_bwd, dim3((B + 3) / 4), dim3(256), 0, st, x, y, lse, gscale, per_row, mul, B, C, dx);
+  hipLaunchKernelGGL(k_xent_bwd<float>, dim3((B + 3) / 4), dim3(256), 0, st, x, y, lse, gscale, per_row, mul, B, C, dx);
+  return hipGetLastError();
+}
+
+hipError_t pde_xent_fwd_bf16(const void* x, const long long* y, int B, int C, float* row_loss, float* lse,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_xent_fwd<bf16_t>, dim3((B + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, y, B, C, row_loss,
+                     lse);
+  return hipGetLastError();
+}
+
+hipError_t pde_xent_bwd_bf16(const void* x, const long long* y, const float* lse, const float* gscale, int per_row,
+                             float mul, int B, int C, void* dx, hipStream_t st) {
+  hipLaunchKernelGGL(k_xent_bwd<bf16_t>, dim3((B + 3) / 4), dim3(256), 0, st, (const bf16_t*)x, y, lse, gscale,
+                     per_row, mul, B, C, (bf16_t*)dx);
   return hipGetLastError();
 }
 

@@ -90,6 +90,16 @@ struct FoldLane {
   float g;       // its folded gradient (before grad_scale)
 };
 
+// The flat element fold lane (fb, threadIdx.x) updates (-1: none) -- known before any load, so the
+// optimizer state of that element is fetched in the same round trip as the replicas.
+__device__ __forceinline__ long long fold_elem(const Fold& fd, int fb) {
+  const int nb0 = fold_blocks(fd.f[0]);
+  const int k = fb < nb0 ? 0 : 1;
+  const Fold1& f = fd.f[k];
+  const long long j = ((long long)(k ? fb - nb0 : fb) * 256 + threadIdx.x) / kLS;
+  return j < f.stride / 4 ? f.off + 4 * j + threadIdx.x % kLS : -1;
+}
+
 // fb = fold-block index (0-based over both ranges).  All lanes of the wave take part in the shuffles.
 __device__ __forceinline__ FoldLane fold_lane(const Fold& fd, float* __restrict__ g, int fb) {
   const int nb0 = fold_blocks(fd.f[0]);
@@ -217,9 +227,15 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   if (fb >= 0) {                                     // fold block: its own range, one pass
     if (pass == 1) break;
     if (ar.nvb > 0) wait_epoch(ar.epoch, t, ar.pd);   // the reduced replicas must be complete
+    const long long e0 = fold_elem(fd, fb);
+    float pa = 0.f, ma = 0.f, va = 0.f;
+    if (e0 >= 0) {                                   // issued before the replica loads: one round trip
+      pa = p[e0];
+      ma = m[e0];
+      va = v[e0];
+    }
     const FoldLane fl = fold_lane(fd, g, fb);
     if (fl.e >= 0) {
-      float pa = p[fl.e], ma = m[fl.e], va = v[fl.e];
       adam_elem(pa, ma, va, fl.g * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
       p[fl.e] = pa; m[fl.e] = ma; v[fl.e] = va;
       g[fl.e] = fl.g;                                  // p.grad holds the true (folded) gradient

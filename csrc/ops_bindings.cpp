@@ -435,28 +435,40 @@ void gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, const O
 }
 
 void xent_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& row_loss, const at::Tensor& lse) {
-  check_cuda(x, "logits", F32);
   TORCH_CHECK(x.dim() == 2, "logits must be [B, C]");
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  check_cuda(x, "logits", bf ? at::kBFloat16 : F32);
   const int64_t B = x.size(0), C = x.size(1);
   check_cuda(y, "target", I64, B);
   check_cuda(row_loss, "row_loss", F32, B);
   check_cuda(lse, "lse", F32, B);
-  hip_check(pde_xent_fwd(ptr<float>(x), ptr<long long>(y), (int)B, (int)C, ptr<float>(row_loss), ptr<float>(lse),
-                         cur_stream()),
-            "xent_fwd");
+  if (bf)
+    hip_check(pde_xent_fwd_bf16(x.data_ptr(), ptr<long long>(y), (int)B, (int)C, ptr<float>(row_loss), ptr<float>(lse),
+                                cur_stream()),
+              "xent_fwd");
+  else
+    hip_check(pde_xent_fwd(ptr<float>(x), ptr<long long>(y), (int)B, (int)C, ptr<float>(row_loss), ptr<float>(lse),
+                           cur_stream()),
+              "xent_fwd");
 }
 
 void xent_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& lse, const at::Tensor& gscale, bool per_row,
               double mul, const at::Tensor& dx) {
-  check_cuda(x, "logits", F32);
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  check_cuda(x, "logits", bf ? at::kBFloat16 : F32);
   const int64_t B = x.size(0), C = x.size(1);
   check_cuda(y, "target", I64, B);
   check_cuda(lse, "lse", F32, B);
   check_cuda(gscale, "grad", F32, per_row ? B : 1);
-  check_cuda(dx, "dx", F32, B * C);
-  hip_check(pde_xent_bwd(ptr<float>(x), ptr<long long>(y), ptr<float>(lse), ptr<float>(gscale), per_row, (float)mul,
-                         (int)B, (int)C, ptr<float>(dx), cur_stream()),
-            "xent_bwd");
+  check_cuda(dx, "dx", bf ? at::kBFloat16 : F32, B * C);
+  if (bf)
+    hip_check(pde_xent_bwd_bf16(x.data_ptr(), ptr<long long>(y), ptr<float>(lse), ptr<float>(gscale), per_row,
+                                (float)mul, (int)B, (int)C, dx.data_ptr(), cur_stream()),
+              "xent_bwd");
+  else
+    hip_check(pde_xent_bwd(ptr<float>(x), ptr<long long>(y), ptr<float>(lse), ptr<float>(gscale), per_row, (float)mul,
+                           (int)B, (int)C, ptr<float>(dx), cur_stream()),
+              "xent_bwd");
 }
 
 void log_softmax_fwd(const at::Tensor& x, const at::Tensor& out) {

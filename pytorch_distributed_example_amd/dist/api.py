@@ -462,8 +462,9 @@ def _check(t: torch.Tensor):
         raise TypeError(f"unsupported dtype {t.dtype}")
 
 
-def _gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool, what: str = "collective"):
-    """Run fn(stream_handle) on the group's comm stream, ordered after the caller's stream."""
+def gpu_launch(g: ProcessGroup, tensors, fn, async_op: bool, what: str = "collective"):
+    """Run fn(stream_handle) on the group's comm stream, ordered after the caller's stream (the
+    watchdog covers it when the group has RCCL); returns a Work (async) or joins the caller's stream."""
     g.check_health()
     g.p2p_flush()        # host isend/irecv issued before this collective start now (asynchronously)
     cur = torch.cuda.current_stream(g.device)
@@ -504,7 +505,7 @@ def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool
     _check(tensor)
     code, dt, n = _op_code(op), _DTYPES[tensor.dtype], tensor.numel()
     if g._gpu_ok(tensor) and code <= 4:      # RCCL has no bitwise reductions
-        return _gpu_launch(g, [tensor], lambda s: g.rccl.all_reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt,
+        return gpu_launch(g, [tensor], lambda s: g.rccl.all_reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt,
                                                                      code, s), async_op)
     if tensor.is_cuda:
         _host_staged([tensor], lambda c: _host(g).allreduce(c[0].data_ptr(), n, dt, code))
@@ -520,7 +521,7 @@ def broadcast(tensor: torch.Tensor, src: int = 0, group=None, async_op: bool = F
     _check(tensor)
     root = g.group_rank(src)
     if g._gpu_ok(tensor):
-        return _gpu_launch(g, [tensor], lambda s: g.rccl.broadcast(tensor.data_ptr(), tensor.data_ptr(),
+        return gpu_launch(g, [tensor], lambda s: g.rccl.broadcast(tensor.data_ptr(), tensor.data_ptr(),
                                                                     tensor.numel(), _DTYPES[tensor.dtype], root, s),
                            async_op)
     if tensor.is_cuda:
@@ -540,7 +541,7 @@ def all_gather_into_tensor(output_tensor: torch.Tensor, input_tensor: torch.Tens
     if output_tensor.numel() != input_tensor.numel() * g.size():
         raise ValueError("output must hold world_size x input elements")
     if g._gpu_ok(input_tensor):
-        return _gpu_launch(g, [output_tensor, input_tensor],
+        return gpu_launch(g, [output_tensor, input_tensor],
                            lambda s: g.rccl.all_gather(input_tensor.data_ptr(), output_tensor.data_ptr(),
                                                        input_tensor.numel(), _DTYPES[input_tensor.dtype], s),
                            async_op)
@@ -583,7 +584,7 @@ def reduce_scatter_tensor(output: torch.Tensor, input: torch.Tensor, op=ReduceOp
         raise ValueError("input must hold world_size x output elements")
     code, dt = _op_code(op), _DTYPES[input.dtype]
     if g._gpu_ok(input) and code <= 4:
-        return _gpu_launch(g, [output, input], lambda s: g.rccl.reduce_scatter(input.data_ptr(), output.data_ptr(),
+        return gpu_launch(g, [output, input], lambda s: g.rccl.reduce_scatter(input.data_ptr(), output.data_ptr(),
                                                                                output.numel(), dt, code, s), async_op)
     if input.is_cuda:
         _host_staged([output, input], lambda c: _host(g).reduce_scatter(c[1].data_ptr(), c[0].data_ptr(),
@@ -605,7 +606,7 @@ def reduce(tensor: torch.Tensor, dst: int = 0, op=ReduceOp.SUM, group=None, asyn
     _check(tensor)
     root, code, dt, n = g.group_rank(dst), _op_code(op), _DTYPES[tensor.dtype], tensor.numel()
     if g._gpu_ok(tensor) and code <= 4:
-        return _gpu_launch(g, [tensor], lambda s: g.rccl.reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt, code,
+        return gpu_launch(g, [tensor], lambda s: g.rccl.reduce(tensor.data_ptr(), tensor.data_ptr(), n, dt, code,
                                                                  root, s), async_op)
     if tensor.is_cuda:
         _host_staged([tensor], lambda c: _host(g).reduce(c[0].data_ptr(), n, dt, code, root))
@@ -659,7 +660,7 @@ def all_to_all_single(output: torch.Tensor, input: torch.Tensor, output_split_si
     _check(input)
     per = input.numel() // g.size()
     if g._gpu_ok(input):
-        return _gpu_launch(g, [output, input], lambda s: g.rccl.all_to_all(input.data_ptr(), output.data_ptr(), per,
+        return gpu_launch(g, [output, input], lambda s: g.rccl.all_to_all(input.data_ptr(), output.data_ptr(), per,
                                                                            _DTYPES[input.dtype], s), async_op)
     if input.is_cuda:
         _host_staged([output, input], lambda c: _host(g).alltoall(c[1].data_ptr(), c[0].data_ptr(),
@@ -674,7 +675,7 @@ def send(tensor: torch.Tensor, dst: int, group=None, tag: int = 0):
     _check(tensor)
     peer = g.group_rank(dst)
     if g._gpu_ok(tensor):
-        _gpu_launch(g, [tensor], lambda s: g.rccl.send(tensor.data_ptr(), tensor.numel(), _DTYPES[tensor.dtype],
+        gpu_launch(g, [tensor], lambda s: g.rccl.send(tensor.data_ptr(), tensor.numel(), _DTYPES[tensor.dtype],
                                                        peer, s), False)
         return
     t = tensor.detach().cpu().contiguous() if tensor.is_cuda else tensor
@@ -688,7 +689,7 @@ def recv(tensor: torch.Tensor, src: Optional[int] = None, group=None, tag: int =
         raise NotImplementedError("recv from any source")
     peer = g.group_rank(src)
     if g._gpu_ok(tensor):
-        _gpu_launch(g, [tensor], lambda s: g.rccl.recv(tensor.data_ptr(), tensor.numel(), _DTYPES[tensor.dtype],
+        gpu_launch(g, [tensor], lambda s: g.rccl.recv(tensor.data_ptr(), tensor.numel(), _DTYPES[tensor.dtype],
                                                        peer, s), False)
         return src
     if tensor.is_cuda:
@@ -753,7 +754,7 @@ def batch_isend_irecv(p2p_op_list: List[P2POp]) -> List[Work]:
                     f(t.data_ptr(), t.numel(), _DTYPES[t.dtype], g.group_rank(o.peer), stream)
             finally:
                 g.rccl.group_end()
-        w = _gpu_launch(g, [o.tensor for o in p2p_op_list], fn, True)
+        w = gpu_launch(g, [o.tensor for o in p2p_op_list], fn, True)
         return [w]
     # host: every send and receive of the batch in ONE full-duplex exchange (GPU tensors staged)
     staged = []

@@ -50,8 +50,11 @@ def _host_allreduce_max_f64(group, vals) -> list:
 class PeerAllReduce:
     """Collective constructor; see the module docstring.  ``ok`` says whether the path is usable."""
 
-    def __init__(self, group, device: torch.device, capacity_bytes: int, timeout_ms: int = 10000,
+    def __init__(self, group, device: torch.device, capacity_bytes: int, timeout_ms: Optional[int] = None,
                  self_test: bool = True):
+        # barrier time-out: a dead / hung peer latches an error instead of hanging (PDE_PEER_TIMEOUT_MS)
+        if timeout_ms is None:
+            timeout_ms = int(os.environ.get("PDE_PEER_TIMEOUT_MS", "10000"))
         self.group = group
         self.device = torch.device(device)
         self.rank, self.world = group.rank(), group.size()

@@ -106,9 +106,8 @@ class CrossEntropyFn(torch.autograd.Function):
         if reduction == "none":
             return rl
         tot = torch.empty(1, device=x.device, dtype=torch.float32)
-        kernels().colsum(rl, B, 1, tot)
-        out = tot.reshape(())
-        return out / B if reduction == "mean" else out
+        kernels().sum_f32(rl, tot, 1.0 / B if reduction == "mean" else 1.0)   # the mean's divide folded in
+        return tot.reshape(())
 
     @staticmethod
     def backward(ctx, g):
@@ -117,7 +116,10 @@ class CrossEntropyFn(torch.autograd.Function):
         dx = torch.empty_like(xc)
         per_row = ctx.reduction == "none"
         mul = 1.0 / B if ctx.reduction == "mean" else 1.0
-        kernels().xent_bwd(xc, yc, lse, _c(g.float().reshape(-1)), per_row, mul, dx)
+        gs = g.reshape(-1)
+        if gs.dtype != torch.float32:
+            gs = gs.float()
+        kernels().xent_bwd(xc, yc, lse, _c(gs), per_row, mul, dx)
         return dx, None, None
 
 
@@ -224,4 +226,6 @@ def log_softmax(x, dim=1):
 def cross_entropy(logits, target, reduction="mean"):
     if logits.dim() != 2:
         raise NotImplementedError("GPU cross_entropy kernel: [B, C] logits")
-    return CrossEntropyFn.apply(logits.float(), target, reduction)
+    if logits.dtype not in (torch.float32, torch.bfloat16):
+        logits = logits.float()
+    return CrossEntropyFn.apply(logits, target, reduction)          # bf16 logits read as they are

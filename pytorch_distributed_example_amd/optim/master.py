@@ -80,6 +80,14 @@ class _MasterBase(torch.optim.Optimizer):
                 st[k] = layout.view(buf, name)
             st["step"] = self._flat["step_dev"] if self.capturable else torch.tensor(float(self._step))
 
+    def state_tensors(self):
+        """The optimizer's device state (fp32 master weights, moments, device step count): what a caller
+        snapshots and restores around trial steps (``parallel.tune_bucket_cap(restore=...)``), together
+        with the host step count ``_step``."""
+        if self._flat is None:
+            self._build()
+        return list(self._flat["bufs"].values()) + [self._flat["step_dev"]]
+
     def _sync_grads(self):
         f = self._flat
         for p in self._all_params():

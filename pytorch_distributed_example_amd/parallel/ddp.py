@@ -25,12 +25,20 @@ changed after construction (``set_bucket_cap``: bucket boundaries only, the flat
 cap-independent) so a benchmark can time whole steps per cap on the node and keep the fastest
 (``tune_bucket_cap``).
 
-Reduction precision: bf16 parameters have bf16 gradients; ``reduce_dtype=torch.float32`` (the
-default for non-fp32 gradients) all-reduces each bucket through an fp32 staging buffer -- one
-rounding of the exact sum back to the gradient dtype instead of one rounding per ring hop (RCCL sums
-bf16 buckets in bf16 between hops: up to W-1 roundings, inherited by fp32 master weights).  It
-doubles the bytes on the wire; with buckets overlapped with backward that is mostly hidden.
-``reduce_dtype=None`` reduces in the gradient dtype (torch DDP's behaviour).
+Reduction routes (``reduce_route``; bf16 / fp16 gradients):
+
+* ``"peer"``  -- bf16 on the wire, fp32 accumulation, ONE rounding: the xGMI peer all-reduce
+  (``dist/peer.py``, two-shot: every GPU reduces 1/W of the bucket from all peers over the 7 links,
+  then gathers the other chunks), run on the comm stream in chunks of the peer buffer's capacity;
+* ``"fp32"``  -- RCCL through an fp32 staging copy (one rounding, twice the bytes on the wire);
+* ``"param"`` -- RCCL in the gradient dtype (torch DDP's behaviour: RCCL's ring sums bf16 between
+  hops, up to W-1 roundings).
+
+``"auto"`` (default) starts on ``peer`` when the peer path set up on every rank, else ``fp32`` for
+bf16 / fp16 gradients, else ``param``; ``tune_bucket_cap`` times whole training steps per
+(cap, route) on the node and keeps the fastest precise one.  ``PDE_DDP_REDUCE_DTYPE=param`` forces
+torch's behaviour.  (The older ``reduce_dtype=torch.float32`` argument selects ``fp32``.)  Staging
+buffers are allocated on the first bucket that needs them (nothing at world size 1).
 """
 from __future__ import annotations
 
@@ -59,7 +67,8 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: float = 25.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 static_graph: bool = False, init_sync: bool = True, reduce_dtype="auto"):
+                 static_graph: bool = False, init_sync: bool = True, reduce_dtype="auto",
+                 reduce_route: str = "auto", peer_capacity_mb: float = 32.0):
         super().__init__()
         self.module = module
         if process_group is None and not dist.is_initialized():
@@ -89,14 +98,33 @@ class DistributedDataParallel(nn.Module):
         self.flat_params, self.flat_grads = self.layout.bind(dict(named), dtype=named[0][1].dtype)
         self._params = dict(named)
         gdt = named[0][1].dtype
-        if reduce_dtype == "auto":
-            # PDE_DDP_REDUCE_DTYPE=param: reduce in the gradient dtype (torch DDP's behaviour)
-            if os.environ.get("PDE_DDP_REDUCE_DTYPE", "auto") == "param":
-                reduce_dtype = None
-            else:
-                reduce_dtype = torch.float32 if gdt in (torch.bfloat16, torch.float16) else None
-        self.reduce_dtype = reduce_dtype if reduce_dtype != gdt else None
+        self._gdt = gdt
+        low = gdt in (torch.bfloat16, torch.float16)
+        if reduce_dtype is None or os.environ.get("PDE_DDP_REDUCE_DTYPE", "auto") == "param":
+            reduce_route = "param"
+        elif reduce_dtype != "auto" and reduce_dtype != gdt:
+            reduce_route = "fp32"
         self._stage = None
+        self._peer = None
+        self.peer_reason = ""
+        want_peer = (reduce_route in ("auto", "peer") and self.world_size > 1 and self.device.type == "cuda"
+                     and gdt in (torch.bfloat16, torch.float32) and os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0")
+        if want_peer:
+            # collective: every rank sets up (or fails) together; any failure -> no peer route anywhere
+            from ..dist.peer import PeerAllReduce
+            cap = min(int(peer_capacity_mb * (1 << 20)), self.layout.total * named[0][1].element_size())
+            pk = PeerAllReduce(self.process_group, self.device, max(cap, 1 << 16))
+            if pk.ok:
+                self._peer = pk
+            else:
+                self.peer_reason = pk.reason
+        if reduce_route == "auto":
+            reduce_route = "peer" if self._peer is not None else ("fp32" if low else "param")
+        if reduce_route == "peer" and self._peer is None:
+            raise RuntimeError(f"reduce_route='peer' but the xGMI peer all-reduce is unavailable: {self.peer_reason}")
+        if reduce_route not in ("peer", "fp32", "param"):
+            raise ValueError(f"unknown reduce_route {reduce_route!r}")
+        self.reduce_route = reduce_route
         self.set_bucket_cap(bucket_cap_mb)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(n)) for n, p in named]
         self._callback_queued = False
@@ -117,10 +145,29 @@ class DistributedDataParallel(nn.Module):
             self.buckets.append(_Bucket(i, bn, a, b))
             for n in bn:
                 self._bucket_of[n] = i
-        if self.reduce_dtype is not None and self._stage is None:
-            # one fp32 slot per gradient element: every bucket stages into its own range, so no
-            # bucket's fill can race another bucket's in-flight all-reduce or copy-back
-            self._stage = torch.empty(self.layout.total, device=self.device, dtype=self.reduce_dtype)
+
+    @property
+    def reduce_dtype(self):
+        """Accumulation dtype of the gradient reduction (None: the gradient dtype itself)."""
+        return None if self.reduce_route == "param" or self._gdt == torch.float32 else torch.float32
+
+    def set_reduce_route(self, route: str):
+        """Switch the reduction route between iterations (identically on every rank)."""
+        if route == "peer" and self._peer is None:
+            raise RuntimeError("the xGMI peer all-reduce is unavailable")
+        if route not in ("peer", "fp32", "param"):
+            raise ValueError(route)
+        self.reduce_route = route
+
+    def reduce_routes(self):
+        """Routes this DDP can run ("peer" only where the peer path set up on every rank)."""
+        precise = ["fp32"] if self._gdt != torch.float32 else ["param"]
+        return (["peer"] if self._peer is not None else []) + precise
+
+    def wire_bytes_per_step(self) -> int:
+        """Gradient bytes each rank hands to the all-reduce per step on the current route."""
+        esz = 4 if self.reduce_route == "fp32" else self.flat_grads.element_size()
+        return self.layout.total * esz
 
     # ------------------------------------------------------------------ forward
     def forward(self, *inputs, **kwargs):
@@ -163,10 +210,17 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, bk: _Bucket):
         view = self.flat_grads[bk.start:bk.end]
         with prof.range(f"ddp.bucket{bk.index}.all_reduce"):
-            if self.reduce_dtype is None:
+            if self.reduce_route == "peer":
+                bk.work = self._launch_peer(view)
+                return
+            if self.reduce_route == "param" or self._gdt == torch.float32:
                 bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
                 return
-            # fp32 staging: one rounding of the all-reduced sum back to the gradient dtype
+            # fp32 staging: one rounding of the all-reduced sum back to the gradient dtype.  One fp32
+            # slot per gradient element (allocated on first use): no bucket's fill can race another
+            # bucket's in-flight all-reduce or copy-back
+            if self._stage is None:
+                self._stage = torch.empty(self.layout.total, device=self.device, dtype=torch.float32)
             st = self._stage[bk.start:bk.end]
             st.copy_(view)
             work = dist.all_reduce(st, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
@@ -179,6 +233,23 @@ class DistributedDataParallel(nn.Module):
                 prev = work._post
                 work._post = (lambda: (prev(), post())) if prev else post
             bk.work = work
+
+    def _launch_peer(self, view: torch.Tensor):
+        """AVG of one bucket by the xGMI peer kernel (two-shot, fp32 accumulation, one rounding),
+        chunked by the peer buffer's capacity, on the group's comm stream after the compute stream."""
+        pk = self._peer
+        esz = view.element_size()
+        chunk = max(8, (pk.capacity_bytes // esz) // 8 * 8)
+        n = view.numel()
+        fn_native = pk.native.all_reduce_bf16 if view.dtype == torch.bfloat16 else pk.native.all_reduce_f32
+        scale = 1.0 / self.world_size
+        base = view.data_ptr()
+
+        def fn(stream):
+            for off in range(0, n, chunk):
+                cnt = min(chunk, n - off)
+                fn_native(base + off * esz, base + off * esz, cnt, scale, 2, stream)
+        return dist.gpu_launch(self.process_group, [view], fn, async_op=True, what="ddp peer all-reduce")
 
     def _finalize(self):
         for bk in self.buckets:
@@ -209,36 +280,52 @@ class DistributedDataParallel(nn.Module):
 
 
 def tune_bucket_cap(ddp: "DistributedDataParallel", step, caps=(4, 8, 16, 25, 50, 64), warmup: int = 1,
-                    iters: int = 3):
-    """Pick the DDP bucket cap by timing WHOLE training steps on this node (the cap that
-    keeps every bucket in the xGMI bandwidth regime while leaving overlap room depends on the model and
-    the link topology, so it is measured, not assumed).  ``step()`` runs one training step.  Per cap:
-    ``warmup`` untimed steps, then ``iters`` timed ones; the MAX over ranks decides, so every rank
-    keeps the same cap.  Returns ({cap_mb: ms per step}, best cap); the DDP is left at the best cap."""
+                    iters: int = 3, routes=None, restore=None):
+    """Pick the DDP bucket cap and reduction route by timing WHOLE training steps on this node
+    (the cap that keeps every bucket in the xGMI bandwidth regime while leaving overlap
+    room depends on the model and the link topology, so it is measured, not assumed).  ``step()``
+    runs one training step.  Per (route, cap): ``warmup`` untimed steps, then ``iters`` timed ones;
+    the MAX over ranks decides, so every rank keeps the same choice.  ``routes`` defaults to the
+    precise routes this DDP can run (``ddp.reduce_routes()``).
+
+    The trial steps train: pass ``restore`` (a list of tensors -- parameters, optimizer state, ...)
+    to have them snapshotted before and copied back after tuning; the data position the steps
+    advanced is the caller's.  Returns ({"route/cap_mb": ms per step}, best cap); the DDP is left at
+    the best cap and route."""
     import time
 
     group = ddp.process_group
-    times = []
-    for cap in caps:
-        ddp.set_bucket_cap(cap)
-        for _ in range(warmup):
-            step()
-        if ddp.device.type == "cuda":
-            torch.cuda.synchronize(ddp.device)
-        if group is not None:
-            dist.barrier(group=group)
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            step()
-        if ddp.device.type == "cuda":
-            torch.cuda.synchronize(ddp.device)
-        times.append((time.perf_counter() - t0) / iters * 1e3)
+    routes = list(routes or ddp.reduce_routes())
+    snap = [t.detach().clone() for t in (restore or [])]
+    keys, times = [], []
+    for route in routes:
+        ddp.set_reduce_route(route)
+        for cap in caps:
+            ddp.set_bucket_cap(cap)
+            for _ in range(warmup):
+                step()
+            if ddp.device.type == "cuda":
+                torch.cuda.synchronize(ddp.device)
+            if group is not None:
+                dist.barrier(group=group)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                step()
+            if ddp.device.type == "cuda":
+                torch.cuda.synchronize(ddp.device)
+            keys.append((route, float(cap)))
+            times.append((time.perf_counter() - t0) / iters * 1e3)
     t = torch.tensor(times, dtype=torch.float64)
     if group is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    res = {float(c): round(float(x), 3) for c, x in zip(caps, t.tolist())}
-    best = min(res, key=res.get)
+    res = {f"{r}/{c:g}": round(float(x), 3) for (r, c), x in zip(keys, t.tolist())}
+    bi = min(range(len(keys)), key=lambda i: t[i].item())
+    best_route, best = keys[bi]
+    ddp.set_reduce_route(best_route)
     ddp.set_bucket_cap(best)
+    with torch.no_grad():
+        for d, s0 in zip(restore or [], snap):
+            d.copy_(s0)
     return res, best
 
 

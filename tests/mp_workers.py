@@ -296,6 +296,42 @@ def case_ddp_bf16_reduce(reduce="fp32"):
     dist.destroy_process_group()
 
 
+def case_ddp_peer_bf16(cap_mb="32"):
+    """Verdict r2 item 5: bf16 DDP gradients reduced by the xGMI peer route (bf16 on the wire, fp32
+    accumulation, ONE rounding) on W ranks sharing one GPU, against the exact fp64 average; a small
+    peer capacity forces the chunked path (several peer calls per bucket)."""
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    dev = _shared_gpu_init()
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 384)).to(dev, torch.bfloat16)
+    ddp = DistributedDataParallel(net, bucket_cap_mb=0.25, reduce_route="peer", peer_capacity_mb=float(cap_mb))
+    assert ddp.reduce_route == "peer", ddp.peer_reason
+    g = torch.Generator().manual_seed(100 + R)
+    x = torch.randn(64, 256, generator=g).to(dev, torch.bfloat16)
+    local = {}
+    with ddp.no_sync():
+        ddp(x).float().pow(2).sum().backward()
+        for n, p in net.named_parameters():
+            local[n] = p.grad.detach().double().cpu().clone()
+    ddp.zero_grad()
+    for step in range(3):                       # several steps: both peer parities, chunk reuse
+        ddp.zero_grad()
+        ddp(x).float().pow(2).sum().backward()
+        torch.cuda.synchronize()
+    errs = {}
+    for n, p in net.named_parameters():
+        allg = [torch.empty_like(local[n]) for _ in range(W)]
+        dist.all_gather(allg, local[n])
+        exact = torch.stack(allg).mean(0)
+        ulp = exact.abs().clamp_min(1e-30) * 2.0 ** -8          # one bf16 rounding of the exact average
+        errs[n] = float(((p.grad.double().cpu() - exact).abs() / ulp).max())
+    bits = [int(p.grad.view(torch.int16).to(torch.int64).sum().item()) for p in net.parameters()]
+    emit({"rank": R, "max_err_ulp": max(errs.values()), "n_buckets": len(ddp.buckets), "bits": bits,
+          "peer_error": ddp._peer.error()})
+    dist.destroy_process_group()
+
+
 def case_manual_average(backend="gloo", steps="4"):
     """The reference's path: per-parameter all_reduce SUM / W after backward."""
     from pytorch_distributed_example_amd.models import build_net
