@@ -472,7 +472,10 @@ def bn_relu_maxpool(y, stats, bn):
 
 
 def max_pool3s2(x):
-    if x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0:
+    if x.is_cuda:
+        if x.dim() != 4 or x.shape[1] % 8 != 0:
+            # no silent library fallback on the GPU: the kernel moves 8 channels per lane
+            raise NotImplementedError(f"max_pool3s2: GPU kernel needs NCHW with C % 8 == 0, got {tuple(x.shape)}")
         return MaxPool3s2Fn.apply(x.contiguous(memory_format=torch.channels_last))
     return F.max_pool2d(x, 3, 2, 1)
 

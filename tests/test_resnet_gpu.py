@@ -166,6 +166,13 @@ def test_maxpool3s2(shape):
     assert rel_err(x.grad, xr.grad) < 1e-2
 
 
+def test_maxpool3s2_unsupported_raises():
+    """A GPU shape the kernel does not cover raises instead of falling back to the library."""
+    from pytorch_distributed_example_amd.ops.resnet import max_pool3s2
+    with pytest.raises(NotImplementedError):
+        max_pool3s2(torch.randn(2, 3, 8, 8, device=dev, dtype=torch.bfloat16))
+
+
 @pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 64, 9, 7), (3, 16, 6, 6)])
 def test_bn_relu_maxpool_fused(shape):
     """Fused stem tail (BN apply + ReLU + max-pool forward, pooling gather + ReLU mask + BN backward in

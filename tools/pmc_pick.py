@@ -12,7 +12,7 @@ from collections import defaultdict
 def main():
     root, keys = sys.argv[1], sys.argv[2:]
     acc = defaultdict(lambda: defaultdict(list))
-    for p in glob.glob(f"{root}/*/*counter_collection.csv"):
+    for p in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(p)):
             for k in keys:
                 if k in r["Kernel_Name"]:
