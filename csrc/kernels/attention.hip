@@ -92,17 +92,36 @@ __device__ __forceinline__ void store_dimrows(bf16_t* dst, const f32x16& a0, con
   }
 }
 
+// ------------------------------------------------------------------------------------ block map
+// (tile, batch*head) of this block.  The dispatcher deals blocks to the 8 XCDs round-robin, so with a
+// plain 2-D grid the tiles of one (batch, head) land on every XCD and each XCD re-fetches that head's
+// K/V (or Q/dO) tiles through its own L2 -- the kernels then run at the fabric rate of those
+// re-fetches.  Instead: XCD-contiguous ids (pde_hip.h xcd_remap), cut into groups of kAttnGroup heads
+// whose tiles stay L2-resident while the group runs, heaviest causal tiles first inside a group.
+// G = 0 keeps the plain order (no remap, one head per group) for A/B runs.
+constexpr int kAttnGroup = 8;
+__device__ __forceinline__ void attn_block(int nt, int nbh, int G, bool heavy_high, int& t, int& bh) {
+  const int id = G ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  G = G ? G : 1;
+  const int grp = id / (G * nt), r = id - grp * G * nt;
+  const int gsz = min(G, nbh - grp * G);
+  const int k = r / gsz;
+  bh = grp * G + (r - k * gsz);
+  t = heavy_high ? nt - 1 - k : k;
+}
+
 // ------------------------------------------------------------------------------------ forward
-// grid (T/128, B*H), 256 threads: wave w owns queries qt*128 + 32w + (0..31)
+// grid (T/128 * B*H), 256 threads: wave w owns queries qt*128 + 32w + (0..31)
 template <int NST, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_attn_fwd(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                      const bf16_t* __restrict__ V, int ldq, bf16_t* __restrict__ O,
                                                      int ldo, float* __restrict__ LSE, int T, int H, float sl2,
-                                                     float scale) {
+                                                     float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
-  const int qt = gridDim.x - 1 - blockIdx.x;  // longest (most keys) tiles first
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  int qt, bh;
+  attn_block(T / 128, gridDim.x / (T / 128), G, true, qt, bh);   // longest (most keys) tiles first
+  const int b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
   const uint32_t tbytes = (uint32_t)T * ldq * 2;
   const rsrc_t kr = make_rsrc(K + boff, tbytes), vr = make_rsrc(V + boff, tbytes);
@@ -214,7 +233,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_pre(const bf16_t* __restrict__
   Dd[((size_t)b * H + hh) * T + t] = acc;
 }
 
-// dQ: grid (T/128, B*H); transposed-score structure of the forward; K, V tiles staged in LDS
+// dQ: grid (T/128 * B*H); transposed-score structure of the forward; K, V tiles staged in LDS
 // (K rows for S^T, V rows for dP^T, K^T via transposed reads for dQ^T += K^T dS^T).
 template <int NST, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
@@ -222,11 +241,12 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restri
                                                         const bf16_t* __restrict__ dO, int ldo,
                                                         const float* __restrict__ LSE, const float* __restrict__ Dd,
                                                         bf16_t* __restrict__ dQ, int T, int H, float sl2,
-                                                        float scale) {
+                                                        float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
-  const int qt = gridDim.x - 1 - blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  int qt, bh;
+  attn_block(T / 128, gridDim.x / (T / 128), G, true, qt, bh);   // longest (most keys) tiles first
+  const int b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
   const uint32_t tbytes = (uint32_t)T * ldq * 2;
   const rsrc_t kr = make_rsrc(K + boff, tbytes), vr = make_rsrc(V + boff, tbytes);
@@ -302,7 +322,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restri
   store_dimrows(dQ + boff + (size_t)myq * ldq, a0, a1, scale, h);
 }
 
-// dK, dV: grid (T/128, B*H); wave w owns keys kb*128 + 32w + (0..31); loops over 64-query tiles
+// dK, dV: grid (T/128 * B*H); wave w owns keys kb*128 + 32w + (0..31); loops over 64-query tiles
 // with Q / dO / LSE / D staged in LDS (rows for S / dP, transposed reads for dK / dV).
 constexpr int kDkdvStage = 2 * TILE + 512;           // Q | dO | LSE[64] | D[64]
 template <int NST, int OCC>
@@ -312,11 +332,12 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkdv(const bf16_t* __rest
                                                           const float* __restrict__ LSE,
                                                           const float* __restrict__ Dd, bf16_t* __restrict__ dK,
                                                           bf16_t* __restrict__ dV, int T, int H, float sl2,
-                                                          float scale) {
+                                                          float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * kDkdvStage];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
-  const int kb = blockIdx.x;  // tile 0 has the most queries: natural order is heavy-first
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  int kb, bh;
+  attn_block(T / 128, gridDim.x / (T / 128), G, false, kb, bh);  // key tile 0 sees the most queries
+  const int b = bh / H, hh = bh % H;
   const size_t boff = (size_t)b * T * ldq + hh * HD;
   const rsrc_t qr = make_rsrc(Q + boff, (uint32_t)T * ldq * 2);
   const rsrc_t gr = make_rsrc(dO + (size_t)b * T * ldo + hh * HD, (uint32_t)T * ldo * 2);
@@ -417,29 +438,30 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkdv(const bf16_t* __rest
 }
 
 int g_attn_variant = 5;   // pde_attn_set_variant: LDS ring depth / occupancy (default: measured best)
+int g_attn_group = kAttnGroup;   // heads per L2 group of the block map (0: plain order)
 
 template <int NST, int OCC>
 void launch_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B, int T,
                 int H, float scale, hipStream_t st) {
-  hipLaunchKernelGGL((k_attn_fwd<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+  hipLaunchKernelGGL((k_attn_fwd<NST, OCC>), dim3(T / 128 * B * H), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, ldq, (bf16_t*)o, ldo, lse, T, H, scale * 1.4426950408889634f,
-                     scale);
+                     scale, g_attn_group);
 }
 
 template <int NST, int OCC>
 void launch_dq(const void* q, const void* k, const void* v, int ldq, const void* dout, int ldo, const float* lse,
                const float* Dd, void* dq, int B, int T, int H, float sl2, float scale, hipStream_t st) {
-  hipLaunchKernelGGL((k_attn_bwd_dq<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+  hipLaunchKernelGGL((k_attn_bwd_dq<NST, OCC>), dim3(T / 128 * B * H), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dq, T, H,
-                     sl2, scale);
+                     sl2, scale, g_attn_group);
 }
 
 template <int NST, int OCC>
 void launch_dkdv(const void* q, const void* k, const void* v, int ldq, const void* dout, int ldo, const float* lse,
                  const float* Dd, void* dk, void* dv, int B, int T, int H, float sl2, float scale, hipStream_t st) {
-  hipLaunchKernelGGL((k_attn_bwd_dkdv<NST, OCC>), dim3(T / 128, B * H), dim3(256), 0, st, (const bf16_t*)q,
+  hipLaunchKernelGGL((k_attn_bwd_dkdv<NST, OCC>), dim3(T / 128 * B * H), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, ldq, (const bf16_t*)dout, ldo, lse, Dd, (bf16_t*)dk,
-                     (bf16_t*)dv, T, H, sl2, scale);
+                     (bf16_t*)dv, T, H, sl2, scale, g_attn_group);
 }
 
 }  // namespace
@@ -449,7 +471,12 @@ extern "C" {
 // variant bits: 1 = forward with a 3-deep ring at 3 blocks per CU, 2 = dQ likewise (spills: slower),
 //               4 = dK/dV with a 3-deep ring (2 blocks per CU).  Default 5, measured on MI355X at the
 //               GPT-2 shape (tools/attn_bench.py, profiles/r2_attn/): fwd 85.3 -> 71.3 us, bwd 263.8 -> 241.0 us
-void pde_attn_set_variant(int v) { g_attn_variant = v; }
+//               bits 8..15: heads per L2 group of the block map (attn_block), 0 = default, 255 = plain order
+void pde_attn_set_variant(int v) {
+  g_attn_variant = v & 0xff;
+  const int g = (v >> 8) & 0xff;
+  g_attn_group = g == 0 ? kAttnGroup : g == 255 ? 0 : g;
+}
 
 hipError_t pde_attn_fwd(const void* q, const void* k, const void* v, int ldq, void* o, int ldo, float* lse, int B,
                         int T, int H, float scale, hipStream_t st) {

@@ -101,7 +101,7 @@ def _attn_ref(qkv, H):
     return y.transpose(1, 2).reshape(B, Tn, C)
 
 
-@pytest.mark.parametrize("B,Tn,H", [(2, 256, 3), (1, 128, 1), (1, 1024, 12)])
+@pytest.mark.parametrize("B,Tn,H", [(2, 256, 3), (1, 128, 1), (1, 1024, 12), (3, 512, 5)])
 def test_flash_attention(B, Tn, H):
     torch.manual_seed(4)
     C = 64 * H
@@ -118,6 +118,30 @@ def test_flash_attention(B, Tn, H):
     assert rel_err(dv, rv) < 3e-2
     assert rel_err(dk, rk) < 3e-2
     assert rel_err(dq, rq) < 3e-2
+
+
+def test_flash_attention_block_maps_agree():
+    """The XCD-grouped block map (any group size, partial last group) computes exactly what the
+    plain block order computes: every block's work is the same, only its placement changes."""
+    from pytorch_distributed_example_amd._ext import kernels
+    K = kernels()
+    torch.manual_seed(6)
+    B, Tn, H = 3, 384, 7
+    C = 64 * H
+    qkv = torch.randn(B, Tn, 3 * C).to(dev, torch.bfloat16)
+    g = torch.randn(B, Tn, C).to(dev, torch.bfloat16)
+    outs = []
+    try:
+        for grp in (255, 0, 3, 16):
+            K.attn_set_variant(5 | (grp << 8))
+            x = qkv.clone().requires_grad_()
+            y = T.causal_attention(x, H)
+            y.backward(g)
+            outs.append((y.detach(), x.grad))
+    finally:
+        K.attn_set_variant(5)
+    for y, dx in outs[1:]:
+        assert torch.equal(y, outs[0][0]) and torch.equal(dx, outs[0][1])
 
 
 def _tiny_cfg():
