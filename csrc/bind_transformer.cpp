@@ -111,12 +111,14 @@ void embed_bwd(const at::Tensor& dX, const at::Tensor& idx, const at::Tensor& dw
             "embed_bwd");
 }
 
-void sumsq_bf16(const at::Tensor& g, double scale, const at::Tensor& out) {
+void sumsq_bf16(const at::Tensor& g, double scale, const at::Tensor& out, const OptT& step_inc) {
   check_cuda(g, "g", BF16);
   check_cuda(out, "out", F32, 1025);      // [0] result, [1..1024] per-block partials
   TORCH_CHECK(g.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0,
               "sumsq: numel % 8 and a 16-byte aligned buffer");
-  hip_check(pde_sumsq_bf16(g.data_ptr(), g.numel(), (float)scale, ptr<float>(out), cur_stream()), "sumsq_bf16");
+  hip_check(pde_sumsq_bf16(g.data_ptr(), g.numel(), (float)scale, ptr<float>(out),
+                           optr<float>(step_inc, "step_inc", F32, 1), cur_stream()),
+            "sumsq_bf16");
 }
 
 void adamw_master(const at::Tensor& master, const at::Tensor& p16, const at::Tensor& g16, const at::Tensor& m,
@@ -290,7 +292,7 @@ void register_transformer(pybind11::module& m) {
   m.def("xent_bf16", &xent_bf16);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
-  m.def("sumsq_bf16", &sumsq_bf16);
+  m.def("sumsq_bf16", &sumsq_bf16, py::arg("g"), py::arg("scale"), py::arg("out"), py::arg("step_inc") = py::none());
   m.def("adamw_master", &adamw_master, py::arg("master"), py::arg("p16"), py::arg("g16"), py::arg("m"), py::arg("v"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("grad_scale"),
         py::arg("step"), py::arg("decay_blk") = py::none(), py::arg("clip_sumsq") = py::none(),

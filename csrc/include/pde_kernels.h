@@ -120,7 +120,7 @@ hipError_t pde_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, v
                          hipStream_t st);
 hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* dwpe, float* acc, uint8_t* touched,
                          int N, int T, int C, int Vp, int accumulate_pos, hipStream_t st);
-hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st);
+hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, float* step_inc, hipStream_t st);
 hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m, float* v, int64_t n, float lr,
                             float b1, float b2, float eps, float wd, float grad_scale, int step,
                             const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, const float* step_dev,

@@ -25,7 +25,9 @@
 // The MFMA is issued with the operands swapped (D' = B^T A^T), so a lane's accumulator registers
 // hold FOUR CONSECUTIVE COLUMNS of C: the epilogue writes 8-byte pieces into an LDS tile and stores
 // C as coalesced 16-byte rows, applying bias (fp32, before the single bf16 rounding), GELU (writing
-// pre-activation and activation), or the GELU backward (reading the saved pre-activation).
+// the activation and its derivative gelu'(pre), so the backward is one multiply and the pre-activation
+// is never stored), or the GELU backward (reading the saved derivative).  GELU runs in the sigmoid
+// form on float2 (packed VALU) with one exp2 + one rcp per value (pde_act.h).
 //
 // Bias gradient: db[m] = sum_k A(m, k) is one more MFMA per k-step against a ones fragment, issued
 // only by the blocks of the first column tile (k-steps shared round-robin by their WN waves), into
@@ -45,18 +47,20 @@ namespace {
 
 using namespace pde_lds;
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
 enum Epi { kBf16 = 0, kGelu = 1, kGeluBwd = 2, kSlab = 3 };
 
 struct GemmArgs {
   const bf16_t* A;
   const bf16_t* B;
   void* C;               // bf16 [M][ldc], or fp32 slabs [splits][M][ldc] (kSlab)
-  bf16_t* C2;            // kGelu: activation output [M][ldc] (C gets the pre-activation)
+  bf16_t* C2;            // kGelu: gelu'(pre) [M][ldc] (C gets the activation gelu(pre))
   const bf16_t* bias;    // [N] or null (kBf16 / kGelu)
-  const bf16_t* aux;     // kGeluBwd: pre-activation [M][ldc]
+  const bf16_t* aux;     // kGeluBwd: gelu'(pre) [M][ldc] as written by kGelu
   float* colsum;         // [splits][M] bias-gradient partials (CS) or null
   const float* scale;    // kBf16: device scalar multiplying the result (e.g. a loss gradient) or null
-  uint32_t a_bytes, b_bytes;
+  uint32_t a_bytes, b_bytes, c_bytes;   // c_bytes: C (and C2 / aux) extent, persistent kernel's stores
   int M, N, K, lda, ldb, ldc;
   int mtiles, ntiles, kper;
   int dbg;               // ablation (v1 loop, wrong results): 1 no DMA, 2 no waits/barriers, 4 no LDS reads
@@ -171,24 +175,28 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
         const size_t o = (size_t)m * a.ldc + n;
         if constexpr (EPI == kBf16) {
           *reinterpret_cast<uint4*>(C + o) = v;
-        } else if constexpr (EPI == kGelu) {
-          *reinterpret_cast<uint4*>(C + o) = v;
-          float f[8];
-          unpack8(v, f);
+        } else if constexpr (EPI == kGelu) {           // C = gelu(pre), C2 = gelu'(pre) (the backward's factor)
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          uint32_t ya[4], da[4];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = gelu_t(f[e], nullptr);
-          *reinterpret_cast<uint4*>(a.C2 + o) = pack8(f);
-        } else {                                       // kGeluBwd: dX = bf16(acc) * gelu'(pre)
-          float f[8], p[8];
-          unpack8(v, f);
-          unpack8(*reinterpret_cast<const uint4*>(a.aux + o), p);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float d;
-            gelu_t(p[e], &d);
-            f[e] *= d;
+          for (int e = 0; e < 4; ++e) {
+            pde_f2 d;
+            const pde_f2 y = gelu2_d(pde_f2{bf_lo(w[e]), bf_hi(w[e])}, d);
+            ya[e] = pack_bf2(y.x, y.y);
+            da[e] = pack_bf2(d.x, d.y);
           }
-          *reinterpret_cast<uint4*>(C + o) = pack8(f);
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(ya[0], ya[1], ya[2], ya[3]);
+          *reinterpret_cast<uint4*>(a.C2 + o) = make_uint4(da[0], da[1], da[2], da[3]);
+        } else {                                       // kGeluBwd: dX = bf16(acc) * gelu'(pre), gelu' saved by kGelu
+          const uint4 g = *reinterpret_cast<const uint4*>(a.aux + o);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w}, gw[4] = {g.x, g.y, g.z, g.w};
+          uint32_t r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const pde_f2 p = pde_f2{bf_lo(w[e]), bf_hi(w[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+            r[e] = pack_bf2(p.x, p.y);
+          }
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(r[0], r[1], r[2], r[3]);
         }
       }
     }
@@ -595,6 +603,296 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm2(GemmArgs a) {
   gemm_epilogue<TM, TN, WM, WN, EPI, CS>(a, acc, accb, smem, m0, n0, split, cs_on);
 }
 
+// ============================================================================ persistent v1 (fprop / dgrad)
+// One block per CU walks the tiles r * gridDim + slot (slot = XCD-contiguous remap of blockIdx, so each
+// XCD works on a contiguous run of the grouped tile order, as the one-shot grid does).  What it buys:
+// the output of tile i drains to memory while tile i+1 computes.  Per tile, after the K loop:
+//   acc -> LDS tile (bias / scale, bf16) -> barrier -> this thread's 16-byte chunks into registers
+//   (and, GELU backward, its gelu' chunks from memory) -> barrier -> LDS-DMA of tile i+1's stage 0
+//   -> GELU math + buffer stores of tile i (masked lanes store to an out-of-range offset: the store
+//   count per wave is a compile-time constant) -> tile i+1's K loop, whose first wait leaves those
+//   NSTORE stores in flight (vmcnt counts them in issue order: they are younger than stage 0).
+// In the one-shot grid every CU wrote its tile and only then started the next block's loads; on the
+// GPT-2 shapes the writes of a round of tiles (25-200 MB) were not overlapped with any MFMA work.
+// NST = 2 stages (64-deep), K-contiguous A (TA = 0), no split-K, no bias gradient.
+template <int TM, int TN, int WM, int WN, int SPREAD, bool TB, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int WTM = TM * 32, WTN = TN * 32, BM = WM * WTM, BN = WN * WTN;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
+  constexpr int AG = BM / 8 / NW, BG = BN / 8 / NW;
+  static_assert(AG * 8 * NW == BM && BG * 8 * NW == BN, "one 8-row group per wave-instruction");
+  static_assert(!TB || BN % 64 == 0, "transposed operands come in 64-wide images");
+  static_assert(EPI == kBf16 || EPI == kGelu || EPI == kGeluBwd, "bf16 epilogues only");
+  constexpr int LPS = AG + BG;
+  constexpr int RS = BN * 2 + 16;
+  constexpr int TILE_BYTES = BM * RS;
+  constexpr int SMEM = 2 * STAGE > TILE_BYTES ? 2 * STAGE : TILE_BYTES;
+  constexpr int CPR = BN / 8, CH = BM * CPR / NT;       // 16-byte chunks per tile row / per thread
+  static_assert(CH * NT == BM * CPR, "whole chunks per thread");
+  constexpr int CPI = 2, SPC = EPI == kGelu ? 2 : 1;    // deferred chunk jobs per K iteration, stores per job
+  static_assert(CH >= 2 * CPI, "the GELU-backward prefetch covers two iterations of jobs");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int t = threadIdx.x, l = t & 63, lr = l & 31, lh = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ntile = a.mtiles * a.ntiles;
+  const int P = gridDim.x;
+  int id = xcd_remap(blockIdx.x, P);
+  if (id >= ntile) return;
+  const int KT = (a.K + 63) >> 6;
+  const int lrow = glds_row(l);
+  const uint32_t bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  const rsrc_t cr = make_rsrc(a.C, a.c_bytes);
+  const rsrc_t c2r = make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
+  const rsrc_t xr = make_rsrc(EPI == kGeluBwd ? (const void*)a.aux : a.C, EPI == kGeluBwd ? a.c_bytes : 0);
+
+  auto coords = [&](int tid, int& m0, int& n0) {
+    constexpr int G = 8;
+    const int grp = tid / (G * a.ntiles), r2 = tid - grp * (G * a.ntiles);
+    const int gsz = min(G, a.mtiles - grp * G);
+    m0 = (grp * G + r2 % gsz) * BM;
+    n0 = (r2 / gsz) * BN;
+  };
+  uint32_t aoff[AG], boff[BG];
+  int ach[AG], bch[BG];
+  auto setup = [&](int m0, int n0) {
+#pragma unroll
+    for (int u = 0; u < AG; ++u) {
+      const int g = NW * u + w, ch = glds_chunk(l, g & 1);
+      ach[u] = 8 * ch;
+      const int m = m0 + 8 * g + lrow;
+      aoff[u] = m < a.M ? (uint32_t)(((size_t)m * a.lda + 8 * ch) * 2) : kOOB;
+    }
+#pragma unroll
+    for (int v = 0; v < BG; ++v) {
+      const int g = NW * v + w, ch = glds_chunk(l, g & 1);
+      bch[v] = 8 * ch;
+      if constexpr (!TB) {
+        const int n = n0 + 8 * g + lrow;
+        boff[v] = n < a.N ? (uint32_t)(((size_t)n * a.ldb + 8 * ch) * 2) : kOOB;
+      } else {
+        const int k = 8 * (g & 7) + lrow, n = n0 + 64 * (g >> 3) + 8 * ch;
+        boff[v] = n < a.N ? (uint32_t)(((size_t)k * a.ldb + n) * 2) : kOOB;
+      }
+    }
+  };
+  auto issue_piece = [&](auto P_, int kt, int buf) {
+    constexpr int Pc = decltype(P_)::value;
+    const char* As = smem + buf * STAGE;
+    const int kb = kt * 64;
+    if constexpr (Pc < AG) {
+      glds16(ar, As + (NW * Pc + w) * 1024, kb + ach[Pc] < a.K ? aoff[Pc] + (uint32_t)kt * 128u : kOOB);
+    } else {
+      constexpr int V = Pc - AG;
+      glds16(br, As + ABYTES + (NW * V + w) * 1024,
+             (TB || kb + bch[V] < a.K) ? boff[V] + (uint32_t)kt * bstep : kOOB);
+    }
+  };
+  auto issue = [&](int kt, int buf) { static_for<0, LPS>([&](auto P_) { issue_piece(P_, kt, buf); }); };
+
+  uint2 bbase[TB ? TN : 1];
+  const uint2 abase = row_lane_off(wm * WTM);
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bbase[j] = add2(tr_lane_off_k8(), colblk_off(wn * TN + j));
+  } else {
+    bbase[0] = row_lane_off(wn * WTN);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+  const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+  const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+
+  // chunk c (0..CH-1) of this thread in a tile: row (t + c*NT) / CPR, 16-byte column chunk (t + c*NT) % CPR.
+  // tv is t laundered through an empty asm, so the compiler cannot hoist CH per-chunk offsets out of
+  // the tile loop (16 loop-invariant registers at 256x256 spilled)
+  int tv = t;
+  auto chunk_off = [&](int c, int tm0, int tn0) -> uint32_t {
+    const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
+    const int m = tm0 + row, n = tn0 + 8 * cc;
+    return (m < a.M && n < a.N) ? (uint32_t)(((size_t)m * a.ldc + n) * 2) : kOOB;
+  };
+  // the epilogue job of one chunk: GELU / GELU-backward math on packed float2 and SPC buffer stores
+  auto job = [&](const uint4& v, const uint4& gx, uint32_t co) {
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (EPI == kBf16) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), cr, co, 0, 0);
+    } else if constexpr (EPI == kGelu) {
+      uint32_t ya[4], da[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pde_f2 d;
+        const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+        ya[e] = pack_bf2(y.x, y.y);
+        da[e] = pack_bf2(d.x, d.y);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
+    } else {
+      const uint32_t gw[4] = {gx.x, gx.y, gx.z, gx.w};
+      uint32_t r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const pde_f2 p = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+        r[e] = pack_bf2(p.x, p.y);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
+    }
+  };
+
+  int m0, n0;
+  coords(id, m0, n0);
+  setup(m0, n0);
+  issue(0, 0);
+  // The previous tile's chunks (cv), its origin and, for the GELU backward, the gelu' chunks of the
+  // next two jobs (gcur = this iteration's, loaded one iteration ahead).  The jobs of K iteration kt
+  // are chunks CPI*kt .. CPI*kt+CPI-1, issued after the k-steps 1 and 3 MFMAs (they run in their
+  // shadow); their stores are younger than the iteration's DMA, so iteration kt+1 waits with
+  // vmcnt(CPI*SPC [+ CPI aux loads]) and they drain over the next iteration.
+  uint4 cv[CH], gcur[CPI], gnxt[CPI];                 // cv: indexed with compile-time indices only
+  int pm0 = 0, pn0 = 0;
+  int jobs_left = 0;                                   // chunks of the previous tile still to store
+  for (;;) {
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
+    int buf = 0;
+    bf16x8 fa[2][TM], fb[2][TN];
+    bool stored = false;                               // the previous iteration issued jobs after its DMA
+    for (int kt = 0; kt < KT; ++kt) {
+      if (stored) wait_vm<CPI * SPC + (EPI == kGeluBwd ? CPI : 0)>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      const bool do_issue = kt + 1 < KT;
+      const int c0 = CPI * kt;
+      const bool jobs = c0 < jobs_left;                 // wave-uniform (every thread has CH chunks)
+      const int nb = buf ^ 1;
+      const uint32_t sa = lds0 + buf * STAGE, sb = sa + ABYTES;
+      uint2 bb[TB ? TN : 1];
+#pragma unroll
+      for (int j = 0; j < (TB ? TN : 1); ++j) bb[j] = add2(bbase[j], sb);
+      const uint2 ab = add2(abase, sa);
+      auto load = [&](auto S_, bf16x8* fa_, bf16x8* fb_) {
+        constexpr int S = decltype(S_)::value;
+        static_for<0, TM>([&](auto I_) {
+          constexpr int i = decltype(I_)::value;
+          fa_[i] = rd128<4096 * i + 512 * (S >> 1)>((S & 1) ? ab.y : ab.x);
+        });
+        static_for<0, TN>([&](auto J_) {
+          constexpr int j = decltype(J_)::value;
+          if constexpr (TB) fb_[j] = trpair<2048 * S>(bb[j]);
+          else fb_[j] = rd128<4096 * j + 512 * (S >> 1)>((S & 1) ? bb[0].y : bb[0].x);
+        });
+      };
+      load(std::integral_constant<int, 0>{}, fa[0], fb[0]);
+      lgkm_fence();
+      static_for<0, 4>([&](auto S_) {
+        constexpr int S = decltype(S_)::value;
+        if constexpr (S < 3) load(std::integral_constant<int, S + 1>{}, fa[(S + 1) & 1], fb[(S + 1) & 1]);
+        if constexpr (S < SPREAD) {
+          constexpr int P0 = S * LPS / SPREAD, P1 = (S + 1) * LPS / SPREAD;
+          if (do_issue) static_for<P0, P1>([&](auto P_) { issue_piece(P_, kt + 1, nb); });
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fb[S & 1][j], fa[S & 1][i], acc[i][j]);
+        if constexpr (S == 1 || S == 3) {
+          constexpr int h = S == 1 ? 0 : 1;
+          static_assert(CPI == 2, "one job after the k-step 1 and one after the k-step 3 MFMAs");
+          // the chunk index must be a compile-time constant (a runtime index puts cv in scratch): one
+          // inlined job per chunk, selected by the wave-uniform iteration number
+          if (jobs) {
+            static_for<0, CH / CPI>([&](auto K_) {
+              constexpr int c = CPI * decltype(K_)::value + h;
+              if (kt == decltype(K_)::value && c < jobs_left) job(cv[c], gcur[h], chunk_off(c, pm0, pn0));
+            });
+          }
+          if constexpr (EPI == kGeluBwd && S == 3) {
+            if (jobs) {                                // gelu' of the next iteration's jobs
+#pragma unroll
+              for (int u = 0; u < CPI; ++u) {
+                gcur[u] = gnxt[u];
+                gnxt[u] = bload16(xr, c0 + CPI + CPI + u < jobs_left ? chunk_off(c0 + CPI + CPI + u, pm0, pn0)
+                                                                     : kOOB);
+              }
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (S < 3) lgkm_fence();
+      });
+      stored = jobs;
+      buf = nb;
+    }
+    // jobs the K loop was too short for (KT < CH / CPI)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (c >= CPI * KT && c < jobs_left) {
+        uint4 gx = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (EPI == kGeluBwd) gx = bload16(xr, chunk_off(c, pm0, pn0));
+        job(cv[c], gx, chunk_off(c, pm0, pn0));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                      // every wave is done reading the stage buffers
+
+    // ---- accumulators -> bf16 LDS tile (bias and scale before the single rounding) ----
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = wn * WTN + 32 * j + 8 * g + 4 * lh;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ml = wm * WTM + 32 * i + lr;
+          const float v[4] = {(acc[i][j][4 * g] + bv[0]) * sc, (acc[i][j][4 * g + 1] + bv[1]) * sc,
+                              (acc[i][j][4 * g + 2] + bv[2]) * sc, (acc[i][j][4 * g + 3] + bv[3]) * sc};
+          *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" : "+v"(tv));
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
+      cv[c] = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+    }
+    pm0 = m0;
+    pn0 = n0;
+    jobs_left = CH;
+    if constexpr (EPI == kGeluBwd) {                   // gelu' of the first two iterations' jobs
+#pragma unroll
+      for (int u = 0; u < CPI; ++u) {
+        gcur[u] = bload16(xr, chunk_off(u, pm0, pn0));
+        gnxt[u] = bload16(xr, chunk_off(CPI + u, pm0, pn0));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                      // the LDS tile is free: the next tile's stage 0 may land
+    const int nid = id + P;
+    if (nid >= ntile) break;
+    coords(nid, m0, n0);
+    setup(m0, n0);
+    issue(0, 0);
+    id = nid;
+  }
+  // the last tile's jobs
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    uint4 gx = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (EPI == kGeluBwd) gx = c < CPI ? gcur[c] : c < 2 * CPI ? gnxt[c - CPI] : bload16(xr, chunk_off(c, pm0, pn0));
+    job(cv[c], gx, chunk_off(c, pm0, pn0));
+  }
+}
+
 // dW (bf16 [M][N] contiguous) = sum of the fp32 slabs [S][M][N]; blocks past the dW range fold the
 // bias-gradient partials [S][M] into db (bf16) the same way
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int S, int64_t mn,
@@ -646,7 +944,27 @@ template <> struct Cfg<10> { static constexpr int V = 1, TM = 2, TN = 3, WM = 4,
 template <> struct Cfg<11> { static constexpr int V = 1, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<12> { static constexpr int V = 1, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 4; };
 template <> struct Cfg<13> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4, WN = 2, NST = 3, OCC = 1, SP = 4; };
-constexpr int kNumCfg = 14;
+//   14, 15: persistent v1 (k_gemm_p) at 256x192 (as 9) and 256x256 (as 11) for fprop / dgrad; a wgrad
+//           (TA = 1), split-K or bias-gradient call with these ids runs the one-shot 9 / 11
+template <> struct Cfg<14> { static constexpr int V = 3, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+template <> struct Cfg<15> { static constexpr int V = 3, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+//   16, 17: 256x192 with ONE wave per SIMD (4 waves of 128 x 96, up to 512 VGPRs per lane): one-shot v1 (16)
+//           and persistent (17), whose registers hold a whole deferred tile (24 chunks per thread)
+template <> struct Cfg<16> { static constexpr int V = 1, TM = 4, TN = 3, WM = 2, WN = 2, NST = 2, OCC = 1, SP = 2; };
+template <> struct Cfg<17> { static constexpr int V = 3, TM = 4, TN = 3, WM = 2, WN = 2, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 18;
+
+int g_num_cu = 0;
+int num_cu() {
+  if (g_num_cu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    g_num_cu = n;
+  }
+  return g_num_cu;
+}
 
 template <int CFG, bool TA, bool TB, int EPI, bool CS>
 hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
@@ -655,7 +973,17 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 1)
+  if constexpr (C::V == 3) {
+    constexpr bool ok = !TA && !CS && EPI != kSlab;
+    if constexpr (ok) {
+      if (splits == 1 && a.c_bytes < kOOB) {
+        hipLaunchKernelGGL((k_gemm_p<C::TM, C::TN, C::WM, C::WN, C::SP, TB, EPI>), dim3(std::min(grid, num_cu())),
+                           dim3(64 * C::WM * C::WN), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<CFG == 14 ? 9 : CFG == 15 ? 11 : 16, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 1)
     hipLaunchKernelGGL((k_gemm<C::TM, C::TN, C::WM, C::WN, C::NST, C::OCC, C::SP, TA, TB, EPI, CS>), dim3(grid),
                        dim3(64 * C::WM * C::WN), 0, st, a);
   else
@@ -680,7 +1008,11 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 10: return launch_cfg<10, TA, TB, EPI, CS>(a, splits, st);
     case 11: return launch_cfg<11, TA, TB, EPI, CS>(a, splits, st);
     case 12: return launch_cfg<12, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<13, TA, TB, EPI, CS>(a, splits, st);
+    case 13: return launch_cfg<13, TA, TB, EPI, CS>(a, splits, st);
+    case 14: return launch_cfg<14, TA, TB, EPI, CS>(a, splits, st);
+    case 15: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
+    case 16: return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -693,14 +1025,15 @@ int pde_gemm_num_cfgs() { return kNumCfg; }
 void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
-                                     {256, 192}, {256, 256}, {256, 256}, {256, 128}};
+                                     {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
+                                     {256, 256}, {256, 192}, {256, 192}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
 }
 
-// See the file header for the operand conventions.  epi: 0 bf16 (+bias), 1 bias+GELU (C = pre,
-// C2 = act), 2 GELU backward (aux = pre), 3 fp32 split-K slabs (C = float [splits][M][ldc]).
+// See the file header for the operand conventions.  epi: 0 bf16 (+bias), 1 bias+GELU (C = act,
+// C2 = gelu'(pre)), 2 GELU backward (aux = gelu'(pre)), 3 fp32 split-K slabs (C = float [splits][M][ldc]).
 // colsum (wgrad only): fp32 [splits][M] bias-gradient partials.  Supported combinations:
 // (ta, tb) = (0, 0) with epi 0/1, (0, 1) with epi 0/2, (1, 1) with epi 0/3 (+colsum).
 int g_gemm_dbg = 0;   // pde_gemm_set_dbg: ablation flags of the v1 main loop (benchmarks only)
@@ -731,6 +1064,8 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   a.scale = scale;
   a.a_bytes = (uint32_t)a_bytes;
   a.b_bytes = (uint32_t)b_bytes;
+  const size_t c_bytes = (size_t)M * ldc * 2;
+  a.c_bytes = c_bytes < kOOB ? (uint32_t)c_bytes : kOOB;   // >= kOOB: cfgs 14 / 15 run the one-shot grid
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.dbg = g_gemm_dbg;
   a.kper = (((K + 63) / 64 + splits - 1) / splits) * 64;

@@ -529,14 +529,20 @@ __global__ __launch_bounds__(256) void k_sumsq_bf16(const uint4* __restrict__ g,
   if (threadIdx.x == 0) out[1 + blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
-__global__ __launch_bounds__(256) void k_sumsq_finish(float* __restrict__ out, int nparts, float scale) {
+// step_inc (nullable): the optimizer's device step count, advanced here (the launch right before the
+// optimizer's, one block) instead of by a separate ATen add kernel per step
+__global__ __launch_bounds__(256) void k_sumsq_finish(float* __restrict__ out, int nparts, float scale,
+                                                      float* __restrict__ step_inc) {
   __shared__ float sh[4];
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 256) s += out[1 + i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) * scale * scale;
+  if (threadIdx.x == 0) {
+    out[0] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) * scale * scale;
+    if (step_inc) *step_inc += 1.f;
+  }
 }
 
 // AdamW (torch semantics, decoupled decay) on fp32 master weights; writes the bf16 model copy.
@@ -804,12 +810,12 @@ hipError_t pde_embed_bwd(const void* dX, const int64_t* idx, void* dwte, void* d
   return hipGetLastError();
 }
 
-hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, hipStream_t st) {
+hipError_t pde_sumsq_bf16(const void* g, int64_t n, float scale, float* out, float* step_inc, hipStream_t st) {
   if (n % 8) return hipErrorInvalidValue;
   const int64_t n8 = n / 8;
   const int grid = grid_for(n8, 256 * 4, kSumsqMaxBlocks);
   hipLaunchKernelGGL(k_sumsq_bf16, dim3(grid), dim3(256), 0, st, (const uint4*)g, n8, out);
-  hipLaunchKernelGGL(k_sumsq_finish, dim3(1), dim3(256), 0, st, out, grid, scale);
+  hipLaunchKernelGGL(k_sumsq_finish, dim3(1), dim3(256), 0, st, out, grid, scale, step_inc);
   return hipGetLastError();
 }
 

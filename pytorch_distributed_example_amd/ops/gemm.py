@@ -2,10 +2,11 @@
 tied LM head -- the reference's ``nn.Linear`` op class (/root/reference/mnist/main.py:136-137) at
 GPT-2 shapes, with the epilogues a library GEMM cannot fuse:
 
-* ``fprop(x, w, bias, gelu)``   y = x w^T + b; with ``gelu`` the kernel writes the pre-activation
-                                AND gelu(pre) (the next projection's input) in one pass.
-* ``dgrad(dy, w, pre)``         dx = dy w; with ``pre`` the GELU backward is applied in the
-                                epilogue (dx = (dy w) * gelu'(pre)).
+* ``fprop(x, w, bias, gelu)``   y = x w^T + b; with ``gelu`` the kernel writes gelu(pre) (the next
+                                projection's input) AND gelu'(pre) (the backward's factor) in one
+                                pass; the pre-activation itself is never stored.
+* ``dgrad(dy, w, dgelu)``       dx = dy w; with ``dgelu`` the GELU backward is applied in the
+                                epilogue (dx = (dy w) * gelu'(pre), one multiply).
 * ``wgrad(dy, x, dw, db)``      dw = dy^T x (split-K over tokens, fp32 slabs, one reduction kernel
                                 that also folds the bias gradient db = sum_tokens dy, computed by
                                 the GEMM's own MFMAs against a ones fragment).
@@ -16,7 +17,10 @@ All operands stay in their natural row-major layouts (the kernel reads transpose
 Tile configurations (``gemm_tile(cfg)``): 0 = 256x192, 1 = 256x128, 2 = 128x128, 3 = 256x256,
 4 = 128x128 at two blocks per CU; 5-8 = the same tiles (256x256, 256x192, 256x128, 128x128 x2)
 on the v2 main loop (32-deep sub-stages, fragments of the next sub-stage read across the barrier);
-9-13 = v1 tiles with the next stage's LDS-DMA spread over 2 or 4 k-steps.
+9-13 = v1 tiles with the next stage's LDS-DMA spread over 2 or 4 k-steps; 14 / 15 = persistent 9 / 11
+(one block per CU walking the tiles, each tile's output stores draining under the next tile's K loop;
+fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 with one wave per
+SIMD (4 waves of 128x96), one-shot / persistent.
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -33,10 +37,11 @@ EPI_BF16, EPI_GELU, EPI_GELU_BWD, EPI_SLAB = 0, 1, 2, 3
 N_CU = 256
 _TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (128, 128),
           5: (256, 256), 6: (256, 192), 7: (256, 128), 8: (128, 128), 9: (256, 192), 10: (256, 192),
-          11: (256, 256), 12: (256, 256), 13: (256, 128)}
+          11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 192), 15: (256, 256),
+          16: (256, 192), 17: (256, 192)}
 # relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
 _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 8: 0.8, 9: 1.0, 10: 1.0, 11: 1.0,
-             12: 1.0, 13: 0.93}
+             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 0.95, 17: 0.95}
 
 # GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/):
 #   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
@@ -98,7 +103,7 @@ def _chk(t: torch.Tensor, name: str):
 
 def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
           out: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
-    """x2 [M, K] . w[N, K]^T (+ bias) -> y [M, N]; with ``gelu`` returns (pre, act)."""
+    """x2 [M, K] . w[N, K]^T (+ bias) -> y [M, N]; with ``gelu`` returns (gelu(y), gelu'(y))."""
     _chk(x2, "x")
     _chk(w, "w")
     M, K = x2.shape
@@ -106,25 +111,26 @@ def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     c = pick("fprop", M, N, K)[0] if cfg is None else cfg
     y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16) if out is None else out
     if gelu:
-        act = torch.empty_like(y)
-        kernels().gemm_bf16(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=act, bias=bias)
-        return y, act
+        dgelu = torch.empty_like(y)
+        kernels().gemm_bf16(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=dgelu, bias=bias)
+        return y, dgelu
     kernels().gemm_bf16(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c, bias=bias)
     return y
 
 
-def dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
+def dgrad(dy2: torch.Tensor, w: torch.Tensor, dgelu: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
           scale: Optional[torch.Tensor] = None):
-    """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``pre`` ([M, K]) returns dx * gelu'(pre); ``scale`` (a
-    one-element fp32 device tensor, e.g. the loss gradient) multiplies the result in the epilogue."""
+    """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``dgelu`` ([M, K], gelu'(pre) from ``fprop(gelu=True)``)
+    returns dx * dgelu; ``scale`` (a one-element fp32 device tensor, e.g. the loss gradient) multiplies
+    the result in the epilogue."""
     _chk(dy2, "dy")
     _chk(w, "w")
     M, Nk = dy2.shape                  # reduction over the weight's rows
     Kout = w.shape[1]
     c = pick("dgrad", M, Kout, Nk)[0] if cfg is None else cfg
     dx = torch.empty(M, Kout, device=dy2.device, dtype=torch.bfloat16)
-    if pre is not None:
-        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=pre)
+    if dgelu is not None:
+        kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=dgelu)
     else:
         kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_BF16, M, Kout, Nk, Nk, Kout, Kout, 1, c, scale=scale)
     return dx

@@ -83,6 +83,7 @@ class LayerNormResFn(torch.autograd.Function):
         rstd = torch.empty(N, device=x.device, dtype=torch.float32)
         kernels().ln_fwd(xc, w, b, y, mean, rstd, eps)
         ctx.save_for_backward(xc, w, b, mean, rstd)
+        ctx.set_materialize_grads(False)     # an unused residual output gets None, not an ATen zero fill
         return xc.view_as(xc), y
 
     @staticmethod
@@ -126,6 +127,7 @@ class AddLayerNormResFn(torch.autograd.Function):
         rstd = torch.empty(N, device=x.device, dtype=torch.float32)
         kernels().ln_fwd(xc, w, b, y, mean, rstd, eps, dc, s)
         ctx.save_for_backward(s, w, b, mean, rstd)
+        ctx.set_materialize_grads(False)     # the last block's residual output is unused: no zero fill
         return s, y
 
     @staticmethod
@@ -371,28 +373,29 @@ class LinearFn(torch.autograd.Function):
 
 
 class MLPFn(torch.autograd.Function):
-    """GPT-2 MLP  y = c_proj(gelu(c_fc(x)))  as two GEMMs with fused epilogues: c_fc writes the
-    pre-activation and gelu(pre) in one pass; backward runs c_proj's dgrad with the GELU backward in
-    its epilogue (no separate GELU kernels), and both wgrads with their bias gradients."""
+    """GPT-2 MLP  y = c_proj(gelu(c_fc(x)))  as two GEMMs with fused epilogues: c_fc writes gelu(pre)
+    and gelu'(pre) in one pass (the pre-activation is never stored); backward runs c_proj's dgrad with
+    the GELU backward (one multiply by the saved gelu') in its epilogue, and both wgrads with their
+    bias gradients."""
 
     @staticmethod
     def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
         C = x.shape[-1]
         x2 = _c(x.reshape(-1, C))
-        pre, act = G.fprop(x2, w_fc, b_fc, gelu=True)
+        act, dgelu = G.fprop(x2, w_fc, b_fc, gelu=True)
         y = G.fprop(act, w_proj, b_proj)
-        ctx.save_for_backward(x2, w_fc, w_proj, pre, act)
+        ctx.save_for_backward(x2, w_fc, w_proj, dgelu, act)
         ctx.biases = (b_fc, b_proj)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w_proj.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w_fc, w_proj, pre, act = ctx.saved_tensors
+        x2, w_fc, w_proj, dgelu, act = ctx.saved_tensors
         b_fc, b_proj = ctx.biases
         dy2 = _c(dy.reshape(-1, w_proj.shape[0]))
         dw_proj, db_proj = G.wgrad(dy2, act, dw=_grad_out(w_proj), db=_grad_out(b_proj), want_db=True)
-        dpre = G.dgrad(dy2, w_proj, pre=pre)                 # (dy W_proj) * gelu'(pre)
+        dpre = G.dgrad(dy2, w_proj, dgelu=dgelu)             # (dy W_proj) * gelu'(pre)
         dw_fc, db_fc = G.wgrad(dpre, x2, dw=_grad_out(w_fc), db=_grad_out(b_fc), want_db=True)
         dx = G.dgrad(dpre, w_fc).view(ctx.xshape)
         return dx, dw_fc, db_fc, dw_proj, db_proj

@@ -123,8 +123,6 @@ class _MasterBase(torch.optim.Optimizer):
             self._build()
         self._sync_grads()
         self._step += 1
-        if self.capturable:
-            self._flat["step_dev"].add_(1.0)             # stream-ordered: a graph replay counts too
         self._kernel()
         if not self.capturable:
             for p in self._all_params():
@@ -169,9 +167,14 @@ class AdamWMaster(_MasterBase):
     def _kernel(self):
         f, K = self._flat, kernels()
         clip = None
+        # capturable: the device step count advances in stream order (a graph replay counts too) --
+        # inside the grad-norm reduction's one-block finish kernel when clipping, else by an add
+        inc = f["step_dev"] if self.capturable else None
         if self.max_grad_norm is not None:
-            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"])    # deterministic: replicas never drift
+            K.sumsq_bf16(f["g"], self.grad_scale, f["sumsq"], inc)    # deterministic: replicas never drift
             clip = f["sumsq"][:1]
+        elif inc is not None:
+            inc.add_(1.0)
         g0 = self.param_groups[0]
         b1, b2 = g0["betas"]
         K.adamw_master(f["bufs"]["master"], f["p"], f["g"], f["bufs"]["exp_avg"], f["bufs"]["exp_avg_sq"], g0["lr"],

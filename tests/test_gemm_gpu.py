@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(14))
+CFGS = list(range(18))
 
 
 def rel_err(a, b):
@@ -25,10 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 14
+    assert K.gemm_num_cfgs() == 18
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
-                                                     (256, 192), (256, 256), (256, 256), (256, 128)]
+                                                     (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
+                                                     (256, 256), (256, 192), (256, 192)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -48,12 +49,13 @@ def test_fprop_bias(cfg, M, N, K):
 def test_fprop_gelu(cfg):
     M, N, K = 520, 392, 256
     x, w, b = _bf(M, K, seed=4), _bf(N, K, scale=0.06, seed=5), _bf(N, scale=0.5, seed=6)
-    pre, act = G.fprop(x, w, b, gelu=True, cfg=cfg)
-    rp = F.linear(x.float(), w.float(), b.float())
-    assert rel_err(pre, rp) < 1e-2
-    # act is gelu of the bf16-rounded pre-activation (the module's semantics)
-    assert rel_err(act, F.gelu(pre.float(), approximate="tanh")) < 1e-2
-    assert rel_err(act, F.gelu(rp, approximate="tanh")) < 2e-2
+    act, dgelu = G.fprop(x, w, b, gelu=True, cfg=cfg)
+    rp = F.linear(x.float(), w.float(), b.float()).requires_grad_()
+    ref = F.gelu(rp, approximate="tanh")
+    ref.backward(torch.ones_like(ref))
+    # gelu and gelu' of the fp32 accumulator rounded once to bf16 (the pre-activation is never stored)
+    assert rel_err(act, ref) < 2e-2
+    assert rel_err(dgelu, rp.grad) < 2e-2
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -63,11 +65,11 @@ def test_dgrad(cfg, M, N, K):
     dy, w = _bf(M, K, seed=7), _bf(K, N, scale=0.05, seed=8)
     dx = G.dgrad(dy, w, cfg=cfg)
     assert rel_err(dx, dy.float() @ w.float()) < 1e-2
-    pre = _bf(M, N, seed=9)
-    dxg = G.dgrad(dy, w, pre=pre, cfg=cfg)
-    pr = pre.float().requires_grad_()
-    F.gelu(pr, approximate="tanh").backward(dx.float())
-    assert rel_err(dxg, pr.grad) < 1e-2
+    pre = _bf(M, N, seed=9).float().requires_grad_()
+    F.gelu(pre, approximate="tanh").backward(torch.ones_like(pre))
+    dgelu = pre.grad.to(torch.bfloat16)                  # gelu'(pre) as the forward epilogue saves it
+    dxg = G.dgrad(dy, w, dgelu=dgelu, cfg=cfg)
+    assert rel_err(dxg, dx.float() * dgelu.float()) < 1e-2
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -124,3 +126,27 @@ def test_k_tail(cfg):
         dw, db = G.wgrad(dy3, x3, want_db=True, cfg=cfg, splits=2)
         assert rel_err(dw, dy3.float().t() @ x3.float()) < 1e-2
         assert rel_err(db, dy3.float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [14, 15, 17])
+@pytest.mark.parametrize("M,N,K", [(8200, 1544, 192), (4100, 3080, 1000)])
+def test_persistent_multi_tile(cfg, M, N, K):
+    """Persistent configs with more tiles than CUs (each block walks several tiles, the previous tile's
+    epilogue jobs deferred into the next K loop): ragged M / N edges, a K shorter than the deferred
+    job schedule (K = 192: leftover jobs after the K loop) and a K % 64 tail; bias, GELU and GELU
+    backward epilogues."""
+    x, w, b = _bf(M, K, seed=30), _bf(N, K, scale=0.05, seed=31), _bf(N, seed=32)
+    y = G.fprop(x, w, b, cfg=cfg)
+    rp = F.linear(x.float(), w.float(), b.float())
+    assert rel_err(y, rp) < 1e-2
+    act, dgelu = G.fprop(x, w, b, gelu=True, cfg=cfg)
+    rq = rp.clone().requires_grad_()
+    ref = F.gelu(rq, approximate="tanh")
+    ref.backward(torch.ones_like(ref))
+    assert rel_err(act, ref) < 2e-2 and rel_err(dgelu, rq.grad) < 2e-2
+    dy, w2 = _bf(M, K, seed=33), _bf(K, N, scale=0.05, seed=34)
+    dx = G.dgrad(dy, w2, cfg=cfg)
+    rd = dy.float() @ w2.float()
+    assert rel_err(dx, rd) < 1e-2
+    dxg = G.dgrad(dy, w2, dgelu=dgelu, cfg=cfg)
+    assert rel_err(dxg, rd * dgelu.float()) < 1e-2

@@ -30,7 +30,7 @@ if a.kind == "fprop":
 elif a.kind == "dgrad":
     dy, w = r(a.M, a.K), r(a.K, a.N)
     pre = r(a.M, a.N) if a.epi == "geluback" else None
-    fn = lambda: G.dgrad(dy, w, pre=pre, cfg=a.cfg)
+    fn = lambda: G.dgrad(dy, w, dgelu=pre, cfg=a.cfg)
 else:
     dy, x = r(a.K, a.M), r(a.K, a.N)
     fn = lambda: G.wgrad(dy, x, cfg=a.cfg, splits=a.splits, want_db=True)

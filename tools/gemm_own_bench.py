@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fprop,dgrad,wgrad")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--cfgs", default="0,3,4,6,9,10,11,12,13")
+    ap.add_argument("--cfgs", default="9,11,14,15,16,17")
     a = ap.parse_args()
     T = a.tokens
     CFGS = [int(c) for c in a.cfgs.split(",")]
@@ -69,7 +69,7 @@ def main():
             lib = timeit(lambda: torch.matmul(dy, w), a.iters)
             res = {}
             for cfg in CFGS:
-                res[cfg] = timeit(lambda: G.dgrad(dy, w, pre=pre, cfg=cfg), a.iters)
+                res[cfg] = timeit(lambda: G.dgrad(dy, w, dgelu=pre, cfg=cfg), a.iters)
             best = min(res, key=res.get)
             lines.append({"gemm": f"{name}.dgrad", "M": T, "N": fin, "K": out,
                           "epilogue": "gelu_bwd" if pre is not None else "none",
@@ -81,8 +81,8 @@ def main():
             dw = torch.empty(out, fin, device=dev, dtype=torch.bfloat16)
             lib = timeit(lambda: torch.matmul(dy.t(), x, out=dw), a.iters)
             res = {}
-            for cfg in CFGS:
-                for s in (1, 2, 4, 8, 16):
+            for cfg in [c for c in CFGS if c in (0, 3, 4, 6, 9, 10, 11, 12, 13, 16)]:
+                for s in (1, 2, 4, 5, 6, 7, 8, 9, 12, 16, 20):
                     if name == "lm_head" and s > 2:
                         continue
                     res[f"{cfg}/{s}"] = timeit(lambda: G.wgrad(dy, x, dw=dw, want_db=name != "lm_head", cfg=cfg,
