@@ -630,8 +630,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
   constexpr int SMEM = 2 * STAGE > TILE_BYTES ? 2 * STAGE : TILE_BYTES;
   constexpr int CPR = BN / 8, CH = BM * CPR / NT;       // 16-byte chunks per tile row / per thread
   static_assert(CH * NT == BM * CPR, "whole chunks per thread");
-  constexpr int CPI = 2, SPC = EPI == kGelu ? 2 : 1;    // deferred chunk jobs per K iteration, stores per job
-  static_assert(CH >= 2 * CPI, "the GELU-backward prefetch covers two iterations of jobs");
+  constexpr int NSTORE = CH * (EPI == kGelu ? 2 : 1);
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int t = threadIdx.x, l = t & 63, lr = l & 31, lh = l >> 5;
@@ -705,55 +704,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
   const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
   const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
 
-  // chunk c (0..CH-1) of this thread in a tile: row (t + c*NT) / CPR, 16-byte column chunk (t + c*NT) % CPR.
-  // tv is t laundered through an empty asm, so the compiler cannot hoist CH per-chunk offsets out of
-  // the tile loop (16 loop-invariant registers at 256x256 spilled)
-  int tv = t;
-  auto chunk_off = [&](int c, int tm0, int tn0) -> uint32_t {
-    const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
-    const int m = tm0 + row, n = tn0 + 8 * cc;
-    return (m < a.M && n < a.N) ? (uint32_t)(((size_t)m * a.ldc + n) * 2) : kOOB;
-  };
-  // the epilogue job of one chunk: GELU / GELU-backward math on packed float2 and SPC buffer stores
-  auto job = [&](const uint4& v, const uint4& gx, uint32_t co) {
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-    if constexpr (EPI == kBf16) {
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), cr, co, 0, 0);
-    } else if constexpr (EPI == kGelu) {
-      uint32_t ya[4], da[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        pde_f2 d;
-        const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
-        ya[e] = pack_bf2(y.x, y.y);
-        da[e] = pack_bf2(d.x, d.y);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
-    } else {
-      const uint32_t gw[4] = {gx.x, gx.y, gx.z, gx.w};
-      uint32_t r[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const pde_f2 p = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
-        r[e] = pack_bf2(p.x, p.y);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
-    }
-  };
-
   int m0, n0;
   coords(id, m0, n0);
   setup(m0, n0);
   issue(0, 0);
-  // The previous tile's chunks (cv), its origin and, for the GELU backward, the gelu' chunks of the
-  // next two jobs (gcur = this iteration's, loaded one iteration ahead).  The jobs of K iteration kt
-  // are chunks CPI*kt .. CPI*kt+CPI-1, issued after the k-steps 1 and 3 MFMAs (they run in their
-  // shadow); their stores are younger than the iteration's DMA, so iteration kt+1 waits with
-  // vmcnt(CPI*SPC [+ CPI aux loads]) and they drain over the next iteration.
-  uint4 cv[CH], gcur[CPI], gnxt[CPI];                 // cv: indexed with compile-time indices only
-  int pm0 = 0, pn0 = 0;
-  int jobs_left = 0;                                   // chunks of the previous tile still to store
+  bool pending = false;                                // the previous tile's stores are in flight
   for (;;) {
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -762,14 +717,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{0.f};
     int buf = 0;
     bf16x8 fa[2][TM], fb[2][TN];
-    bool stored = false;                               // the previous iteration issued jobs after its DMA
     for (int kt = 0; kt < KT; ++kt) {
-      if (stored) wait_vm<CPI * SPC + (EPI == kGeluBwd ? CPI : 0)>();
+      if (kt == 0 && pending) wait_vm<NSTORE>();      // stage 0 landed; the older tile's stores may fly
       else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       const bool do_issue = kt + 1 < KT;
-      const int c0 = CPI * kt;
-      const bool jobs = c0 < jobs_left;                 // wave-uniform (every thread has CH chunks)
       const int nb = buf ^ 1;
       const uint32_t sa = lds0 + buf * STAGE, sb = sa + ABYTES;
       uint2 bb[TB ? TN : 1];
@@ -802,42 +754,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fb[S & 1][j], fa[S & 1][i], acc[i][j]);
-        if constexpr (S == 1 || S == 3) {
-          constexpr int h = S == 1 ? 0 : 1;
-          static_assert(CPI == 2, "one job after the k-step 1 and one after the k-step 3 MFMAs");
-          // the chunk index must be a compile-time constant (a runtime index puts cv in scratch): one
-          // inlined job per chunk, selected by the wave-uniform iteration number
-          if (jobs) {
-            static_for<0, CH / CPI>([&](auto K_) {
-              constexpr int c = CPI * decltype(K_)::value + h;
-              if (kt == decltype(K_)::value && c < jobs_left) job(cv[c], gcur[h], chunk_off(c, pm0, pn0));
-            });
-          }
-          if constexpr (EPI == kGeluBwd && S == 3) {
-            if (jobs) {                                // gelu' of the next iteration's jobs
-#pragma unroll
-              for (int u = 0; u < CPI; ++u) {
-                gcur[u] = gnxt[u];
-                gnxt[u] = bload16(xr, c0 + CPI + CPI + u < jobs_left ? chunk_off(c0 + CPI + CPI + u, pm0, pn0)
-                                                                     : kOOB);
-              }
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
         if constexpr (S < 3) lgkm_fence();
       });
-      stored = jobs;
       buf = nb;
     }
-    // jobs the K loop was too short for (KT < CH / CPI)
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-      if (c >= CPI * KT && c < jobs_left) {
-        uint4 gx = make_uint4(0u, 0u, 0u, 0u);
-        if constexpr (EPI == kGeluBwd) gx = bload16(xr, chunk_off(c, pm0, pn0));
-        job(cv[c], gx, chunk_off(c, pm0, pn0));
-      }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                      // every wave is done reading the stage buffers
 
@@ -859,37 +779,69 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    // chunk c of this thread: tile row (t + c*NT) / CPR, 16-byte column chunk (t + c*NT) % CPR.  tv is
+    // t laundered through an empty asm per tile, so the compiler cannot hoist CH per-chunk offsets out of
+    // the tile loop (16 loop-invariant registers at 256x256 spilled)
+    int tv = t;
     asm volatile("" : "+v"(tv));
+    auto chunk_off = [&](int c, int tm0, int tn0) -> uint32_t {
+      const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
+      const int m = tm0 + row, n = tn0 + 8 * cc;
+      return (m < a.M && n < a.N) ? (uint32_t)(((size_t)m * a.ldc + n) * 2) : kOOB;
+    };
+    uint4 cv[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
       cv[c] = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
     }
-    pm0 = m0;
-    pn0 = n0;
-    jobs_left = CH;
-    if constexpr (EPI == kGeluBwd) {                   // gelu' of the first two iterations' jobs
+    uint4 gv[EPI == kGeluBwd ? CH : 1];
+    if constexpr (EPI == kGeluBwd) {
 #pragma unroll
-      for (int u = 0; u < CPI; ++u) {
-        gcur[u] = bload16(xr, chunk_off(u, pm0, pn0));
-        gnxt[u] = bload16(xr, chunk_off(CPI + u, pm0, pn0));
-      }
+      for (int c = 0; c < CH; ++c) gv[c] = bload16(xr, chunk_off(c, m0, n0));   // before the next tile's DMA
     }
+    const int tm0 = m0, tn0 = n0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                      // the LDS tile is free: the next tile's stage 0 may land
     const int nid = id + P;
-    if (nid >= ntile) break;
-    coords(nid, m0, n0);
-    setup(m0, n0);
-    issue(0, 0);
-    id = nid;
-  }
-  // the last tile's jobs
+    if (nid < ntile) {
+      coords(nid, m0, n0);
+      setup(m0, n0);
+      issue(0, 0);
+    }
+    // ---- this tile's epilogue math and stores (NSTORE buffer stores per thread, exactly) ----
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    uint4 gx = make_uint4(0u, 0u, 0u, 0u);
-    if constexpr (EPI == kGeluBwd) gx = c < CPI ? gcur[c] : c < 2 * CPI ? gnxt[c - CPI] : bload16(xr, chunk_off(c, pm0, pn0));
-    job(cv[c], gx, chunk_off(c, pm0, pn0));
+    for (int c = 0; c < CH; ++c) {
+      const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
+      const uint32_t co = chunk_off(c, tm0, tn0);
+      if constexpr (EPI == kBf16) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
+      } else if constexpr (EPI == kGelu) {
+        uint32_t ya[4], da[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pde_f2 d;
+          const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+          ya[e] = pack_bf2(y.x, y.y);
+          da[e] = pack_bf2(d.x, d.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
+      } else {
+        const uint32_t gw[4] = {gv[c].x, gv[c].y, gv[c].z, gv[c].w};
+        uint32_t r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const pde_f2 p = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+          r[e] = pack_bf2(p.x, p.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);                 // keep the next tile's accumulator zeroing below the stores
+    if (nid >= ntile) break;
+    id = nid;
+    pending = true;
   }
 }
 
@@ -948,11 +900,7 @@ template <> struct Cfg<13> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4,
 //           (TA = 1), split-K or bias-gradient call with these ids runs the one-shot 9 / 11
 template <> struct Cfg<14> { static constexpr int V = 3, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<15> { static constexpr int V = 3, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
-//   16, 17: 256x192 with ONE wave per SIMD (4 waves of 128 x 96, up to 512 VGPRs per lane): one-shot v1 (16)
-//           and persistent (17), whose registers hold a whole deferred tile (24 chunks per thread)
-template <> struct Cfg<16> { static constexpr int V = 1, TM = 4, TN = 3, WM = 2, WN = 2, NST = 2, OCC = 1, SP = 2; };
-template <> struct Cfg<17> { static constexpr int V = 3, TM = 4, TN = 3, WM = 2, WN = 2, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 18;
+constexpr int kNumCfg = 16;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -982,7 +930,7 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
         return hipGetLastError();
       }
     }
-    return launch_cfg<CFG == 14 ? 9 : CFG == 15 ? 11 : 16, TA, TB, EPI, CS>(a, splits, st);
+    return launch_cfg<CFG == 14 ? 9 : 11, TA, TB, EPI, CS>(a, splits, st);
   } else if constexpr (C::V == 1)
     hipLaunchKernelGGL((k_gemm<C::TM, C::TN, C::WM, C::WN, C::NST, C::OCC, C::SP, TA, TB, EPI, CS>), dim3(grid),
                        dim3(64 * C::WM * C::WN), 0, st, a);
@@ -1010,9 +958,7 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 12: return launch_cfg<12, TA, TB, EPI, CS>(a, splits, st);
     case 13: return launch_cfg<13, TA, TB, EPI, CS>(a, splits, st);
     case 14: return launch_cfg<14, TA, TB, EPI, CS>(a, splits, st);
-    case 15: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
-    case 16: return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -1026,7 +972,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                                     {256, 256}, {256, 192}, {256, 192}};
+                                     {256, 256}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];

@@ -19,8 +19,7 @@ Tile configurations (``gemm_tile(cfg)``): 0 = 256x192, 1 = 256x128, 2 = 128x128,
 on the v2 main loop (32-deep sub-stages, fragments of the next sub-stage read across the barrier);
 9-13 = v1 tiles with the next stage's LDS-DMA spread over 2 or 4 k-steps; 14 / 15 = persistent 9 / 11
 (one block per CU walking the tiles, each tile's output stores draining under the next tile's K loop;
-fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 with one wave per
-SIMD (4 waves of 128x96), one-shot / persistent.
+fprop / dgrad only -- wgrad calls with these ids run 9 / 11).
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -37,22 +36,23 @@ EPI_BF16, EPI_GELU, EPI_GELU_BWD, EPI_SLAB = 0, 1, 2, 3
 N_CU = 256
 _TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (128, 128),
           5: (256, 256), 6: (256, 192), 7: (256, 128), 8: (128, 128), 9: (256, 192), 10: (256, 192),
-          11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 192), 15: (256, 256),
-          16: (256, 192), 17: (256, 192)}
+          11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 192), 15: (256, 256)}
 # relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
 _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 8: 0.8, 9: 1.0, 10: 1.0, 11: 1.0,
-             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 0.95, 17: 0.95}
+             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99}
 
-# GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/):
+# GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/,
+# profiles/r3_gemm/):
 #   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
 #   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
 _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
-    ("fprop", 2304, 768): (9, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (11, 1),
-    ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (11, 1),
+    ("fprop", 2304, 768): (9, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (15, 1),
+    ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (15, 1),
     ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
-    ("dgrad", 3072, 768): (11, 1), ("dgrad", 768, 50304): (9, 1),
-    ("wgrad", 2304, 768): (11, 8), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (9, 4),
-    ("wgrad", 768, 3072): (9, 4), ("wgrad", 50304, 768): (11, 1),
+    ("dgrad", 3072, 768): (15, 1), ("dgrad", 768, 50304): (9, 1),
+    # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/)
+    ("wgrad", 2304, 768): (9, 7), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (9, 5),
+    ("wgrad", 768, 3072): (9, 5), ("wgrad", 50304, 768): (11, 2),
 }
 
 _SCRATCH: Dict[Tuple, torch.Tensor] = {}
