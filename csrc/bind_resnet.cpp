@@ -306,12 +306,22 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
 }
 
 // desc: int64 GPU tensor [nconv][4] = (w ptr, wt ptr, N | T << 32, C | tile0 << 32), the WtDesc table
-void conv_wtrans_batch(const at::Tensor& desc, int64_t total) {
+void conv_wtrans_batch(const at::Tensor& desc, int64_t total, const OptT& counters) {
   TORCH_CHECK(pde_conv_wtdesc_bytes() == 32, "conv_wtrans_batch: descriptor layout mismatch");
-  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 4 &&
-                  desc.is_contiguous(),
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.dim() == 2 &&
+                  desc.size(1) == 4,
               "conv_wtrans_batch: desc must be a contiguous int64 GPU tensor [nconv, 4]");
-  hip_check(pde_conv_wtrans_batch(desc.data_ptr(), (int)desc.size(0), (int)total, cur_stream()), "conv_wtrans_batch");
+  long long* ctr = nullptr;
+  int ncnt = 0;
+  if (counters.has_value()) {
+    const at::Tensor& c = *counters;
+    TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kLong && c.is_contiguous() && c.numel() <= 256,
+                "conv_wtrans_batch: counters must be a contiguous int64 GPU tensor of <= 256 elements");
+    ctr = reinterpret_cast<long long*>(c.data_ptr());
+    ncnt = (int)c.numel();
+  }
+  hip_check(pde_conv_wtrans_batch(desc.data_ptr(), (int)desc.size(0), (int)total, ctr, ncnt, cur_stream()),
+            "conv_wtrans_batch");
 }
 
 int64_t conv_wgrad_splits(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
@@ -411,7 +421,7 @@ void register_resnet(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt"), py::arg("dx"), py::arg("stride"),
         py::arg("pad"), py::arg("res") = py::none(), py::arg("ds_dy") = py::none(), py::arg("ds_w") = py::none(),
         py::arg("ds_wt") = py::none(), py::arg("wt_ready") = false);
-  m.def("conv_wtrans_batch", &conv_wtrans_batch);
+  m.def("conv_wtrans_batch", &conv_wtrans_batch, py::arg("desc"), py::arg("total"), py::arg("counters") = py::none());
   m.def("conv_wgrad_splits", &conv_wgrad_splits);
   m.def("conv_wgrad", &conv_wgrad);
 }

@@ -146,7 +146,7 @@ hipError_t pde_stem_wgrad(const void* X, const void* dY, float* part, void* dW, 
 hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, int Bn, int H, int W, int C, int N,
                           int R, int S, int stride, int pad, int OH, int OW, hipStream_t st);
 hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStream_t st);
-hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, hipStream_t st);
+hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, long long* ctr, int ncnt, hipStream_t st);
 int pde_conv_wtdesc_bytes();
 hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, const void* dy2, const void* wt2,
                           int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW,

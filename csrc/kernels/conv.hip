@@ -321,8 +321,12 @@ struct WtDesc {
   bf16_t* wt;
   int N, T, C, tile0;
 };
-__global__ __launch_bounds__(256) void k_wtrans_batch(const WtDesc* __restrict__ d, int nconv) {
+// ctr (nullable): ncnt int64 counters bumped by block 0 -- the model's BatchNorm num_batches_tracked,
+// advanced by this once-per-training-forward launch instead of an ATen add kernel
+__global__ __launch_bounds__(256) void k_wtrans_batch(const WtDesc* __restrict__ d, int nconv,
+                                                      long long* __restrict__ ctr, int ncnt) {
   const int b = blockIdx.x;
+  if (ctr && b == 0 && (int)threadIdx.x < ncnt) ctr[threadIdx.x] += 1;
   int i = 0;
   while (i + 1 < nconv && d[i + 1].tile0 <= b) ++i;
   const WtDesc& q = d[i];
@@ -1168,9 +1172,10 @@ hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStre
 }
 
 // desc: device array of nconv WtDesc (tile0 = running sum of (C/64)*(N/64)*T); total = all tiles
-hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, hipStream_t st) {
+hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, long long* ctr, int ncnt, hipStream_t st) {
+  if (ncnt > 256) return hipErrorInvalidValue;
   if (nconv < 1 || total < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_wtrans_batch, dim3(total), dim3(256), 0, st, (const WtDesc*)desc, nconv);
+  hipLaunchKernelGGL(k_wtrans_batch, dim3(total), dim3(256), 0, st, (const WtDesc*)desc, nconv, ctr, ncnt);
   return hipGetLastError();
 }
 int pde_conv_wtdesc_bytes() { return (int)sizeof(WtDesc); }

@@ -439,106 +439,179 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
 
 // Backward, one thread per POOLED cell (oh, ow, chunk) handling the 2x2 input block (2oh + i, 2ow + j):
 // an even input row / column is covered by window oh / ow only, an odd one by oh and oh + 1, so the
-// four windows {oh, oh+1} x {ow, ow+1} (4 gradient + 4 argmax loads) serve all four input elements
-// (12 loads per 4 output chunks instead of 9 per chunk gathering from each input element).  A block
-// covers rows_per_block pooled rows (2 x as many input rows) of one image.
-template <bool APPLY>
-__global__ __launch_bounds__(512) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
+// four windows {oh, oh+1} x {ow, ow+1} serve all four input elements.  A block covers RB pooled rows
+// (2 RB input rows) of one image with one thread per (column, chunk) of a row:
+//  * the RB + 1 pooled gradient / argmax rows it needs (one halo row) are staged in LDS once with
+//    16-byte loads, and the four windows of a cell are LDS reads (the first version loaded them from
+//    global memory per cell: every window 4 times, 12 dependent loads per cell);
+//  * a thread's input chunks (y) of the next one (REDUCE) or two (APPLY) row pairs are in flight while
+//    the current pair computes;
+//  * REDUCE accumulates (sum d, sum d*y), folds them over the lanes of a chunk with shuffles, then over
+//    the waves in LDS (the earlier [rows][2][C] LDS image was 8-way bank conflicted: 11 M conflict
+//    cycles / pass), and writes (sum d, rstd * (sum d*y - mean * sum d)) = (sum d, sum d*xhat).
+template <int RB, bool APPLY>
+__global__ __launch_bounds__(512, APPLY ? 2 : 4) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
                                                     const uint4* __restrict__ Y, const float* __restrict__ scale,
                                                     const float* __restrict__ shift, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ coef,
                                                     float* __restrict__ part, uint4* __restrict__ dY, int H, int W,
-                                                    int OH, int OW, int CP, int lgcp, int rows_per_block) {
-  extern __shared__ float sh[];  // REDUCE: [blockDim / CP][2][C]
-  const int n = blockIdx.y, c8 = threadIdx.x & (CP - 1), C = CP * 8;
-  float sc[8], sf[8], k0[8], k1[8], k2[8], s[8], q[8];
+                                                    int OH, int OW, int CP, int lgcp) {
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
+  const int ncell = OW * CP;                            // cells of a pooled row
+  uint4* gs = reinterpret_cast<uint4*>(bsm);           // [RB + 1][ncell] pooled gradient chunks
+  uint2* as = reinterpret_cast<uint2*>(bsm + (size_t)(RB + 1) * ncell * 16);   // [RB + 1][ncell] argmax codes
+  const int n = blockIdx.y, t = threadIdx.x, c8 = t & (CP - 1), C = CP * 8;
+  const int r0 = blockIdx.x * RB;
+  const int nrow = min(RB + 1, OH - r0);               // staged pooled rows (incl. the halo row)
+  const uint4* dimg = dP + ((size_t)n * OH + r0) * ncell;
+  const uint2* aimg = Arg + ((size_t)n * OH + r0) * ncell;
+  for (int e = t; e < nrow * ncell; e += blockDim.x) {
+    gs[e] = dimg[e];
+    as[e] = aimg[e];
+  }
+  float sc[8], sf[8], k0[APPLY ? 8 : 1], k1[APPLY ? 8 : 1], k2[APPLY ? 8 : 1];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = c8 * 8 + e;
     sc[e] = scale[c];
     sf[e] = shift[c];
-    if (APPLY) {
+    if constexpr (APPLY) {
       k0[e] = coef[c];
       k1[e] = coef[C + c];
       k2[e] = coef[2 * C + c];
-    } else {
-      k0[e] = mean[c];
-      k1[e] = rstd[c];
     }
-    s[e] = q[e] = 0.f;
   }
-  const int r0 = blockIdx.x * rows_per_block, r1 = min(OH, r0 + rows_per_block);
-  const uint4* dimg = dP + (size_t)n * OH * OW * CP;
-  const uint2* aimg = Arg + (size_t)n * OH * OW * CP;
-  for (int oh = r0; oh < r1; ++oh) {
-    for (int idx = threadIdx.x; idx < OW * CP; idx += blockDim.x) {
-      const int ow = idx >> lgcp;
-      float g[2][2][8];
-      uint2 ar[2][2];
+  const bool live = t < ncell;
+  const int cell = live ? t : 0, ow = cell >> lgcp;
+  // the thread's input chunks of a row pair (zeros past the image); the next pair's are loaded while
+  // the current one is processed
+  auto load_y = [&](int r, uint4 (&v)[2][2]) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int o = (min(oh + a, OH - 1) * OW + min(ow + b, OW - 1)) * CP + c8;
-          unpack8(dimg[o], g[a][b]);
-          ar[a][b] = aimg[o];
-        }
-      const bool aok = oh + 1 < OH, bok = ow + 1 < OW;
+      for (int j = 0; j < 2; ++j) {
+        const int ih = 2 * (r0 + r) + i, iw = 2 * ow + j;
+        v[i][j] = make_uint4(0u, 0u, 0u, 0u);
+        if (live && r0 + r < OH && ih < H && iw < W) v[i][j] = Y[((size_t)(n * H + ih) * W + iw) * CP + c8];
+      }
+  };
+  // rows PRE ahead of the one being processed are in flight (the unrolled row loop keeps only those
+  // live): 1 for REDUCE (128 VGPRs, two blocks per CU), 2 for APPLY (one block per CU)
+  constexpr int PRE = APPLY ? 2 : 1;
+  uint4 yv[RB][2][2], ycur[2][2], ynxt[2][2];
+  if constexpr (PRE == 1) {
+    load_y(0, ycur);
+    if (RB > 1) load_y(1, ynxt);
+  } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int ih = 2 * oh + i;
+    for (int r = 0; r <= PRE && r < RB; ++r) load_y(r, yv[r]);
+  }
+  __syncthreads();
+  float s[8], q[8];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int iw = 2 * ow + j;
-          if (ih >= H || iw >= W) continue;
-          const size_t yi = ((size_t)(n * H + ih) * W + iw) * CP + c8;
-          float y[8];
-          unpack8(Y[yi], y);
-          float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  const bool bok = ow + 1 < OW;
 #pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            if (a > i) continue;                       // window row oh+1 covers odd rows only
+  for (int r = 0; r < RB; ++r) {
+    const int oh = r0 + r;
+    if constexpr (PRE == 1) {
+      if (r > 0) {
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-              if (b > j) continue;
-              const bool ok = (a == 0 || aok) && (b == 0 || bok);
-              const uint32_t want = (uint32_t)((i - 2 * a + 1) * 3 + (j - 2 * b + 1));
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const uint32_t ae = ((e < 4 ? ar[a][b].x : ar[a][b].y) >> (8 * (e & 3))) & 0xffu;
-                acc[e] += (ok && ae == want) ? g[a][b][e] : 0.f;
-              }
+          for (int j = 0; j < 2; ++j) ycur[i][j] = ynxt[i][j];
+        if (r + 1 < RB) load_y(r + 1, ynxt);
+      }
+    } else {
+      if (r > 0 && r + PRE < RB) load_y(r + PRE, yv[r + PRE]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) ycur[i][j] = yv[r][i][j];
+    }
+    if (!live || oh >= OH) continue;
+    const bool aok = oh + 1 < OH;
+    uint4 g[2][2];                                     // window gradients, packed bf16
+    uint2 ar[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int rr = min(r + a, nrow - 1), oc = min(ow + b, OW - 1);
+        const int o = rr * ncell + oc * CP + c8;
+        g[a][b] = gs[o];
+        ar[a][b] = as[o];
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ih = 2 * oh + i;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int iw = 2 * ow + j;
+        if (ih >= H || iw >= W) continue;
+        float y[8];
+        unpack8(ycur[i][j], y);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (a > i) continue;                       // window row oh+1 covers odd rows only
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b > j) continue;
+            const bool ok = (a == 0 || aok) && (b == 0 || bok);
+            const uint32_t want = (uint32_t)((i - 2 * a + 1) * 3 + (j - 2 * b + 1));
+            float gv[8];
+            unpack8(g[a][b], gv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t ae = ((e < 4 ? ar[a][b].x : ar[a][b].y) >> (8 * (e & 3))) & 0xffu;
+              acc[e] += (ok && ae == want) ? gv[e] : 0.f;
             }
           }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
-            if (APPLY) {
-              acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
-            } else {
-              s[e] += d;
-              q[e] += d * (y[e] - k0[e]) * k1[e];
-            }
-          }
-          if (APPLY) dY[yi] = pack8(acc);
         }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
+          if (APPLY) {
+            acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
+          } else {
+            s[e] += d;
+            q[e] += d * y[e];                        // sum d*xhat = rstd * (sum d*y - mean * sum d), at the end
+          }
+        }
+        if (APPLY) dY[((size_t)(n * H + ih) * W + iw) * CP + c8] = pack8(acc);
       }
     }
   }
   if (!APPLY) {
-    const int rl = threadIdx.x >> lgcp, RL = blockDim.x >> lgcp;
+    // lanes l, l ^ CP, l ^ 2CP, ... hold the same channel chunk: fold them, then the waves in LDS
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      sh[(rl * 2 + 0) * C + c8 * 8 + e] = s[e];
-      sh[(rl * 2 + 1) * C + c8 * 8 + e] = q[e];
+    for (int o = 32; o >= CP; o >>= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += __shfl_xor(s[e], o, 64);
+        q[e] += __shfl_xor(q[e], o, 64);
+      }
+    __syncthreads();                                    // the staged rows are no longer read
+    float* red = reinterpret_cast<float*>(bsm);         // [waves][2][C]
+    const int w = t >> 6, l = t & 63, nw = blockDim.x >> 6;
+    if (l < CP) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(w * 2 + 0) * C + l * 8 + e] = s[e];
+        red[(w * 2 + 1) * C + l * 8 + e] = q[e];
+      }
     }
     __syncthreads();
     const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    for (int k = threadIdx.x; k < 2 * C; k += blockDim.x) {
-      const int which = k / C, c = k % C;
-      float t = 0.f;
-      for (int j = 0; j < RL; ++j) t += sh[(j * 2 + which) * C + c];
-      part[blk * 2 * C + k] = t;
+    for (int c = t; c < C; c += blockDim.x) {
+      float sd = 0.f, sdy = 0.f;
+      for (int j = 0; j < nw; ++j) {
+        sd += red[(j * 2 + 0) * C + c];
+        sdy += red[(j * 2 + 1) * C + c];
+      }
+      part[blk * 2 * C + c] = sd;
+      part[blk * 2 * C + C + c] = rstd[c] * (sdy - mean[c] * sd);
     }
   }
 }
@@ -663,17 +736,17 @@ static int bnpool_threads(int cols_cp) {
   const int iters = (cols_cp + 511) / 512;
   return ((cols_cp + iters - 1) / iters + 63) / 64 * 64;
 }
-constexpr int kBnpoolRows = 4;
+constexpr int kBnpoolRB = 4;            // pooled rows per backward block
 static int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
   return l;
 }
 
-// blocks of the backward passes: kBnpoolRows / 2 pooled rows (kBnpoolRows input rows) of one image
+// blocks of the backward passes: kBnpoolRB pooled rows (2 kBnpoolRB input rows) of one image
 int pde_bnpool_part_floats(int N, int H, int C) {
-  const int OH = (H - 1) / 2 + 1, rows = kBnpoolRows / 2;
-  const int nblk = N * ((OH + rows - 1) / rows);
+  const int OH = (H - 1) / 2 + 1;
+  const int nblk = N * ((OH + kBnpoolRB - 1) / kBnpoolRB);
   return pde_bn_part_rows(nblk) * 2 * C;
 }
 
@@ -686,18 +759,20 @@ hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift,
   return hipGetLastError();
 }
 
-// part: pde_bnpool_part_floats(N, H, C) floats; coef: 3C floats
+// part: pde_bnpool_part_floats(N, H, C) floats; coef: 3C floats.  The backward runs one thread per
+// (column, chunk) of a pooled row: OW * C / 8 <= 512 (ResNet stem: 56 * 8 = 448).
 hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const float* scale, const float* shift,
                           const void* gamma, const float* mean, const float* rstd, float* part, float* coef,
                           void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
                           hipStream_t st) {
   const int CP = C / 8;
-  if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
-  const int lg = ilog2(CP), nt = bnpool_threads(OW * CP), rows = kBnpoolRows / 2, gx = (OH + rows - 1) / rows;
-  const size_t lds = (size_t)(nt / CP) * 2 * C * sizeof(float);
-  hipLaunchKernelGGL(k_bnpool_bwd<false>, dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp, (const uint2*)arg,
-                     (const uint4*)y, scale, shift, mean, rstd, (const float*)nullptr, part, (uint4*)nullptr, H, W, OH,
-                     OW, CP, lg, rows);
+  if (C % 8 || (CP & (CP - 1)) || CP > 64 || OW * CP > 512) return hipErrorInvalidValue;
+  const int lg = ilog2(CP), nt = (OW * CP + 63) / 64 * 64, gx = (OH + kBnpoolRB - 1) / kBnpoolRB;
+  const size_t lds = (size_t)(kBnpoolRB + 1) * OW * CP * 24;      // staged gradient (16 B) + argmax (8 B) rows
+  if (lds > 65536) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB, false>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
+                     (const uint2*)arg, (const uint4*)y, scale, shift, mean, rstd, (const float*)nullptr, part,
+                     (uint4*)nullptr, H, W, OH, OW, CP, lg);
   int nblk = gx * N;
   float* pp = part;
   if (nblk > kFoldThreshold) {
@@ -709,9 +784,9 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
   }
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, pp, nblk, C, N * H * W,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
-  hipLaunchKernelGGL(k_bnpool_bwd<true>, dim3(gx, N), dim3(nt), 0, st, (const uint4*)dp, (const uint2*)arg,
-                     (const uint4*)y, scale, shift, mean, rstd, (const float*)coef, (float*)nullptr, (uint4*)dy, H, W,
-                     OH, OW, CP, lg, rows);
+  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB, true>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
+                     (const uint2*)arg, (const uint4*)y, scale, shift, mean, rstd, (const float*)coef,
+                     (float*)nullptr, (uint4*)dy, H, W, OH, OW, CP, lg);
   return hipGetLastError();
 }
 

@@ -132,13 +132,16 @@ class ResNet(tnn.Module):
         return ws
 
     def forward(self, x):
-        if self.training:
-            self._bn_counters().add_(1)
+        counted = False
         if self.training and x.is_cuda:
             ws = self._dgrad_weights()
             if all(w.is_contiguous(memory_format=torch.channels_last) and w.shape[0] % 64 == 0
                    and w.shape[1] % 64 == 0 for w in ws):
-                self.__dict__.setdefault("_wt_cache", DgradWeights()).refresh(ws)
+                # the batched dgrad-weight transpose launch also bumps the BN counters
+                self.__dict__.setdefault("_wt_cache", DgradWeights()).refresh(ws, self._bn_counters())
+                counted = True
+        if self.training and not counted:
+            self._bn_counters().add_(1)
         if self.training and x.is_cuda:
             # stem BN + ReLU + max-pool as one fused node: the 64x112x112 post-BN map is never stored
             y, stats = self.conv1(x, True)

@@ -216,7 +216,9 @@ class DgradWeights:
     def __init__(self):
         self.key = None
 
-    def refresh(self, weights):
+    def refresh(self, weights, counters=None):
+        """``counters`` (optional int64 GPU tensor): bumped by 1 inside the same launch (the model's
+        BatchNorm ``num_batches_tracked``, one ATen add kernel per step less)."""
         key = tuple((w.data_ptr(), tuple(w.shape)) for w in weights)
         if key != self.key:               # (re)built outside graph capture: the warm-up steps see it first
             dev = weights[0].device
@@ -231,7 +233,7 @@ class DgradWeights:
                 self.views.append(v)
             self.desc = torch.tensor(rows, dtype=torch.int64).to(dev)
             self.total, self.key = tile, key
-        kernels().conv_wtrans_batch(self.desc, self.total)
+        kernels().conv_wtrans_batch(self.desc, self.total, counters)
         for w, v in zip(weights, self.views):
             w._pde_wt = v
 
@@ -464,7 +466,7 @@ def bn_relu_maxpool(y, stats, bn):
     (``(partials, nblk)``) came from the convolution that produced ``y``: one fused node on the GPU."""
     C = y.shape[1]
     if (y.is_cuda and bn.training and stats is not None and y.dim() == 4 and C % 8 == 0
-            and (C // 8) & (C // 8 - 1) == 0 and C // 8 <= 64):
+            and (C // 8) & (C // 8 - 1) == 0 and C // 8 <= 64 and ((y.shape[3] - 1) // 2 + 1) * (C // 8) <= 512):
         part, nblk = stats
         return BNReluMaxPoolFn.apply(_cl(y), bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
                                      bn.eps, part, nblk)
