@@ -27,6 +27,8 @@
 // offsets (the builtin makes hipcc drain the DMA queue before each one).  exp2 is the bare
 // v_exp_f32 (inputs <= 0; no denormal fix-up), and the O rescale is skipped when no query's
 // running max grew (cdna_hip_programming.md T13 with threshold 0: exact).
+#include <type_traits>
+
 #include "pde_hip.h"
 #include "pde_bf16.h"
 #include "pde_kernels.h"
@@ -208,7 +210,8 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(const bf16_t* __restrict_
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   store_dimrows(O + (size_t)b * T * ldo + (size_t)myq * ldo + hh * HD, o0, o1, 1.f / lt, h);
-  if (h == 0) LSE[(size_t)bh * T + myq] = m * scale + __logf(lt);
+  // log-sum-exp in base-2 units of the scaled scores (what the backward's exp2 consumes directly)
+  if (h == 0) LSE[(size_t)bh * T + myq] = m * sl2 + __log2f(lt);
 }
 
 // ------------------------------------------------------------------------------------ backward
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restri
     gf[s] = ld16(dOb + (size_t)myq * ldo + 16 * s + 8 * h);
     of[s] = ld16(Ob + (size_t)myq * ldo + 16 * s + 8 * h);
   }
-  const float lse2 = LSE[(size_t)bh * T + myq] * 1.4426950408889634f;
+  const float lse2 = LSE[(size_t)bh * T + myq];        // base-2 units (k_attn_fwd)
   float dq_d = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -288,8 +291,8 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restri
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float p0 = fexp2(s0[i] * sl2 - lse2);
-        float p1 = fexp2(s1[i] * sl2 - lse2);
+        float p0 = fexp2(fmaf(s0[i], sl2, -lse2));
+        float p1 = fexp2(fmaf(s1[i], sl2, -lse2));
         if (diag) {
           p0 = key > myq ? 0.f : p0;
           p1 = key + 32 > myq ? 0.f : p1;
@@ -384,22 +387,32 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkdv(const bf16_t* __rest
           g00 = tfrag<2, 0>(gbv); g01 = tfrag<2, 1>(gbv); g10 = tfrag<3, 0>(gbv); g11 = tfrag<3, 1>(gbv);
           q00 = tfrag<2, 0>(qbv); q01 = tfrag<2, 1>(qbv); q10 = tfrag<3, 0>(qbv); q11 = tfrag<3, 1>(qbv);
         }
+        // the causal mask only matters where this wave's keys reach past the half's first query
+        // (wave-uniform): the other tiles skip the per-element compare / select
+        const bool need_mask = k0 + 31 > qbase + 32 * u;
+        auto softmax_grad = [&](auto MASK_) {
+          constexpr bool MASK = decltype(MASK_)::value;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 l4 = *reinterpret_cast<const float4*>(&Ls[32 * u + 8 * g + 4 * h]);
-          const float4 d4 = *reinterpret_cast<const float4*>(&Ds[32 * u + 8 * g + 4 * h]);
-          const float lv[4] = {l4.x * 1.4426950408889634f, l4.y * 1.4426950408889634f,
-                               l4.z * 1.4426950408889634f, l4.w * 1.4426950408889634f};
-          const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+          for (int g = 0; g < 4; ++g) {
+            const float4 l4 = *reinterpret_cast<const float4*>(&Ls[32 * u + 8 * g + 4 * h]);
+            const float4 d4 = *reinterpret_cast<const float4*>(&Ds[32 * u + 8 * g + 4 * h]);
+            const float lv[4] = {l4.x, l4.y, l4.z, l4.w};   // base-2 log-sum-exp (k_attn_fwd)
+            const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i = 4 * g + e;
-            const int q = qbase + 32 * u + 8 * g + 4 * h + e;
-            const float p = myk > q ? 0.f : fexp2(S[i] * sl2 - lv[e]);
-            S[i] = p;
-            dP[i] = p * (dP[i] - dv[e]);
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * g + e;
+              float p = fexp2(fmaf(S[i], sl2, -lv[e]));
+              if constexpr (MASK) {
+                const int q = qbase + 32 * u + 8 * g + 4 * h + e;
+                p = myk > q ? 0.f : p;
+              }
+              S[i] = p;
+              dP[i] = p * (dP[i] - dv[e]);
+            }
           }
-        }
+        };
+        if (need_mask) softmax_grad(std::true_type{});
+        else softmax_grad(std::false_type{});
         const bf16x8 p0 = frag_of<0>(S), p1 = frag_of<1>(S);
         const bf16x8 d0 = frag_of<0>(dP), d1 = frag_of<1>(dP);
         lgkm_fence();
