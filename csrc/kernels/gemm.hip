@@ -845,6 +845,204 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
   }
 }
 
+// ============================================================================ 16x16x32 main loop (fprop)
+// The same LDS images, LDS-DMA staging and epilogue as k_gemm, with v_mfma_f32_16x16x32_bf16 instead of
+// 32x32x16: equal cycles per FLOP, but the chip holds a higher clock under the smaller shape
+// (MI355X_MICROARCH.md, DVFS give-back item 7: 1.12-1.15x FLOP/s with operands re-read from LDS).
+// Wave tile (16 TM) x (16 TN); per 64-deep stage two k32-steps; a fragment is one ds_read_b128 per lane
+// (one row of the 16-row block, 16-byte k chunk l >> 4 of the k32-step; the lane -> row permutation
+// below keeps it conflict-free).  With swapped operands (D' = B^T A^T) a lane holds one row and four
+// consecutive columns of each 16x16 tile.
+// TB (dgrad: B stored [K][N]): B fragments are two ds_read_b64_tr_b16 from the [64 k][64 n] images (lane
+// 4q+p of a 16-lane group addresses k row 8g + q (+4), columns 4p..4p+3 of the 16-column block; T10),
+// columns in natural order.
+__device__ __forceinline__ uint2 tr16_lane_off(int ncol0) {
+  const int l = threadIdx.x & 63, g = l >> 4, q = (l & 15) >> 2, p = l & 3;
+  const int col = ncol0 + 4 * p, img = col >> 6, ch = (col & 63) >> 3;
+  const int o = img * 8192 + 8 * (p & 1);
+  return make_uint2(o + toff(8 * g + q, ch), o + toff(8 * g + 4 + q, ch));
+}
+
+template <int TM, int TN, int WM, int WN, int SPREAD, bool TB, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
+  constexpr int AG = BM / 8 / NW, BG = BN / 8 / NW;
+  static_assert(AG * 8 * NW == BM && BG * 8 * NW == BN, "one 8-row group per wave-instruction");
+  constexpr int LPS = AG + BG;
+  constexpr int RS = BN * 2 + 16;
+  constexpr int TILE_BYTES = BM * RS;
+  constexpr int SMEM = 2 * STAGE > TILE_BYTES ? 2 * STAGE : TILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int G = 8;
+  const int grp = id / (G * a.ntiles), r2 = id - grp * (G * a.ntiles);
+  const int gsz = min(G, a.mtiles - grp * G);
+  const int m0 = (grp * G + r2 % gsz) * BM, n0 = (r2 / gsz) * BN;
+  const int KT = (a.K + 63) >> 6;
+  const int lrow = glds_row(l);
+  uint32_t aoff[AG], boff[BG];
+  int ach[AG], bch[BG];
+#pragma unroll
+  for (int u = 0; u < AG; ++u) {
+    const int g = NW * u + w, ch = glds_chunk(l, g & 1);
+    ach[u] = 8 * ch;
+    const int m = m0 + 8 * g + lrow;
+    aoff[u] = m < a.M ? (uint32_t)(((size_t)m * a.lda + 8 * ch) * 2) : kOOB;
+  }
+#pragma unroll
+  for (int v = 0; v < BG; ++v) {
+    const int g = NW * v + w, ch = glds_chunk(l, g & 1);
+    bch[v] = 8 * ch;
+    if constexpr (!TB) {
+      const int n = n0 + 8 * g + lrow;
+      boff[v] = n < a.N ? (uint32_t)(((size_t)n * a.ldb + 8 * ch) * 2) : kOOB;
+    } else {
+      const int k = 8 * (g & 7) + lrow, n = n0 + 64 * (g >> 3) + 8 * ch;
+      boff[v] = n < a.N ? (uint32_t)(((size_t)k * a.ldb + n) * 2) : kOOB;
+    }
+  }
+  const uint32_t bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  auto issue_piece = [&](auto P_, int kt, int buf) {
+    constexpr int Pc = decltype(P_)::value;
+    const char* As = smem + buf * STAGE;
+    const int kb = kt * 64;
+    if constexpr (Pc < AG) {
+      glds16(ar, As + (NW * Pc + w) * 1024, kb + ach[Pc] < a.K ? aoff[Pc] + (uint32_t)kt * 128u : kOOB);
+    } else {
+      constexpr int V = Pc - AG;
+      glds16(br, As + ABYTES + (NW * V + w) * 1024,
+             (TB || kb + bch[V] < a.K) ? boff[V] + (uint32_t)kt * bstep : kOOB);
+    }
+  };
+  // lane base of a 16-row fragment: MFMA row q = l & 15 reads physical row pi(q) of the block, chunk
+  // (l >> 4) of k32-step 0; row block i is +2048 bytes (16 rows), k32-step 1 is +512 (chunks 4..7).
+  // pi = {0..3} -> 0..3, {4..11} -> 8..15, {12..15} -> 4..7 makes the ds_read_b128 conflict-free: its
+  // lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (and +32) then hold rows 0-7 with one chunk and
+  // rows 8-15 with the next, whose toff() swizzles (c ^ (row >> 2 & 3)) land on 16 distinct 4-bank groups
+  // (identity rows: 2-way, cdna_hip_programming.md T10)
+  const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
+  const uint32_t abase = (uint32_t)toff(wm * WTM + prow, l >> 4);
+  const uint32_t bbase = (uint32_t)toff(wn * WTN + prow, l >> 4) + ABYTES;
+  uint2 tbase[TB ? TN : 1];
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) tbase[j] = add2(tr16_lane_off(wn * WTN + 16 * j), ABYTES);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (KT > 0) {
+    static_for<0, LPS>([&](auto P_) { issue_piece(P_, 0, 0); });
+    int buf = 0;
+    bf16x8 fa[2][TM], fb[2][TN];
+    for (int kt = 0; kt < KT; ++kt) {
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      const bool do_issue = kt + 1 < KT;
+      const int nb = buf ^ 1;
+      const uint32_t st0 = lds0 + buf * STAGE, sa = st0 + abase, sb = st0 + bbase;
+      auto load = [&](auto S_, bf16x8* fa_, bf16x8* fb_) {
+        constexpr int S = decltype(S_)::value;
+        static_for<0, TM>([&](auto I_) {
+          constexpr int i = decltype(I_)::value;
+          fa_[i] = rd128<2048 * i + 512 * S>(sa);
+        });
+        static_for<0, TN>([&](auto J_) {
+          constexpr int j = decltype(J_)::value;
+          if constexpr (TB) fb_[j] = trpair<4096 * S>(add2(tbase[j], st0));
+          else fb_[j] = rd128<2048 * j + 512 * S>(sb);
+        });
+      };
+      load(std::integral_constant<int, 0>{}, fa[0], fb[0]);
+      lgkm_fence();
+      static_for<0, 2>([&](auto S_) {
+        constexpr int S = decltype(S_)::value;
+        if constexpr (S < 1) load(std::integral_constant<int, 1>{}, fa[1], fb[1]);
+        if (do_issue) {
+          constexpr int P0 = S * LPS / 2, P1 = (S + 1) * LPS / 2;
+          static_for<P0, P1>([&](auto P_) { issue_piece(P_, kt + 1, nb); });
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[S][j], fa[S][i], acc[i][j], 0, 0, 0);
+        if constexpr (S < 1) lgkm_fence();
+      });
+      buf = nb;
+    }
+  }
+  __syncthreads();
+  // ---- epilogue: accumulators -> bf16 LDS tile (bias before the single rounding) -> coalesced rows ----
+  const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+  const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+  // lane l holds MFMA row q16 (physical row prow) and MFMA columns 4 (l >> 4) .. +3 = physical columns
+  // pi(4 (l >> 4)) .. +3 (pi keeps aligned groups of 4 together)
+  const int pcol = TB ? 4 * (l >> 4) : (int)((0x4c80u >> (4 * (l >> 4))) & 0xfu);   // {0, 8, 12, 4}[l >> 4]
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WTN + 16 * j + pcol;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + 16 * i + prow;
+      const float v[4] = {(acc[i][j][0] + bv[0]) * sc, (acc[i][j][1] + bv[1]) * sc, (acc[i][j][2] + bv[2]) * sc,
+                          (acc[i][j][3] + bv[3]) * sc};
+      *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
+#pragma unroll 4
+  for (int c = t; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int m = m0 + row, n = n0 + 8 * cc;
+    if (m < a.M && n < a.N) {
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+      const size_t o = (size_t)m * a.ldc + n;
+      if constexpr (EPI == kBf16) {
+        *reinterpret_cast<uint4*>(C + o) = v;
+      } else if constexpr (EPI == kGeluBwd) {
+        const uint4 g = *reinterpret_cast<const uint4*>(a.aux + o);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, gw[4] = {g.x, g.y, g.z, g.w};
+        uint32_t r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+          r[e] = pack_bf2(pr.x, pr.y);
+        }
+        *reinterpret_cast<uint4*>(C + o) = make_uint4(r[0], r[1], r[2], r[3]);
+      } else {
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        uint32_t ya[4], da[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pde_f2 d;
+          const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+          ya[e] = pack_bf2(y.x, y.y);
+          da[e] = pack_bf2(d.x, d.y);
+        }
+        *reinterpret_cast<uint4*>(C + o) = make_uint4(ya[0], ya[1], ya[2], ya[3]);
+        *reinterpret_cast<uint4*>(a.C2 + o) = make_uint4(da[0], da[1], da[2], da[3]);
+      }
+    }
+  }
+}
+
 // dW (bf16 [M][N] contiguous) = sum of the fp32 slabs [S][M][N]; blocks past the dW range fold the
 // bias-gradient partials [S][M] into db (bf16) the same way
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int S, int64_t mn,
@@ -900,7 +1098,11 @@ template <> struct Cfg<13> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4,
 //           (TA = 1), split-K or bias-gradient call with these ids runs the one-shot 9 / 11
 template <> struct Cfg<14> { static constexpr int V = 3, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<15> { static constexpr int V = 3, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 16;
+//   16, 17: the 16x16x32 main loop (k_gemm16) at 256x192 (8 waves of 64x96) and 256x256 (8 waves of 64x128)
+//           for fprop and dgrad (bias / GELU / GELU-backward epilogues); wgrad calls with these ids run 9 / 11
+template <> struct Cfg<16> { static constexpr int V = 4, TM = 4, TN = 6, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+template <> struct Cfg<17> { static constexpr int V = 4, TM = 4, TN = 8, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 18;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -921,7 +1123,16 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 3) {
+  if constexpr (C::V == 4) {
+    if constexpr (!TA && !CS && EPI != kSlab && (TB || EPI != kGeluBwd)) {
+      if (splits == 1) {
+        hipLaunchKernelGGL((k_gemm16<C::TM, C::TN, C::WM, C::WN, C::SP, TB, EPI>), dim3(grid),
+                           dim3(64 * C::WM * C::WN), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<CFG == 16 ? 9 : 11, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 3) {
     constexpr bool ok = !TA && !CS && EPI != kSlab;
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB) {
@@ -958,7 +1169,9 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 12: return launch_cfg<12, TA, TB, EPI, CS>(a, splits, st);
     case 13: return launch_cfg<13, TA, TB, EPI, CS>(a, splits, st);
     case 14: return launch_cfg<14, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
+    case 15: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
+    case 16: return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -972,7 +1185,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                                     {256, 256}};
+                                     {256, 256}, {256, 192}, {256, 256}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];

@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(16))
+CFGS = list(range(18))
 
 
 def rel_err(a, b):
@@ -25,11 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 16
+    assert K.gemm_num_cfgs() == 18
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
                                                      (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
-                                                     (256, 256)]
+                                                     (256, 256), (256, 192), (256, 256)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -128,7 +128,7 @@ def test_k_tail(cfg):
         assert rel_err(db, dy3.float().sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [14, 15])
+@pytest.mark.parametrize("cfg", [14, 15, 16, 17])
 @pytest.mark.parametrize("M,N,K", [(8200, 1544, 192), (4100, 3080, 1000)])
 def test_persistent_multi_tile(cfg, M, N, K):
     """Persistent configs with more tiles than CUs (each block walks several tiles, a tile's stores in

@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fprop,dgrad,wgrad")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--cfgs", default="9,11,14,15")
+    ap.add_argument("--cfgs", default="9,11,14,15,16,17")
     a = ap.parse_args()
     T = a.tokens
     CFGS = [int(c) for c in a.cfgs.split(",")]
