@@ -8,7 +8,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_gemm.txt 2>&1 || { tail -40 $O/pytest_gemm.txt; exit 1; }
 tail -2 $O/pytest_gemm.txt
-timeout -k 10 300 python -u tools/gemm_own_bench.py --only fprop --out $O/gemm_fprop.jsonl > $O/gemm_fprop.log 2>&1 || { tail -20 $O/gemm_fprop.log; exit 1; }
+timeout -k 10 300 python -u tools/gemm_own_bench.py --only fprop,dgrad --out $O/gemm_fprop.jsonl > $O/gemm_fprop.log 2>&1 || { tail -20 $O/gemm_fprop.log; exit 1; }
 cut -c1-330 $O/gemm_fprop.jsonl
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -40 $O/pytest_gpu.txt; exit 1; }
 tail -2 $O/pytest_gpu.txt
