@@ -863,28 +863,37 @@ __device__ __forceinline__ uint2 tr16_lane_off(int ncol0) {
   return make_uint2(o + toff(8 * g + q, ch), o + toff(8 * g + 4 + q, ch));
 }
 
-template <int TM, int TN, int WM, int WN, int SPREAD, bool TB, int EPI>
+// TA (wgrad: A stored [K][M]): A fragments are transposed reads like TB's (rows in natural order); split-K
+// slices, fp32 slab epilogue and the bias gradient (one more MFMA against a ones fragment per k32-step,
+// k-steps shared by the WN waves) as in k_gemm.
+template <int TM, int TN, int WM, int WN, bool TA, bool TB, int EPI, bool CS>
 __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
   constexpr int AG = BM / 8 / NW, BG = BN / 8 / NW;
   static_assert(AG * 8 * NW == BM && BG * 8 * NW == BN, "one 8-row group per wave-instruction");
+  static_assert((!TA || BM % 64 == 0) && (!TB || BN % 64 == 0), "transposed operands come in 64-wide images");
   constexpr int LPS = AG + BG;
   constexpr int RS = BN * 2 + 16;
-  constexpr int TILE_BYTES = BM * RS;
-  constexpr int SMEM = 2 * STAGE > TILE_BYTES ? 2 * STAGE : TILE_BYTES;
+  constexpr int TILE_BYTES = EPI == kSlab ? 0 : BM * RS;
+  constexpr int EPI_BYTES = TILE_BYTES + (CS ? WN * BM * 4 : 0);
+  constexpr int SMEM = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w / WN, wn = w % WN;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.mtiles * a.ntiles;
+  const int split = id / ntile, rem = id - split * ntile;
   constexpr int G = 8;
-  const int grp = id / (G * a.ntiles), r2 = id - grp * (G * a.ntiles);
+  const int grp = rem / (G * a.ntiles), r2 = rem - grp * (G * a.ntiles);
   const int gsz = min(G, a.mtiles - grp * G);
-  const int m0 = (grp * G + r2 % gsz) * BM, n0 = (r2 / gsz) * BN;
-  const int KT = (a.K + 63) >> 6;
+  const int mt = grp * G + r2 % gsz, nt = r2 / gsz;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = split * a.kper;
+  const int KT = (min(a.K, kbeg + a.kper) - kbeg + 63) >> 6;
   const int lrow = glds_row(l);
   uint32_t aoff[AG], boff[BG];
   int ach[AG], bch[BG];
@@ -892,8 +901,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
   for (int u = 0; u < AG; ++u) {
     const int g = NW * u + w, ch = glds_chunk(l, g & 1);
     ach[u] = 8 * ch;
-    const int m = m0 + 8 * g + lrow;
-    aoff[u] = m < a.M ? (uint32_t)(((size_t)m * a.lda + 8 * ch) * 2) : kOOB;
+    if constexpr (!TA) {
+      const int m = m0 + 8 * g + lrow;
+      aoff[u] = m < a.M ? (uint32_t)(((size_t)m * a.lda + kbeg + 8 * ch) * 2) : kOOB;
+    } else {
+      const int k = kbeg + 8 * (g & 7) + lrow, m = m0 + 64 * (g >> 3) + 8 * ch;
+      aoff[u] = m < a.M ? (uint32_t)(((size_t)k * a.lda + m) * 2) : kOOB;
+    }
   }
 #pragma unroll
   for (int v = 0; v < BG; ++v) {
@@ -901,20 +915,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
     bch[v] = 8 * ch;
     if constexpr (!TB) {
       const int n = n0 + 8 * g + lrow;
-      boff[v] = n < a.N ? (uint32_t)(((size_t)n * a.ldb + 8 * ch) * 2) : kOOB;
+      boff[v] = n < a.N ? (uint32_t)(((size_t)n * a.ldb + kbeg + 8 * ch) * 2) : kOOB;
     } else {
-      const int k = 8 * (g & 7) + lrow, n = n0 + 64 * (g >> 3) + 8 * ch;
+      const int k = kbeg + 8 * (g & 7) + lrow, n = n0 + 64 * (g >> 3) + 8 * ch;
       boff[v] = n < a.N ? (uint32_t)(((size_t)k * a.ldb + n) * 2) : kOOB;
     }
   }
-  const uint32_t bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const uint32_t astep = TA ? (uint32_t)a.lda * 128u : 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  // K tail: a K-contiguous operand's chunks past K read zeros; a transposed operand's rows past K are past
+  // its buffer resource
   auto issue_piece = [&](auto P_, int kt, int buf) {
     constexpr int Pc = decltype(P_)::value;
     const char* As = smem + buf * STAGE;
-    const int kb = kt * 64;
+    const int kb = kbeg + kt * 64;
     if constexpr (Pc < AG) {
-      glds16(ar, As + (NW * Pc + w) * 1024, kb + ach[Pc] < a.K ? aoff[Pc] + (uint32_t)kt * 128u : kOOB);
+      glds16(ar, As + (NW * Pc + w) * 1024, (TA || kb + ach[Pc] < a.K) ? aoff[Pc] + (uint32_t)kt * astep : kOOB);
     } else {
       constexpr int V = Pc - AG;
       glds16(br, As + ABYTES + (NW * V + w) * 1024,
@@ -926,11 +942,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
   // pi = {0..3} -> 0..3, {4..11} -> 8..15, {12..15} -> 4..7 makes the ds_read_b128 conflict-free: its
   // lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (and +32) then hold rows 0-7 with one chunk and
   // rows 8-15 with the next, whose toff() swizzles (c ^ (row >> 2 & 3)) land on 16 distinct 4-bank groups
-  // (identity rows: 2-way, cdna_hip_programming.md T10)
+  // (identity rows: 2-way, cdna_hip_programming.md T10).  Transposed reads keep the natural order.
   const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
   const uint32_t abase = (uint32_t)toff(wm * WTM + prow, l >> 4);
   const uint32_t bbase = (uint32_t)toff(wn * WTN + prow, l >> 4) + ABYTES;
-  uint2 tbase[TB ? TN : 1];
+  uint2 tabase[TA ? TM : 1], tbase[TB ? TN : 1];
+  if constexpr (TA) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) tabase[i] = tr16_lane_off(wm * WTM + 16 * i);
+  }
   if constexpr (TB) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) tbase[j] = add2(tr16_lane_off(wn * WTN + 16 * j), ABYTES);
@@ -942,6 +962,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[CS ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < (CS ? TM : 1); ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool cs_on = CS && a.colsum != nullptr && nt == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3f80;
   if (KT > 0) {
     static_for<0, LPS>([&](auto P_) { issue_piece(P_, 0, 0); });
     int buf = 0;
@@ -956,7 +983,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
         constexpr int S = decltype(S_)::value;
         static_for<0, TM>([&](auto I_) {
           constexpr int i = decltype(I_)::value;
-          fa_[i] = rd128<2048 * i + 512 * S>(sa);
+          if constexpr (TA) fa_[i] = trpair<4096 * S>(add2(tabase[i], st0));
+          else fa_[i] = rd128<2048 * i + 512 * S>(sa);
         });
         static_for<0, TN>([&](auto J_) {
           constexpr int j = decltype(J_)::value;
@@ -979,65 +1007,108 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[S][j], fa[S][i], acc[i][j], 0, 0, 0);
+        if constexpr (CS) {
+          if (cs_on && (S % WN) == wn) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fa[S][i], accb[i], 0, 0, 0);
+          }
+        }
         if constexpr (S < 1) lgkm_fence();
       });
       buf = nb;
     }
   }
   __syncthreads();
-  // ---- epilogue: accumulators -> bf16 LDS tile (bias before the single rounding) -> coalesced rows ----
-  const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
-  const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
-  // lane l holds MFMA row q16 (physical row prow) and MFMA columns 4 (l >> 4) .. +3 = physical columns
-  // pi(4 (l >> 4)) .. +3 (pi keeps aligned groups of 4 together)
+  // ---- epilogue.  Lane l holds MFMA row q16 (physical row mrow) and MFMA columns 4 (l >> 4) .. +3 =
+  // physical columns pcol .. +3 (pi keeps aligned groups of 4 together) of each 16x16 tile ----
+  const int mrow = TA ? q16 : prow;
   const int pcol = TB ? 4 * (l >> 4) : (int)((0x4c80u >> (4 * (l >> 4))) & 0xfu);   // {0, 8, 12, 4}[l >> 4]
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int nl = wn * WTN + 16 * j + pcol;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+  if constexpr (EPI == kSlab) {
+    float* out = reinterpret_cast<float*>(a.C) + (size_t)split * a.M * a.ldc;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int ml = wm * WTM + 16 * i + prow;
-      const float v[4] = {(acc[i][j][0] + bv[0]) * sc, (acc[i][j][1] + bv[1]) * sc, (acc[i][j][2] + bv[2]) * sc,
-                          (acc[i][j][3] + bv[3]) * sc};
-      *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+      const int m = m0 + wm * WTM + 16 * i + mrow;
+      if (m < a.M) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WTN + 16 * j + pcol;
+          if (n < a.N)
+            *reinterpret_cast<float4*>(out + (size_t)m * a.ldc + n) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+  } else {
+    const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+    const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nl = wn * WTN + 16 * j + pcol;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = wm * WTM + 16 * i + mrow;
+        const float v[4] = {(acc[i][j][0] + bv[0]) * sc, (acc[i][j][1] + bv[1]) * sc, (acc[i][j][2] + bv[2]) * sc,
+                            (acc[i][j][3] + bv[3]) * sc};
+        *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+      }
     }
   }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
+  if constexpr (CS) {
+    // every row of the ones-MFMA output is the row sum: lanes 0..15 take their column (= A row) sum
+    if (cs_on && l < 16) {
+      float* csl = reinterpret_cast<float*>(smem + TILE_BYTES);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) csl[wn * BM + wm * WTM + 16 * i + mrow] = accb[i][0];
+    }
+  }
+  if constexpr (EPI != kSlab || CS) __syncthreads();
+  if constexpr (CS) {
+    if (cs_on && t < BM && m0 + t < a.M) {
+      const float* csl = reinterpret_cast<const float*>(smem + TILE_BYTES);
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < WN; ++q) s += csl[q * BM + t];
+      a.colsum[(size_t)split * a.M + m0 + t] = s;
+    }
+  }
+  if constexpr (EPI != kSlab) {
+    constexpr int CPR = BN / 8;
+    bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
 #pragma unroll 4
-  for (int c = t; c < BM * CPR; c += NT) {
-    const int row = c / CPR, cc = c - row * CPR;
-    const int m = m0 + row, n = n0 + 8 * cc;
-    if (m < a.M && n < a.N) {
-      const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
-      const size_t o = (size_t)m * a.ldc + n;
-      if constexpr (EPI == kBf16) {
-        *reinterpret_cast<uint4*>(C + o) = v;
-      } else if constexpr (EPI == kGeluBwd) {
-        const uint4 g = *reinterpret_cast<const uint4*>(a.aux + o);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, gw[4] = {g.x, g.y, g.z, g.w};
-        uint32_t r[4];
+    for (int c = t; c < BM * CPR; c += NT) {
+      const int row = c / CPR, cc = c - row * CPR;
+      const int m = m0 + row, n = n0 + 8 * cc;
+      if (m < a.M && n < a.N) {
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+        const size_t o = (size_t)m * a.ldc + n;
+        if constexpr (EPI == kBf16) {
+          *reinterpret_cast<uint4*>(C + o) = v;
+        } else if constexpr (EPI == kGeluBwd) {
+          const uint4 g = *reinterpret_cast<const uint4*>(a.aux + o);
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, gw[4] = {g.x, g.y, g.z, g.w};
+          uint32_t r[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
-          r[e] = pack_bf2(pr.x, pr.y);
-        }
-        *reinterpret_cast<uint4*>(C + o) = make_uint4(r[0], r[1], r[2], r[3]);
-      } else {
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        uint32_t ya[4], da[4];
+          for (int e = 0; e < 4; ++e) {
+            const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+            r[e] = pack_bf2(pr.x, pr.y);
+          }
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(r[0], r[1], r[2], r[3]);
+        } else {
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+          uint32_t ya[4], da[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pde_f2 d;
-          const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
-          ya[e] = pack_bf2(y.x, y.y);
-          da[e] = pack_bf2(d.x, d.y);
+          for (int e = 0; e < 4; ++e) {
+            pde_f2 d;
+            const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+            ya[e] = pack_bf2(y.x, y.y);
+            da[e] = pack_bf2(d.x, d.y);
+          }
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(ya[0], ya[1], ya[2], ya[3]);
+          *reinterpret_cast<uint4*>(a.C2 + o) = make_uint4(da[0], da[1], da[2], da[3]);
         }
-        *reinterpret_cast<uint4*>(C + o) = make_uint4(ya[0], ya[1], ya[2], ya[3]);
-        *reinterpret_cast<uint4*>(a.C2 + o) = make_uint4(da[0], da[1], da[2], da[3]);
       }
     }
   }
@@ -1098,8 +1169,8 @@ template <> struct Cfg<13> { static constexpr int V = 1, TM = 2, TN = 2, WM = 4,
 //           (TA = 1), split-K or bias-gradient call with these ids runs the one-shot 9 / 11
 template <> struct Cfg<14> { static constexpr int V = 3, TM = 2, TN = 3, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<15> { static constexpr int V = 3, TM = 2, TN = 4, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
-//   16, 17: the 16x16x32 main loop (k_gemm16) at 256x192 (8 waves of 64x96) and 256x256 (8 waves of 64x128)
-//           for fprop and dgrad (bias / GELU / GELU-backward epilogues); wgrad calls with these ids run 9 / 11
+//   16, 17: the 16x16x32 main loop (k_gemm16) at 256x192 (8 waves of 64x96) and 256x256 (8 waves of 64x128),
+//           every operand layout and epilogue
 template <> struct Cfg<16> { static constexpr int V = 4, TM = 4, TN = 6, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<17> { static constexpr int V = 4, TM = 4, TN = 8, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 constexpr int kNumCfg = 18;
@@ -1119,19 +1190,15 @@ int num_cu() {
 template <int CFG, bool TA, bool TB, int EPI, bool CS>
 hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   using C = Cfg<CFG>;
-  constexpr int BM = C::WM * C::TM * 32, BN = C::WN * C::TN * 32;
+  constexpr int FR = C::V == 4 ? 16 : 32;               // MFMA fragment rows (k_gemm16: 16x16 tiles)
+  constexpr int BM = C::WM * C::TM * FR, BN = C::WN * C::TN * FR;
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
   if constexpr (C::V == 4) {
-    if constexpr (!TA && !CS && EPI != kSlab && (TB || EPI != kGeluBwd)) {
-      if (splits == 1) {
-        hipLaunchKernelGGL((k_gemm16<C::TM, C::TN, C::WM, C::WN, C::SP, TB, EPI>), dim3(grid),
-                           dim3(64 * C::WM * C::WN), 0, st, a);
-        return hipGetLastError();
-      }
-    }
-    return launch_cfg<CFG == 16 ? 9 : 11, TA, TB, EPI, CS>(a, splits, st);
+    hipLaunchKernelGGL((k_gemm16<C::TM, C::TN, C::WM, C::WN, TA, TB, EPI, CS>), dim3(grid),
+                       dim3(64 * C::WM * C::WN), 0, st, a);
+    return hipGetLastError();
   } else if constexpr (C::V == 3) {
     constexpr bool ok = !TA && !CS && EPI != kSlab;
     if constexpr (ok) {

@@ -20,7 +20,7 @@ on the v2 main loop (32-deep sub-stages, fragments of the next sub-stage read ac
 9-13 = v1 tiles with the next stage's LDS-DMA spread over 2 or 4 k-steps; 14 / 15 = persistent 9 / 11
 (one block per CU walking the tiles, each tile's output stores draining under the next tile's K loop;
 fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 / 256x256 on
-v_mfma_f32_16x16x32_bf16 (fprop / dgrad; wgrad calls run 9 / 11).
+v_mfma_f32_16x16x32_bf16 (every operand layout: fprop, dgrad, split-K wgrad).
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
