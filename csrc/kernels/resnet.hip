@@ -389,15 +389,11 @@ __global__ __launch_bounds__(256) void k_maxpool3s2_bwd(const uint4* __restrict_
 // them writing 411 MB).  One block per pooled row (fwd) / per rows_per_block input rows (bwd) of one
 // image, so the row index needs no division; blockDim is a multiple of CP (a thread's channel chunk is
 // fixed) and a thread walks the row's (column, chunk) pairs.
-// A block walks RF consecutive pooled rows of one image with a fixed (column, chunk) per thread: the
-// bottom input row of pooled row oh (2oh + 1) is the top row of oh + 1, so its three chunks stay in
-// registers (6 loads per pooled row after the first instead of 9, each input row read from memory once).
-template <int RF>
 __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y, const float* __restrict__ scale,
                                                     const float* __restrict__ shift, uint4* __restrict__ P,
                                                     uint2* __restrict__ Arg, int H, int W, int OH, int OW, int CP,
                                                     int lgcp) {
-  const int n = blockIdx.y, c8 = threadIdx.x & (CP - 1), oh0 = blockIdx.x * RF;
+  const int oh = blockIdx.x, n = blockIdx.y, c8 = threadIdx.x & (CP - 1);
   float sc[8], sf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -407,56 +403,37 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
   const uint4* yimg = Y + (size_t)n * H * W * CP;
   for (int idx = threadIdx.x; idx < OW * CP; idx += blockDim.x) {
     const int ow = idx >> lgcp;
-    // post-BN values of the three window columns of one input row (bf16-rounded, as the unfused path
-    // pooled them); rows outside the image are -inf (never chosen)
-    auto row_vals = [&](int ih, float (&a)[3][8]) {
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      arg[e] = 0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if (ih < 0 || ih >= H) continue;  // uniform over the block
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const int iw = 2 * ow - 1 + kw;
-        const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const bool ok = iw >= 0 && iw < W;
         float v[8];
-        unpack8(ok ? yimg[(ih * W + iw) * CP + c8] : make_uint4(0u, 0u, 0u, 0u), v);
+        unpack8(yimg[(ih * W + min(max(iw, 0), W - 1)) * CP + c8], v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a[kw][e] = ok ? bf2f(f2bf(fmaxf(v[e] * sc[e] + sf[e], 0.f))) : -INFINITY;
+        for (int e = 0; e < 8; ++e) {
+          // the value the unfused path pooled: relu(bn(y)) rounded to bf16 (same ties, same argmax)
+          const float a = bf2f(f2bf(fmaxf(v[e] * sc[e] + sf[e], 0.f)));
+          const bool better = ok && a > best[e];
+          best[e] = better ? a : best[e];
+          arg[e] = better ? (uint32_t)(kh * 3 + kw) : arg[e];
+        }
       }
-    };
-    float top[3][8], mid[3][8], bot[3][8];
-    row_vals(2 * oh0 - 1, top);
-#pragma unroll
-    for (int r = 0; r < RF; ++r) {
-      const int oh = oh0 + r;
-      if (oh >= OH) break;
-      row_vals(2 * oh, mid);
-      row_vals(2 * oh + 1, bot);
-      float best[8];
-      uint32_t arg[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        best[e] = -INFINITY;
-        arg[e] = 0;
-      }
-      auto scan = [&](const float (&a)[3][8], int kh) {
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool better = a[kw][e] > best[e];     // first maximum in scan order, as ATen
-            best[e] = better ? a[kw][e] : best[e];
-            arg[e] = better ? (uint32_t)(kh * 3 + kw) : arg[e];
-          }
-      };
-      scan(top, 0);
-      scan(mid, 1);
-      scan(bot, 2);
-      const size_t o = ((size_t)(n * OH + oh) * OW + ow) * CP + c8;
-      P[o] = pack8(best);
-      Arg[o] = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
-                          arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) top[kw][e] = bot[kw][e];
     }
+    const size_t o = ((size_t)(n * OH + oh) * OW + ow) * CP + c8;
+    P[o] = pack8(best);
+    Arg[o] = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
+                        arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
   }
 }
 
@@ -777,9 +754,8 @@ hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift,
                           int H, int W, int OH, int OW, hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
-  constexpr int RF = 4;                                          // pooled rows per forward block
-  hipLaunchKernelGGL((k_bnpool_fwd<RF>), dim3((OH + RF - 1) / RF, N), dim3(bnpool_threads(OW * CP)), 0, st,
-                     (const uint4*)y, scale, shift, (uint4*)p, (uint2*)arg, H, W, OH, OW, CP, ilog2(CP));
+  hipLaunchKernelGGL(k_bnpool_fwd, dim3(OH, N), dim3(bnpool_threads(OW * CP)), 0, st, (const uint4*)y, scale, shift,
+                     (uint4*)p, (uint2*)arg, H, W, OH, OW, CP, ilog2(CP));
   return hipGetLastError();
 }
 

@@ -266,16 +266,11 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // softmax statistics and the dlogits come from registers -- the two-pass kernel below reads each
 // 100 KB row twice (the second time mostly from the last-level cache) for 3 row-sized transfers;
 // this one moves 2 (read + write).
-// VALU per logit (the kernel streams 1.65 GB each way at the GPT-2 shape, so the math must stay under
-// the memory time): the row max first (one max per value), then sum 2^(v log2e - M log2e) (one fma +
-// one exp2 + one add), and the gradient as p*scale = 2^(v log2e - (lse log2e - log2 scale)) (one fma +
-// one exp2); the padding mask and the target's one-hot only touch the chunks that hold them.
 template <int NJ>
 __global__ __launch_bounds__(256) void k_xent_bf16_reg(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt,
                                                        int Vp, int V, float scale, float* __restrict__ loss_rows,
                                                        int write_grad) {
-  constexpr float L2E = 1.4426950408889634f;
-  __shared__ float shm[4], shs[4], shx[4];
+  __shared__ float shm[4], shs[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint4* Lr = reinterpret_cast<uint4*>(L + (size_t)row * Vp);
   const int nch = Vp >> 3;
@@ -287,88 +282,61 @@ __global__ __launch_bounds__(256) void k_xent_bf16_reg(bf16_t* __restrict__ L, c
     const int c = tid + 256 * j;
     q[j] = c < nch ? Lr[c] : make_uint4(0u, 0u, 0u, 0u);
   }
-  // a chunk is "full" when all 8 of its columns are real vocabulary entries
-  auto full = [&](int j) { return (tid + 256 * j) * 8 + 8 <= V; };
-  float m = -INFINITY, xt = 0.f;
+  float m = -INFINITY, s = 0.f, xt = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col0 = (tid + 256 * j) * 8;
     float v[8];
     unpack8(q[j], v);
-    if (full(j)) {
+    float bm = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, v[e]);
-    } else {
+    for (int e = 0; e < 8; ++e) bm = fmaxf(bm, col0 + e < V ? v[e] : -INFINITY);
+    float bs = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, col0 + e < V ? v[e] : -INFINITY);
+    for (int e = 0; e < 8; ++e) {
+      bs += col0 + e < V ? __expf(v[e] - bm) : 0.f;
+      xt += col0 + e == t32 ? v[e] : 0.f;
     }
-    if (t32 >= col0 && t32 < col0 + 8) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xt = col0 + e == t32 ? v[e] : xt;
-    }
+    ms_combine(m, s, bm, bs);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    ms_combine(m, s, m2, s2);
     xt += __shfl_xor(xt, o, 64);
   }
+  __shared__ float shx[4];
   if (lane == 0) {
     shm[w] = m;
+    shs[w] = s;
     shx[w] = xt;
   }
   __syncthreads();
-  m = fmaxf(fmaxf(shm[0], shm[1]), fmaxf(shm[2], shm[3]));
+  m = shm[0];
+  s = shs[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) ms_combine(m, s, shm[k], shs[k]);
   xt = (shx[0] + shx[1]) + (shx[2] + shx[3]);
-  const float mL = m * L2E;
-  // re-derive the floats from the packed words in each pass (keeping 200 unpacked floats live across
-  // the reductions took 371 VGPRs)
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(q[j].x), "+v"(q[j].y), "+v"(q[j].z), "+v"(q[j].w));
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col0 = (tid + 256 * j) * 8;
-    float v[8];
-    unpack8(q[j], v);
-    if (full(j)) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += __builtin_amdgcn_exp2f(fmaf(v[e], L2E, -mL));
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += col0 + e < V ? __builtin_amdgcn_exp2f(fmaf(v[e], L2E, -mL)) : 0.f;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) shs[w] = s;
-  __syncthreads();
-  s = (shs[0] + shs[1]) + (shs[2] + shs[3]);
   const float lse = m + __logf(s);
   const bool valid = t >= 0 && t < V;
   if (tid == 0) loss_rows[row] = valid ? lse - xt : 0.f;
   if (!write_grad) return;
   const float sc = valid ? scale : 0.f;
-  // p * sc = 2^(v log2e - off): off = lse log2e - log2(sc); sc == 0 (ignored row) -> off = +inf -> 0
-  const float off = sc > 0.f ? lse * L2E - __log2f(sc) : INFINITY;
   // opaque to the optimiser: the pass-1 unpacked floats are re-derived from the packed words
-  // (2 VGPRs per 4 values) instead of being kept live across the reductions
+  // (2 VGPRs per 4 values) instead of being kept live across the reduction (248 -> fewer VGPRs)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(q[j].x), "+v"(q[j].y), "+v"(q[j].z), "+v"(q[j].w));
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int c = tid + 256 * j, col0 = c * 8;
+    const int c = tid + 256 * j;
     if (c < nch) {
       float v[8];
       unpack8(q[j], v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = __builtin_amdgcn_exp2f(fmaf(v[e], L2E, -off));
-      if (!full(j)) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = col0 + e < V ? v[e] : 0.f;
-      }
-      if (t32 >= col0 && t32 < col0 + 8) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] -= col0 + e == t32 ? sc : 0.f;
+      for (int e = 0; e < 8; ++e) {
+        const int col = c * 8 + e;
+        const float p = col < V ? __expf(v[e] - lse) : 0.f;
+        v[e] = (p - (col == t32 ? 1.f : 0.f)) * sc;
       }
       Lr[c] = pack8(v);
     }
