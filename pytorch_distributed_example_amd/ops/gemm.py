@@ -57,6 +57,21 @@ _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
     ("wgrad", 768, 3072): (9, 5), ("wgrad", 50304, 768): (11, 2),
 }
 
+
+def _env_overrides() -> None:
+    """PDE_GEMM_CFG="fprop:3072:768=15,wgrad:3072:768=9/5" replaces table entries (same-box A/B runs):
+    kind:a:b as the table keys, cfg[/splits]."""
+    import os
+    spec = os.environ.get("PDE_GEMM_CFG", "").strip()
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        key, val = item.split("=")
+        kind, a, b = key.split(":")
+        cfg, _, sp = val.partition("/")
+        _CFG[(kind, int(a), int(b))] = (int(cfg), int(sp) if sp else 1)
+
+
+_env_overrides()
+
 _SCRATCH: Dict[Tuple, torch.Tensor] = {}
 
 
