@@ -48,7 +48,7 @@ _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 
 #   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
 #   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
 _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
-    ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (17, 1),
+    ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (15, 1),
     ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (15, 1),
     ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
     ("dgrad", 3072, 768): (15, 1), ("dgrad", 768, 50304): (9, 1),
