@@ -471,12 +471,10 @@ __global__ __launch_bounds__(256) void k_embed_bwd_tok(const bf16_t* __restrict_
   const int64_t tok = idx[row];
   if (lane == 0) touched[tok] = 1;
   float* a = acc + (size_t)tok * C;
-  for (int c = lane; c < (C >> 2); c += 64) {
-    float x[4];
-    unpack4(reinterpret_cast<const uint2*>(dX + (size_t)row * C)[c], x);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) atomicAdd(a + 4 * c + e, x[e]);
-  }
+  // one float per lane and instruction, lanes on consecutive addresses: every atomic wave-instruction
+  // adds 256 contiguous bytes (full atomic rate; the 4-values-per-lane form hit 16-byte strides)
+  const bf16_t* x = dX + (size_t)row * C;
+  for (int c = lane; c < C; c += 64) atomicAdd(a + c, bf2f(x[c]));
 }
 
 // dwte[v] += acc[v] for touched rows; resets acc / touched for the next step (no memset needed)
