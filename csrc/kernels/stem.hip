@@ -169,12 +169,21 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const bf16_t* __restrict__ X, 
 // [block][64][147] are summed by k_stem_wgrad_reduce into the bf16 gradient.
 // =================================================================================================
 constexpr int kSWRows = 28;              // output rows per wgrad block
-constexpr int kSPixStride = 120;         // bf16 per dY^T row (112 pixels + pad; 240 B)
+constexpr int kSPixStride = 160;         // bf16 per dY^T row (128 swizzled pixels + pad; 320 B)
+
+// dY^T byte offset of (channel, pixel): the 8-pixel group index is XORed with (ch >> 3) & 7.  With the
+// 320-B row stride both the transposed 2-byte stores (lanes = 8 pixels x 8 channel octets) and the
+// 16-byte A-fragment reads (lanes = 32 channels at one pixel octet) hit distinct banks; the plain
+// 240-B layout put every channel octet of a store on one bank (16-way, 45 M conflict cycles per
+// dispatch in the round-2 counters).
+__device__ __forceinline__ int dyt_off(int ch, int px) {
+  return (ch * kSPixStride + ((((px >> 3) ^ ((ch >> 3) & 7)) << 3) | (px & 7))) * 2;
+}
 
 __global__ __launch_bounds__(256) void k_stem_wgrad(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                                                     float* __restrict__ part, int H, int Wd, int OH, int OW) {
   __shared__ __attribute__((aligned(16))) char smem[kSC * kSPixStride * 2 + 7 * kSInCols * 8];
-  char* dyt = smem;                                          // [64][120] bf16
+  char* dyt = smem;                                          // [64][160] bf16 (swizzled)
   char* xin = smem + kSC * kSPixStride * 2;                  // [7][230][4] bf16
   const int t = threadIdx.x, l = t & 63, w = t >> 6, g = l >> 5, i32 = l & 31;
   const int rblocks = (OH + kSWRows - 1) / kSWRows;
@@ -224,8 +233,8 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const bf16_t* __restrict__ X
         const uint32_t wv[4] = {pf_dy[j].x, pf_dy[j].y, pf_dy[j].z, pf_dy[j].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          *reinterpret_cast<bf16_t*>(dyt + ((c8 * 8 + 2 * k) * kSPixStride + px) * 2) = (bf16_t)(wv[k] & 0xffffu);
-          *reinterpret_cast<bf16_t*>(dyt + ((c8 * 8 + 2 * k + 1) * kSPixStride + px) * 2) = (bf16_t)(wv[k] >> 16);
+          *reinterpret_cast<bf16_t*>(dyt + dyt_off(c8 * 8 + 2 * k, px)) = (bf16_t)(wv[k] & 0xffffu);
+          *reinterpret_cast<bf16_t*>(dyt + dyt_off(c8 * 8 + 2 * k + 1, px)) = (bf16_t)(wv[k] >> 16);
         }
       }
     }
@@ -238,8 +247,8 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const bf16_t* __restrict__ X
     if (oh + 1 < oh_hi) prefetch(oh + 1);
     for (int s16 = 0; s16 < npix16; ++s16) {
       const int p0 = 16 * s16 + 8 * g;                       // this lane group's 8 pixels
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dyt + (i32 * kSPixStride + p0) * 2);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dyt + ((i32 + 32) * kSPixStride + p0) * 2);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dyt + dyt_off(i32, p0));
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dyt + dyt_off(i32 + 32, p0));
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         if (a < ntl) {
