@@ -147,15 +147,18 @@ void check_pool_shapes(const at::Tensor& y, const at::Tensor& p, const at::Tenso
   TORCH_CHECK(y.numel() * 2 < (int64_t(1) << 31), "bnpool: y must be < 2 GiB");
 }
 
-int64_t bnpool_part_floats(int64_t N, int64_t H, int64_t C) { return pde_bnpool_part_floats((int)N, (int)H, (int)C); }
+int64_t bnpool_part_floats(int64_t N, int64_t H, int64_t W, int64_t C) {
+  return pde_bnpool_part_floats((int)N, (int)H, (int)W, (int)C);
+}
 
 // training forward: batch statistics from the conv-epilogue partials (part, pre_nblk), running-stat
-// update, then the fused BN-apply + ReLU + max-pool pass writing pooled + argmax
+// update, then the fused BN-apply + ReLU + max-pool pass writing pooled, argmax and y at the argmax
 void bnpool_fwd(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta, double eps, double momentum,
                 const at::Tensor& run_mean, const at::Tensor& run_var, const at::Tensor& part, int64_t pre_nblk,
                 const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift,
-                const at::Tensor& pooled, const at::Tensor& arg) {
+                const at::Tensor& pooled, const at::Tensor& arg, const at::Tensor& ysel) {
   check_pool_shapes(y, pooled, arg);
+  check_same(pooled, ysel, "ysel");
   const int64_t M = nhwc_rows(y, "y"), C = y.size(1);
   check_cuda(gamma, "gamma", BF16, C);
   check_cuda(beta, "beta", BF16, C);
@@ -169,25 +172,28 @@ void bnpool_fwd(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& 
                        ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), 1, 1, (int)pre_nblk, cur_stream()),
             "bnpool_fwd (finalize)");
   hip_check(pde_bnpool_fwd(y.data_ptr(), ptr<float>(scale), ptr<float>(shift), pooled.data_ptr(), arg.data_ptr(),
-                           (int)y.size(0), (int)C, (int)y.size(2), (int)y.size(3), (int)pooled.size(2),
+                           ysel.data_ptr(), (int)y.size(0), (int)C, (int)y.size(2), (int)y.size(3), (int)pooled.size(2),
                            (int)pooled.size(3), cur_stream()),
             "bnpool_fwd");
 }
 
-void bnpool_bwd(const at::Tensor& dp, const at::Tensor& arg, const at::Tensor& y, const at::Tensor& gamma,
+void bnpool_bwd(const at::Tensor& dp, const at::Tensor& arg, const at::Tensor& y, const at::Tensor& ysel,
+                const at::Tensor& gamma,
                 const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift,
                 const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dgamma, const at::Tensor& dbeta,
                 const at::Tensor& dy) {
   check_pool_shapes(y, dp, arg);
   check_same(y, dy, "dy");
+  check_same(dp, ysel, "ysel");
   const int64_t C = y.size(1);
   check_cuda(gamma, "gamma", BF16, C);
   for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
-  check_cuda(part, "part", F32, bnpool_part_floats(y.size(0), y.size(2), C));
+  check_cuda(part, "part", F32, bnpool_part_floats(y.size(0), y.size(2), y.size(3), C));
   check_cuda(coef, "coef", F32, 3 * C);
   check_cuda(dgamma, "dgamma", BF16, C);
   check_cuda(dbeta, "dbeta", BF16, C);
-  hip_check(pde_bnpool_bwd(dp.data_ptr(), arg.data_ptr(), y.data_ptr(), ptr<float>(scale), ptr<float>(shift),
+  hip_check(pde_bnpool_bwd(dp.data_ptr(), arg.data_ptr(), y.data_ptr(), ysel.data_ptr(), ptr<float>(scale),
+                           ptr<float>(shift),
                            gamma.data_ptr(), ptr<float>(mean), ptr<float>(rstd), ptr<float>(part), ptr<float>(coef),
                            dgamma.data_ptr(), dbeta.data_ptr(), dy.data_ptr(), (int)y.size(0), (int)C, (int)y.size(2),
                            (int)y.size(3), (int)dp.size(2), (int)dp.size(3), cur_stream()),

@@ -186,12 +186,12 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, const float* scale, const float* shift, float* part, float* coef,
                       void* dgamma, void* dbeta, void* dx, void* dres, int relu, hipStream_t st);
-int pde_bnpool_part_floats(int N, int H, int C);
-hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, int N, int C,
-                          int H, int W, int OH, int OW, hipStream_t st);
-hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const float* scale, const float* shift,
-                          const void* gamma, const float* mean, const float* rstd, float* part, float* coef,
-                          void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
+int pde_bnpool_part_floats(int N, int H, int W, int C);
+hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, void* ysel,
+                          int N, int C, int H, int W, int OH, int OW, hipStream_t st);
+hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const void* ysel, const float* scale,
+                          const float* shift, const void* gamma, const float* mean, const float* rstd, float* part,
+                          float* coef, void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
                           hipStream_t st);
 hipError_t pde_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int C, int H, int W, int OH, int OW,
                               hipStream_t st);

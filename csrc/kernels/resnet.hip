@@ -391,8 +391,8 @@ __global__ __launch_bounds__(256) void k_maxpool3s2_bwd(const uint4* __restrict_
 // fixed) and a thread walks the row's (column, chunk) pairs.
 __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y, const float* __restrict__ scale,
                                                     const float* __restrict__ shift, uint4* __restrict__ P,
-                                                    uint2* __restrict__ Arg, int H, int W, int OH, int OW, int CP,
-                                                    int lgcp) {
+                                                    uint2* __restrict__ Arg, uint4* __restrict__ Ysel, int H, int W,
+                                                    int OH, int OW, int CP, int lgcp) {
   const int oh = blockIdx.x, n = blockIdx.y, c8 = threadIdx.x & (CP - 1);
   float sc[8], sf[8];
 #pragma unroll
@@ -403,11 +403,12 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
   const uint4* yimg = Y + (size_t)n * H * W * CP;
   for (int idx = threadIdx.x; idx < OW * CP; idx += blockDim.x) {
     const int ow = idx >> lgcp;
-    float best[8];
+    float best[8], ysel[8];
     uint32_t arg[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       best[e] = -INFINITY;
+      ysel[e] = 0.f;
       arg[e] = 0;
     }
 #pragma unroll
@@ -426,36 +427,39 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
           const float a = bf2f(f2bf(fmaxf(v[e] * sc[e] + sf[e], 0.f)));
           const bool better = ok && a > best[e];
           best[e] = better ? a : best[e];
+          ysel[e] = better ? v[e] : ysel[e];
           arg[e] = better ? (uint32_t)(kh * 3 + kw) : arg[e];
         }
       }
     }
     const size_t o = ((size_t)(n * OH + oh) * OW + ow) * CP + c8;
     P[o] = pack8(best);
+    Ysel[o] = pack8(ysel);
     Arg[o] = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
                         arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
   }
 }
 
-// Backward, one thread per POOLED cell (oh, ow, chunk) handling the 2x2 input block (2oh + i, 2ow + j):
-// an even input row / column is covered by window oh / ow only, an odd one by oh and oh + 1, so the
-// four windows {oh, oh+1} x {ow, ow+1} serve all four input elements.  A block covers RB pooled rows
-// (2 RB input rows) of one image with one thread per (column, chunk) of a row:
+// Backward.  The BN partials need only the windows: d is non-zero only where a window took its
+// maximum, so sum d = sum over windows of dP (masked by a > 0) and sum d*y = sum over windows of
+// dP * y[argmax].  The forward stores y[argmax] (Ysel, one pooled map), and the reduce pass is
+// k_bn_bwd_reduce<2> over (dP, Ysel) -- its ReLU mask ysel*scale + shift > 0 is the apply pass's mask
+// at the argmax element -- reading 2 pooled maps instead of dP, the argmax and all of y (565 -> 206 MB
+// at B = 256; the former gather pass took 200 us).
+// The apply pass, one thread per POOLED cell (oh, ow, chunk) handling the 2x2 input block
+// (2oh + i, 2ow + j): an even input row / column is covered by window oh / ow only, an odd one by oh
+// and oh + 1, so the four windows {oh, oh+1} x {ow, ow+1} serve all four input elements.  A block
+// covers RB pooled rows (2 RB input rows) of one image with one thread per (column, chunk) of a row:
 //  * the RB + 1 pooled gradient / argmax rows it needs (one halo row) are staged in LDS once with
-//    16-byte loads, and the four windows of a cell are LDS reads (the first version loaded them from
-//    global memory per cell: every window 4 times, 12 dependent loads per cell);
-//  * a thread's input chunks (y) of the next one (REDUCE) or two (APPLY) row pairs are in flight while
-//    the current pair computes;
-//  * REDUCE accumulates (sum d, sum d*y), folds them over the lanes of a chunk with shuffles, then over
-//    the waves in LDS (the earlier [rows][2][C] LDS image was 8-way bank conflicted: 11 M conflict
-//    cycles / pass), and writes (sum d, rstd * (sum d*y - mean * sum d)) = (sum d, sum d*xhat).
-template <int RB, bool APPLY>
-__global__ __launch_bounds__(512, APPLY ? 2 : 4) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
-                                                    const uint4* __restrict__ Y, const float* __restrict__ scale,
-                                                    const float* __restrict__ shift, const float* __restrict__ mean,
-                                                    const float* __restrict__ rstd, const float* __restrict__ coef,
-                                                    float* __restrict__ part, uint4* __restrict__ dY, int H, int W,
-                                                    int OH, int OW, int CP, int lgcp) {
+//    16-byte loads, and the four windows of a cell are LDS reads;
+//  * a thread's input chunks (y) of the next two row pairs are in flight while the current pair computes;
+//  * dy = A*d + B*y + Cc with d the pooling gather of dP masked by a > 0.
+template <int RB>
+__global__ __launch_bounds__(512, 2) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
+                                                       const uint4* __restrict__ Y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const float* __restrict__ coef,
+                                                       uint4* __restrict__ dY, int H, int W, int OH, int OW, int CP,
+                                                       int lgcp) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   const int ncell = OW * CP;                            // cells of a pooled row
   uint4* gs = reinterpret_cast<uint4*>(bsm);           // [RB + 1][ncell] pooled gradient chunks
@@ -469,22 +473,20 @@ __global__ __launch_bounds__(512, APPLY ? 2 : 4) void k_bnpool_bwd(const uint4* 
     gs[e] = dimg[e];
     as[e] = aimg[e];
   }
-  float sc[8], sf[8], k0[APPLY ? 8 : 1], k1[APPLY ? 8 : 1], k2[APPLY ? 8 : 1];
+  float sc[8], sf[8], k0[8], k1[8], k2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = c8 * 8 + e;
     sc[e] = scale[c];
     sf[e] = shift[c];
-    if constexpr (APPLY) {
-      k0[e] = coef[c];
-      k1[e] = coef[C + c];
-      k2[e] = coef[2 * C + c];
-    }
+    k0[e] = coef[c];
+    k1[e] = coef[C + c];
+    k2[e] = coef[2 * C + c];
   }
   const bool live = t < ncell;
   const int cell = live ? t : 0, ow = cell >> lgcp;
-  // the thread's input chunks of a row pair (zeros past the image); the next pair's are loaded while
-  // the current one is processed
+  // the thread's input chunks of a row pair (zeros past the image); the next two pairs' are loaded
+  // while the current one is processed
   auto load_y = [&](int r, uint4 (&v)[2][2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -495,40 +497,20 @@ __global__ __launch_bounds__(512, APPLY ? 2 : 4) void k_bnpool_bwd(const uint4* 
         if (live && r0 + r < OH && ih < H && iw < W) v[i][j] = Y[((size_t)(n * H + ih) * W + iw) * CP + c8];
       }
   };
-  // rows PRE ahead of the one being processed are in flight (the unrolled row loop keeps only those
-  // live): 1 for REDUCE (128 VGPRs, two blocks per CU), 2 for APPLY (one block per CU)
-  constexpr int PRE = APPLY ? 2 : 1;
-  uint4 yv[RB][2][2], ycur[2][2], ynxt[2][2];
-  if constexpr (PRE == 1) {
-    load_y(0, ycur);
-    if (RB > 1) load_y(1, ynxt);
-  } else {
+  constexpr int PRE = 2;
+  uint4 yv[RB][2][2], ycur[2][2];
 #pragma unroll
-    for (int r = 0; r <= PRE && r < RB; ++r) load_y(r, yv[r]);
-  }
+  for (int r = 0; r <= PRE && r < RB; ++r) load_y(r, yv[r]);
   __syncthreads();
-  float s[8], q[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
   const bool bok = ow + 1 < OW;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
     const int oh = r0 + r;
-    if constexpr (PRE == 1) {
-      if (r > 0) {
+    if (r > 0 && r + PRE < RB) load_y(r + PRE, yv[r + PRE]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) ycur[i][j] = ynxt[i][j];
-        if (r + 1 < RB) load_y(r + 1, ynxt);
-      }
-    } else {
-      if (r > 0 && r + PRE < RB) load_y(r + PRE, yv[r + PRE]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) ycur[i][j] = yv[r][i][j];
-    }
+      for (int j = 0; j < 2; ++j) ycur[i][j] = yv[r][i][j];
     if (!live || oh >= OH) continue;
     const bool aok = oh + 1 < OH;
     uint4 g[2][2];                                     // window gradients, packed bf16
@@ -572,46 +554,10 @@ __global__ __launch_bounds__(512, APPLY ? 2 : 4) void k_bnpool_bwd(const uint4* 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = (y[e] * sc[e] + sf[e] > 0.f) ? acc[e] : 0.f;
-          if (APPLY) {
-            acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
-          } else {
-            s[e] += d;
-            q[e] += d * y[e];                        // sum d*xhat = rstd * (sum d*y - mean * sum d), at the end
-          }
+          acc[e] = k0[e] * d + k1[e] * y[e] + k2[e];
         }
-        if (APPLY) dY[((size_t)(n * H + ih) * W + iw) * CP + c8] = pack8(acc);
+        dY[((size_t)(n * H + ih) * W + iw) * CP + c8] = pack8(acc);
       }
-    }
-  }
-  if (!APPLY) {
-    // lanes l, l ^ CP, l ^ 2CP, ... hold the same channel chunk: fold them, then the waves in LDS
-#pragma unroll
-    for (int o = 32; o >= CP; o >>= 1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s[e] += __shfl_xor(s[e], o, 64);
-        q[e] += __shfl_xor(q[e], o, 64);
-      }
-    __syncthreads();                                    // the staged rows are no longer read
-    float* red = reinterpret_cast<float*>(bsm);         // [waves][2][C]
-    const int w = t >> 6, l = t & 63, nw = blockDim.x >> 6;
-    if (l < CP) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(w * 2 + 0) * C + l * 8 + e] = s[e];
-        red[(w * 2 + 1) * C + l * 8 + e] = q[e];
-      }
-    }
-    __syncthreads();
-    const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    for (int c = t; c < C; c += blockDim.x) {
-      float sd = 0.f, sdy = 0.f;
-      for (int j = 0; j < nw; ++j) {
-        sd += red[(j * 2 + 0) * C + c];
-        sdy += red[(j * 2 + 1) * C + c];
-      }
-      part[blk * 2 * C + c] = sd;
-      part[blk * 2 * C + C + c] = rstd[c] * (sdy - mean[c] * sd);
     }
   }
 }
@@ -744,36 +690,37 @@ static int ilog2(int v) {
 }
 
 // blocks of the backward passes: kBnpoolRB pooled rows (2 kBnpoolRB input rows) of one image
-int pde_bnpool_part_floats(int N, int H, int C) {
-  const int OH = (H - 1) / 2 + 1;
-  const int nblk = N * ((OH + kBnpoolRB - 1) / kBnpoolRB);
-  return pde_bn_part_rows(nblk) * 2 * C;
+int pde_bnpool_part_floats(int N, int H, int W, int C) {
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  return pde_bn_part_rows(pde_bn_blocks(N * OH * OW, C)) * 2 * C;
 }
 
-hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, int N, int C,
-                          int H, int W, int OH, int OW, hipStream_t st) {
+hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, void* ysel,
+                          int N, int C, int H, int W, int OH, int OW, hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bnpool_fwd, dim3(OH, N), dim3(bnpool_threads(OW * CP)), 0, st, (const uint4*)y, scale, shift,
-                     (uint4*)p, (uint2*)arg, H, W, OH, OW, CP, ilog2(CP));
+                     (uint4*)p, (uint2*)arg, (uint4*)ysel, H, W, OH, OW, CP, ilog2(CP));
   return hipGetLastError();
 }
 
-// part: pde_bnpool_part_floats(N, H, C) floats; coef: 3C floats.  The backward runs one thread per
+// part: pde_bnpool_part_floats(N, H, W, C) floats; coef: 3C floats.  The apply pass runs one thread per
 // (column, chunk) of a pooled row: OW * C / 8 <= 512 (ResNet stem: 56 * 8 = 448).
-hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const float* scale, const float* shift,
-                          const void* gamma, const float* mean, const float* rstd, float* part, float* coef,
-                          void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
+hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const void* ysel, const float* scale,
+                          const float* shift, const void* gamma, const float* mean, const float* rstd, float* part,
+                          float* coef, void* dgamma, void* dbeta, void* dy, int N, int C, int H, int W, int OH, int OW,
                           hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64 || OW * CP > 512) return hipErrorInvalidValue;
   const int lg = ilog2(CP), nt = (OW * CP + 63) / 64 * 64, gx = (OH + kBnpoolRB - 1) / kBnpoolRB;
   const size_t lds = (size_t)(kBnpoolRB + 1) * OW * CP * 24;      // staged gradient (16 B) + argmax (8 B) rows
   if (lds > 65536) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB, false>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
-                     (const uint2*)arg, (const uint4*)y, scale, shift, mean, rstd, (const float*)nullptr, part,
-                     (uint4*)nullptr, H, W, OH, OW, CP, lg);
-  int nblk = gx * N;
+  // BN partials from the pooled maps: rows = pooled cells, x = y[argmax], mask x*scale + shift > 0
+  const int Mp = N * OH * OW, RP = 256 / CP;
+  int nblk = pde_bn_blocks(Mp, C);
+  hipLaunchKernelGGL(k_bn_bwd_reduce<2>, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
+                     (const uint4*)dp, (const uint4*)nullptr, (const uint4*)ysel, mean, rstd, scale, shift, Mp, C,
+                     (Mp + nblk - 1) / nblk, part);
   float* pp = part;
   if (nblk > kFoldThreshold) {
     float* folded = part + (size_t)nblk * 2 * C;
@@ -784,9 +731,9 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
   }
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, pp, nblk, C, N * H * W,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
-  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB, true>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
-                     (const uint2*)arg, (const uint4*)y, scale, shift, mean, rstd, (const float*)coef,
-                     (float*)nullptr, (uint4*)dy, H, W, OH, OW, CP, lg);
+  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
+                     (const uint2*)arg, (const uint4*)y, scale, shift, (const float*)coef, (uint4*)dy, H, W, OH, OW,
+                     CP, lg);
   return hipGetLastError();
 }
 

@@ -426,7 +426,9 @@ class BNReluMaxPoolFn(torch.autograd.Function):
     """Training-mode stem tail ``maxpool3x3s2(relu(bn(y)))`` as one autograd node over the stem conv's
     output ``y`` and its fused batch-statistics partials (``k_bnpool_*`` in csrc/kernels/resnet.hip):
     the post-BN map (the largest tensor of ResNet-18) is never written; backward recomputes the ReLU
-    mask from ``y``.  Same math, ties and argmax as BatchNormActFn followed by MaxPool3s2Fn."""
+    mask from ``y``.  The forward also keeps ``y`` at each window's argmax (one pooled map), from which
+    the backward's BN partials are summed without reading ``y``.  Same math, ties and argmax as
+    BatchNormActFn followed by MaxPool3s2Fn."""
 
     @staticmethod
     def forward(ctx, y, gamma, beta, run_mean, run_var, momentum, eps, part, pre_nblk):
@@ -437,27 +439,28 @@ class BNReluMaxPoolFn(torch.autograd.Function):
         mean, rstd, scale, shift = (torch.empty(C, device=dev, dtype=torch.float32) for _ in range(4))
         pooled = torch.empty(N, C, OH, OW, device=dev, dtype=y.dtype, memory_format=torch.channels_last)
         arg = torch.empty(pooled.numel(), device=dev, dtype=torch.uint8)
+        ysel = torch.empty_like(pooled)
         K.bnpool_fwd(y, gamma, beta, eps, momentum, run_mean, run_var, part, pre_nblk, mean, rstd, scale, shift,
-                     pooled, arg)
-        ctx.save_for_backward(y, gamma, mean, rstd, scale, shift, arg)
+                     pooled, arg, ysel)
+        ctx.save_for_backward(y, gamma, mean, rstd, scale, shift, arg, ysel)
         ctx.beta = beta
         return pooled
 
     @staticmethod
     def backward(ctx, dp):
-        y, gamma, mean, rstd, scale, shift, arg = ctx.saved_tensors
+        y, gamma, mean, rstd, scale, shift, arg, ysel = ctx.saved_tensors
         K = kernels()
-        N, C, H, _ = y.shape
+        N, C, H, W = y.shape
         dev = y.device
-        part = torch.empty(K.bnpool_part_floats(N, H, C), device=dev, dtype=torch.float32)
+        part = torch.empty(K.bnpool_part_floats(N, H, W, C), device=dev, dtype=torch.float32)
         coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
         dgamma = flat_grad_slot(gamma)
         dgamma = torch.empty(C, device=dev, dtype=gamma.dtype) if dgamma is None else dgamma
         dbeta = flat_grad_slot(ctx.beta)
         dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
         dy = torch.empty_like(y)
-        K.bnpool_bwd(dp.contiguous(memory_format=torch.channels_last), arg, y, gamma, mean, rstd, scale, shift, part,
-                     coef, dgamma, dbeta, dy)
+        K.bnpool_bwd(dp.contiguous(memory_format=torch.channels_last), arg, y, ysel, gamma, mean, rstd, scale, shift,
+                     part, coef, dgamma, dbeta, dy)
         return dy, dgamma, dbeta, None, None, None, None, None, None
 
 
