@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__
                                                        const uint4* __restrict__ X, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int M, int C,
-                                                       int rows_per_block, float* __restrict__ part) {
+                                                       int rows_per_block, float* __restrict__ part,
+                                                       uint4* __restrict__ dR) {
   extern __shared__ float sh[];
   int CP, RP;
   bn_geom(C, CP, RP);
@@ -223,7 +224,9 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint4* __restrict__
         if constexpr (RELU == 2) d = x[e] * sc[e] + sf[e] > 0.f ? d : 0.f;
         s[e] += d;
         q[e] += d * (x[e] - mu[e]) * rs[e];
+        g[e] = d;
       }
+      if (RELU == 1 && dR) dR[i] = pack8(g);   // the residual gradient IS the masked gradient
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -720,7 +723,7 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
   int nblk = pde_bn_blocks(Mp, C);
   hipLaunchKernelGGL(k_bn_bwd_reduce<2>, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st,
                      (const uint4*)dp, (const uint4*)nullptr, (const uint4*)ysel, mean, rstd, scale, shift, Mp, C,
-                     (Mp + nblk - 1) / nblk, part);
+                     (Mp + nblk - 1) / nblk, part, (uint4*)nullptr);
   float* pp = part;
   if (nblk > kFoldThreshold) {
     float* folded = part + (size_t)nblk * 2 * C;
@@ -748,12 +751,22 @@ hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C
   const int CP = C / 8, RP = 256 / CP;
   const int nblk = pde_bn_blocks(M, C);
   const int rpb = (M + nblk - 1) / nblk;
+  // ReLU after a residual add: the reduce pass writes the masked gradient as dres, and the apply pass
+  // reads it back as its (unmasked) dy -- 7 tensor passes instead of 8 (the apply no longer reads dy
+  // and y, and writes one tensor)
+  const bool res_first = relu == 1 && dres;
   auto red = relu == 0 ? k_bn_bwd_reduce<0> : relu == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>;
   hipLaunchKernelGGL(red, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)dy,
-                     (const uint4*)y, (const uint4*)x, mean, rstd, scale, shift, M, C, rpb, part);
+                     (const uint4*)y, (const uint4*)x, mean, rstd, scale, shift, M, C, rpb, part,
+                     res_first ? (uint4*)dres : (uint4*)nullptr);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
   const int64_t n8 = (int64_t)M * CP;
+  if (res_first) {
+    hipLaunchKernelGGL(k_bn_bwd_apply<0>, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dres,
+                       (const uint4*)nullptr, (const uint4*)x, coef, scale, shift, (uint4*)dx, (uint4*)nullptr, n8, C);
+    return hipGetLastError();
+  }
   auto app = relu == 0 ? k_bn_bwd_apply<0> : relu == 1 ? k_bn_bwd_apply<1> : k_bn_bwd_apply<2>;
   hipLaunchKernelGGL(app, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)dy, (const uint4*)y,
                      (const uint4*)x, coef, scale, shift, (uint4*)dx, (uint4*)dres, n8, C);
