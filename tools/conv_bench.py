@@ -3,6 +3,7 @@
 ResNet-18 conv geometry at batch 256, channels-last bf16.  Interleaved rounds in one process.
 
 usage: python tools/conv_bench.py [--batch 256] [--iters 20]
+       python tools/conv_bench.py --wgrad-sweep 0.5 1 2 3   (wgrad only: split count x factor, per depth)
 """
 import argparse
 import json
@@ -47,7 +48,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stages", type=int, nargs="+", default=[3, 2], help="LDS pipeline depths to time")
+    ap.add_argument("--wgrad-sweep", type=float, nargs="+", default=None,
+                    help="wgrad only: time split counts default x these factors at every depth")
     args = ap.parse_args()
+    if args.wgrad_sweep:
+        return wgrad_sweep(args)
     K = kernels()
     dev = "cuda"
     B = args.batch
@@ -93,6 +98,35 @@ def main():
         print(json.dumps(out), flush=True)
     print(json.dumps({"total_us_per_step_ours": round(tot["ours"], 1),
                       "total_us_per_step_miopen": round(tot["miopen"], 1)}), flush=True)
+
+
+def wgrad_sweep(args):
+    K = kernels()
+    dev = "cuda"
+    B = args.batch
+    for name, C, H, N, k, s, p, cnt in LAYERS:
+        torch.manual_seed(0)
+        x = torch.randn(B, C, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = torch.randn(N, C, k, k, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        OH = (H + 2 * p - k) // s + 1
+        dy = torch.randn(B, N, OH, OH, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dw = torch.empty_like(w)
+        s0 = K.conv_wgrad_splits(x, w, s, p)
+        flops = 2.0 * B * OH * OH * N * C * k * k
+        ref = None
+        for f in args.wgrad_sweep:
+            sp = max(1, int(round(s0 * f)))
+            part = torch.empty(sp * w.numel(), device=dev)
+            for nst in args.stages:
+                K.conv_set_stages(nst)
+                us = min(timeit(lambda: K.conv_wgrad(dy, x, w, part, sp, dw, s, p), args.iters) for _ in range(2))
+                if ref is None:
+                    ref = dw.float().clone()
+                err = ((dw.float() - ref).norm() / ref.norm()).item()
+                print(json.dumps({"layer": name, "count": cnt, "splits": sp, "default_splits": s0, "nst": nst,
+                                  "us": round(us, 1), "tflops": round(flops / us / 1e6, 1), "rel_vs_first": err}),
+                      flush=True)
+        K.conv_set_stages(2)
 
 
 if __name__ == "__main__":
