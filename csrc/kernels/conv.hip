@@ -1265,12 +1265,20 @@ int pde_conv_wgrad_splits2(int Bn, int H, int W, int C, int N, int R, int S, int
 }
 
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C) {
-  // ~2 blocks per CU in total and >= 16 pixel stages per block: enough parallelism without
-  // making the fp32 slab round trip (splits x N x T*C x 4 B, written and re-read) dominate.
+  // At most one round of co-resident blocks (2 per CU) and >= 16 pixel stages per block: enough
+  // parallelism without making the fp32 slab round trip (splits x N x T*C x 4 B, written and re-read)
+  // dominate.  Rounded DOWN: the former ceil(512 / tiles) launched 513-576 blocks for the 3x3 convs of
+  // layers 2-4, and the few blocks past the first round ran as a tail of a whole block's duration
+  // (tools/conv_bench.py --wgrad-blocks: l3 3x3 109.5 -> 76.7 us, l2.0 conv1 72.7 -> 50.4 us;
+  // profiles/r3_models/wgrad_blocks_sweep.jsonl).
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+    ncu = 256;
   const int P = Bn * OH * OW, stages = (P + 63) / 64;
   const int BM = N % 128 == 0 ? 128 : 64, BN = 128;
   const int tiles = (N / BM) * ((T * C + BN - 1) / BN);
-  int splits = (512 + tiles - 1) / tiles;
+  int splits = 2 * ncu / tiles;
   splits = min(splits, stages / 16);
   return max(1, splits);
 }

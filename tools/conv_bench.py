@@ -50,8 +50,10 @@ def main():
     ap.add_argument("--stages", type=int, nargs="+", default=[3, 2], help="LDS pipeline depths to time")
     ap.add_argument("--wgrad-sweep", type=float, nargs="+", default=None,
                     help="wgrad only: time split counts default x these factors at every depth")
+    ap.add_argument("--wgrad-blocks", type=float, nargs="+", default=None,
+                    help="with --wgrad-sweep: split counts floor(k * 512 / tiles) for these k instead")
     args = ap.parse_args()
-    if args.wgrad_sweep:
+    if args.wgrad_sweep or args.wgrad_blocks:
         return wgrad_sweep(args)
     K = kernels()
     dev = "cuda"
@@ -114,8 +116,13 @@ def wgrad_sweep(args):
         s0 = K.conv_wgrad_splits(x, w, s, p)
         flops = 2.0 * B * OH * OH * N * C * k * k
         ref = None
-        for f in args.wgrad_sweep:
-            sp = max(1, int(round(s0 * f)))
+        BM = 128 if N % 128 == 0 else 64
+        tiles = (N // BM) * ((k * k * C + 127) // 128)
+        if args.wgrad_blocks:
+            cands = sorted({s0} | {max(1, int(f * 512) // tiles) for f in args.wgrad_blocks})
+        else:
+            cands = [max(1, int(round(s0 * f))) for f in args.wgrad_sweep]
+        for sp in cands:
             part = torch.empty(sp * w.numel(), device=dev)
             for nst in args.stages:
                 K.conv_set_stages(nst)
@@ -124,6 +131,7 @@ def wgrad_sweep(args):
                     ref = dw.float().clone()
                 err = ((dw.float() - ref).norm() / ref.norm()).item()
                 print(json.dumps({"layer": name, "count": cnt, "splits": sp, "default_splits": s0, "nst": nst,
+                                  "blocks": sp * tiles,
                                   "us": round(us, 1), "tflops": round(flops / us / 1e6, 1), "rel_vs_first": err}),
                       flush=True)
         K.conv_set_stages(2)
