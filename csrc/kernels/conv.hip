@@ -108,8 +108,10 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
-  const int per_phase = a.mtiles * a.ntiles;
-  const int phz = id / per_phase, rem = id % per_phase;
+  // phases interleaved in the block id: each XCD (a contiguous id range, xcd_remap) gets an equal share
+  // of every phase.  Phase-major ids gave the 4-tap phase of a stride-2 dgrad (1, 2, 2, 4 taps) to
+  // XCDs 6-7 alone, which then ran ~1.6x the balanced time.
+  const int phz = id % a.nphase, rem = id / a.nphase;
   const int mt = rem / a.ntiles, nt = rem % a.ntiles;
   const Phase& P = a.phase[phz];
   const int Mq = a.Bn * P.Hq * P.Wq;
