@@ -452,29 +452,37 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
 // The apply pass, one thread per POOLED cell (oh, ow, chunk) handling the 2x2 input block
 // (2oh + i, 2ow + j): an even input row / column is covered by window oh / ow only, an odd one by oh
 // and oh + 1, so the four windows {oh, oh+1} x {ow, ow+1} serve all four input elements.  A block
-// covers RB pooled rows (2 RB input rows) of one image with one thread per (column, chunk) of a row:
-//  * the RB + 1 pooled gradient / argmax rows it needs (one halo row) are staged in LDS once with
-//    16-byte loads, and the four windows of a cell are LDS reads;
+// covers RB pooled rows (2 RB input rows) and cols_per pooled columns (blockIdx.z-th column block) of
+// one image with one thread per (column, chunk):
+//  * the RB + 1 pooled gradient / argmax rows it needs (one halo row) over its columns + one halo
+//    column are staged in LDS once with 16-byte loads, and the four windows of a cell are LDS reads;
+//  * column blocks of <= 256 threads: at 158 VGPRs a CU holds 12 waves, i.e. one whole-row block of
+//    7 waves but three 4-wave half-row blocks;
 //  * a thread's input chunks (y) of the next two row pairs are in flight while the current pair computes;
 //  * dy = A*d + B*y + Cc with d the pooling gather of dP masked by a > 0.
 template <int RB>
-__global__ __launch_bounds__(512, 2) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
+__global__ __launch_bounds__(256, 3) void k_bnpool_bwd(const uint4* __restrict__ dP, const uint2* __restrict__ Arg,
                                                        const uint4* __restrict__ Y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const float* __restrict__ coef,
                                                        uint4* __restrict__ dY, int H, int W, int OH, int OW, int CP,
-                                                       int lgcp) {
+                                                       int lgcp, int cols_per) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   const int ncell = OW * CP;                            // cells of a pooled row
-  uint4* gs = reinterpret_cast<uint4*>(bsm);           // [RB + 1][ncell] pooled gradient chunks
-  uint2* as = reinterpret_cast<uint2*>(bsm + (size_t)(RB + 1) * ncell * 16);   // [RB + 1][ncell] argmax codes
+  const int c_lo = blockIdx.z * cols_per, c_hi = min(OW, c_lo + cols_per);
+  if (c_lo >= OW) return;                               // whole block
+  const int sw = min(c_hi + 1, OW) - c_lo;              // staged columns (incl. the halo column)
+  const int scell = sw * CP;
+  uint4* gs = reinterpret_cast<uint4*>(bsm);           // [RB + 1][scell] pooled gradient chunks
+  uint2* as = reinterpret_cast<uint2*>(bsm + (size_t)(RB + 1) * (cols_per + 1) * CP * 16);   // argmax codes
   const int n = blockIdx.y, t = threadIdx.x, c8 = t & (CP - 1), C = CP * 8;
   const int r0 = blockIdx.x * RB;
   const int nrow = min(RB + 1, OH - r0);               // staged pooled rows (incl. the halo row)
-  const uint4* dimg = dP + ((size_t)n * OH + r0) * ncell;
-  const uint2* aimg = Arg + ((size_t)n * OH + r0) * ncell;
-  for (int e = t; e < nrow * ncell; e += blockDim.x) {
-    gs[e] = dimg[e];
-    as[e] = aimg[e];
+  const uint4* dimg = dP + ((size_t)n * OH + r0) * ncell + c_lo * CP;
+  const uint2* aimg = Arg + ((size_t)n * OH + r0) * ncell + c_lo * CP;
+  for (int e = t; e < nrow * scell; e += blockDim.x) {
+    const int row = e / scell, x = e - row * scell;
+    gs[e] = dimg[row * ncell + x];
+    as[e] = aimg[row * ncell + x];
   }
   float sc[8], sf[8], k0[8], k1[8], k2[8];
 #pragma unroll
@@ -486,8 +494,8 @@ __global__ __launch_bounds__(512, 2) void k_bnpool_bwd(const uint4* __restrict__
     k1[e] = coef[C + c];
     k2[e] = coef[2 * C + c];
   }
-  const bool live = t < ncell;
-  const int cell = live ? t : 0, ow = cell >> lgcp;
+  const bool live = t < (c_hi - c_lo) * CP;
+  const int cell = live ? t : 0, ow = c_lo + (cell >> lgcp);
   // the thread's input chunks of a row pair (zeros past the image); the next two pairs' are loaded
   // while the current one is processed
   auto load_y = [&](int r, uint4 (&v)[2][2]) {
@@ -523,7 +531,7 @@ __global__ __launch_bounds__(512, 2) void k_bnpool_bwd(const uint4* __restrict__
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int rr = min(r + a, nrow - 1), oc = min(ow + b, OW - 1);
-        const int o = rr * ncell + oc * CP + c8;
+        const int o = rr * scell + (oc - c_lo) * CP + c8;
         g[a][b] = gs[o];
         ar[a][b] = as[o];
       }
@@ -715,9 +723,11 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
                           hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64 || OW * CP > 512) return hipErrorInvalidValue;
-  const int lg = ilog2(CP), nt = (OW * CP + 63) / 64 * 64, gx = (OH + kBnpoolRB - 1) / kBnpoolRB;
-  const size_t lds = (size_t)(kBnpoolRB + 1) * OW * CP * 24;      // staged gradient (16 B) + argmax (8 B) rows
-  if (lds > 65536) return hipErrorInvalidValue;
+  // column blocks of <= 256 threads (one per (column, chunk)) with one halo column each
+  const int ncb = (OW * CP + 255) / 256, cols_per = (OW + ncb - 1) / ncb;
+  const int lg = ilog2(CP), nt = (cols_per * CP + 63) / 64 * 64, gx = (OH + kBnpoolRB - 1) / kBnpoolRB;
+  const size_t lds = (size_t)(kBnpoolRB + 1) * (cols_per + 1) * CP * 24;   // staged gradient (16 B) + argmax (8 B)
+  if (lds > 65536 || nt > 256) return hipErrorInvalidValue;
   // BN partials from the pooled maps: rows = pooled cells, x = y[argmax], mask x*scale + shift > 0
   const int Mp = N * OH * OW, RP = 256 / CP;
   int nblk = pde_bn_blocks(Mp, C);
@@ -734,9 +744,9 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
   }
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, pp, nblk, C, N * H * W,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
-  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB>), dim3(gx, N), dim3(nt), lds, st, (const uint4*)dp,
+  hipLaunchKernelGGL((k_bnpool_bwd<kBnpoolRB>), dim3(gx, N, ncb), dim3(nt), lds, st, (const uint4*)dp,
                      (const uint2*)arg, (const uint4*)y, scale, shift, (const float*)coef, (uint4*)dy, H, W, OH, OW,
-                     CP, lg);
+                     CP, lg, cols_per);
   return hipGetLastError();
 }
 
