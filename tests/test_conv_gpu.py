@@ -183,3 +183,24 @@ def test_conv_dgrad_fused_downsample(B, C, H, W, N):
         (F.conv2d(xr, wd.float(), None, 2, 0) * dyd.float()).sum()).backward()
     err = (dx.float() - xr.grad).abs().max().item()
     assert err <= 1e-2 * xr.grad.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("C,H,N,k,s,p", [(64, 56, 128, 3, 2, 1), (128, 28, 128, 3, 1, 1), (128, 28, 256, 3, 2, 1),
+                                         (256, 14, 256, 3, 1, 1), (256, 14, 512, 3, 2, 1), (512, 7, 512, 3, 1, 1),
+                                         (64, 56, 128, 1, 2, 0)])
+def test_wgrad_split_fits_one_block_round(C, H, N, k, s, p):
+    """The split-K wgrad grid (tiles x splits) of every ResNet-18 layer-2..4 geometry at B=256 stays
+    within one round of co-resident blocks (2 per CU): a ceil-rounded split count launched 513-576
+    blocks, and the few past the round ran as a tail as long as a whole block
+    (profiles/r3_models/wgrad_blocks_sweep.jsonl)."""
+    K = kernels()
+    B = 256
+    x = torch.empty(B, C, H, H, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.empty(N, C, k, k, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    splits = K.conv_wgrad_splits(x, w, s, p)
+    BM = 128 if N % 128 == 0 else 64
+    tiles = (N // BM) * ((k * k * C + 127) // 128)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert 1 <= splits and splits * tiles <= 2 * ncu
+    if k == 3:
+        assert splits * tiles > ncu      # and fills at least one block per CU
