@@ -18,6 +18,9 @@ hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float
 hipError_t pde_lenet_head(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
                           float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
                           double* loss_sum, unsigned long long* correct, hipStream_t st);
+hipError_t pde_lenet_head2(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
+                           float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
+                           double* loss_sum, unsigned long long* correct, hipStream_t st);
 hipError_t pde_lenet_head_bwd(const float* H1, int B, const float* W2, const float* logp, const float* g, float* dZ2,
                               float* dZ1, hipStream_t st);
 hipError_t pde_lenet_fc_bwd(const float* P2, const float* H1, const float* dZ1, const float* dZ2, const float* W1,
@@ -69,8 +72,12 @@ struct PdeLenetBwdOpt {
   float* ar_buf;
   long long ar_n;
   int ar_two;
-  int defer;                // 1: leave slabs / replicas for the flat optimizer to fold (no in-launch fold)
+  int defer;                // 0: fold in the launch; 1: leave slabs / replicas for the flat optimizer to fold;
+                            // 2 (ext): slabs + per-image conv1 partials, folded by pde_lenet_conv_grad_fold
+  float* c1img;             // ext: [B][520] per-image conv1 partials
 };
+hipError_t pde_lenet_conv_grad_fold(const float* slab, const float* c1img, int B, float* g, long long c1w, long long c1b,
+                                    long long c2w, long long c2b, hipStream_t st);
 hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,
                                const uint8_t* A2, const float* W2c, int B, const PdeLenetBwdOpt* o,
                                const float* row_loss, const int* row_hit, double* loss_sum, unsigned long long* correct,

@@ -19,6 +19,7 @@ struct PeerDev {
   uint8_t* flags[kPeerMaxRanks];
   uint8_t* data[kPeerMaxRanks];
   uint32_t* ctrl;
+  uint32_t* err_host;   // host-mapped time-out flag (PeerAllReduce::error_async)
   int64_t cap;
   int64_t timeout;   // s_memrealtime ticks (100 MHz)
   int32_t rank;

@@ -19,7 +19,10 @@ __device__ __forceinline__ uint32_t* peer_flag(uint8_t* region, int phase, int v
 }
 
 // Block barrier with virtual block vb of every rank (see peer_allreduce.hip: peer_barrier).
-__device__ __forceinline__ void peer_vbarrier(const PeerDev& d, int phase, int vb, uint32_t target, bool failed) {
+// *bad (the caller's LDS word, block-uniform after the closing __syncthreads): set on a time-out, so
+// the virtual block writes NaN instead of a partial sum (see peer_allreduce.hip: peer_barrier).
+__device__ __forceinline__ void peer_vbarrier(const PeerDev& d, int phase, int vb, uint32_t target, bool failed,
+                                              uint32_t* bad) {
   __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): this wave's stores have landed
   __syncthreads();
   const int t = threadIdx.x;
@@ -36,6 +39,8 @@ __device__ __forceinline__ void peer_vbarrier(const PeerDev& d, int phase, int v
         spins = 0;
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > d.timeout) {
           __hip_atomic_fetch_add(d.ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (d.err_host) __hip_atomic_store(d.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          *bad = 1u;
           break;
         }
       }
@@ -106,11 +111,13 @@ __device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
     }
   }
   if (vb == 0 && threadIdx.x < tail) reinterpret_cast<float*>(my_stage)[n4 * 4 + threadIdx.x] = in_f[n4 * 4 + threadIdx.x];
-  peer_vbarrier(d, 0, vb, target, failed);
+  peer_vbarrier(d, 0, vb, target, failed, lds2 + 1);
+  bool bad = lds2[1] != 0;                        // poisoned before, or a wait of this block timed out
+  const peer_vec_t vnan = {0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u};
   if (vb == 0 && threadIdx.x < tail) {
     float acc = 0.f;
     for (int p = 0; p < W; ++p) acc += reinterpret_cast<const float*>(stage[p])[n4 * 4 + threadIdx.x];
-    out_f[n4 * 4 + threadIdx.x] = acc * scale;
+    out_f[n4 * 4 + threadIdx.x] = bad ? __builtin_nanf("") : acc * scale;
   }
   const int64_t lo = two_shot ? (int64_t)d.rank * chunk4 : 0;
   const int64_t len = two_shot ? ((lo + chunk4 <= n4) ? chunk4 : (n4 > lo ? n4 - lo : 0)) : n4;
@@ -120,12 +127,13 @@ __device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
 #pragma unroll
     for (int p = 0; p < kPeerMaxRanks; ++p)
       if (p < W) v[p] = stage[p][lo + i];
-    const peer_vec_t r = peer_sum(v, W, scale);
+    const peer_vec_t r = bad ? vnan : peer_sum(v, W, scale);
     out[lo + i] = r;
     if (two_shot) reinterpret_cast<peer_vec_t*>(d.data[d.rank] + (2 + par) * d.cap)[lo + i] = r;
   }
   if (two_shot) {
-    peer_vbarrier(d, 1, vb, target, failed);
+    peer_vbarrier(d, 1, vb, target, failed, lds2 + 1);
+    bad = lds2[1] != 0;
     // 3. gather every other chunk from its owner's res[par]
     for (int64_t i = t0; i < chunk4; i += stride) {
       peer_vec_t v[kPeerMaxRanks];
@@ -137,7 +145,7 @@ __device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
 #pragma unroll
       for (int q = 0; q < kPeerMaxRanks; ++q) {
         const int64_t g = (int64_t)q * chunk4 + i;
-        if (q < W && q != d.rank && g <= last) out[g] = v[q];
+        if (q < W && q != d.rank && g <= last) out[g] = bad ? vnan : v[q];
       }
     }
   }

@@ -985,6 +985,14 @@ hipError_t pde_lenet_fc1_fwd(const float* P2, int B, const float* W, const float
 hipError_t pde_lenet_head(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
                           float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
                           double* loss_sum, unsigned long long* correct, hipStream_t st) {
+  // default: the one-row-per-block kernel of lenet_v2.hip; PDE_LENET_HEAD=1 keeps this file's
+  // four-rows-per-block k_head (A/B runs)
+  static const bool v1_head = [] {
+    const char* e = getenv("PDE_LENET_HEAD");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (!v1_head)
+    return pde_lenet_head2(H1, B, W2, b2, labels, inv_b, logp_out, dZ2, dZ1, row_loss, row_hit, loss_sum, correct, st);
   if (g_prof)
     hipLaunchKernelGGL(k_head<true>, dim3((B + 3) / 4), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2,
                        dZ1, row_loss, row_hit, loss_sum, correct, prof_slot(2));

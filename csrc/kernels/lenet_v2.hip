@@ -288,6 +288,8 @@ constexpr int kC1Rep = 576;                        // int64 per conv1 replica: w
                                                    // (the layout of the conv1 slots of the flat gradient buffer)
 constexpr int kC1NRep = 16;
 constexpr float kC1Scale = 1099511627776.f;        // 2^40 fixed point for the order-free int64 sums
+constexpr int kC1BadSlot = 511;                    // replica 0, unused weight slot: non-finite partial count
+constexpr int kC1Img = 520;                        // ext mode: floats per image partial (2 halves x 10 ch x 26)
 constexpr double kC1InvScale = 1.0 / 1099511627776.0;
 enum { kTickD = 16, kTicks = 32 };        // [0, 16): per-k-slice W tickets, [16]: D blocks
 
@@ -304,9 +306,16 @@ struct Bwd2Opt {
   float* ar_buf;
   long long ar_n;
   int ar_nvb, ar_two;
-  int defer;                   // 1: no in-launch fold -- W blocks store slabs, D blocks add replicas, and the
-                               // next launch (the flat optimizer) folds both (W = 1: no seam on the chain)
+  float* c1img;                // ext mode: [B][520] conv1 wgrad|bgrad partial per image (plain stores)
 };
+// Where the conv weight gradients are reduced (template MODE of k_conv_bwd2):
+enum { kBwdFold = 0,    // in-launch: last-arriving W block per k slice folds the 16 slabs (write-through),
+                        // conv1 as int64 fixed-point atomics folded by the last D block -> canonical grads
+       kBwdDefer = 1,   // W = 1: slabs (plain stores) + float-atomic conv1 replicas in the flat buffer,
+                        // folded by the flat optimizer's fold blocks (no reduction seam on the chain)
+       kBwdExt = 2 };   // comm path: slabs + per-image conv1 partials, plain stores only; a small
+                        // deterministic fold launch (k_conv_grad_fold) writes the canonical gradients
+                        // the all-reduce needs
 
 // write-through (sc1) stores and L1-bypassing (sc1) loads for the in-kernel hand-offs
 // (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + vmcnt(0) + barrier + one agent-scope
@@ -349,7 +358,7 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <bool PROF, bool FOLD>
+template <bool PROF, int MODE>
 __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb, const float* __restrict__ P1,
                                                    const uint8_t* __restrict__ A1, const float* __restrict__ dP2m,
                                                    const uint8_t* __restrict__ A2, const float* __restrict__ W2c,
@@ -488,8 +497,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
         if (cor < 50) {
           float* dst = kk < 500 ? sl + cor * 500 + kk : sl + kSlabBias + cor;
           if (kk <= 500) {
-            if (!FOLD) *dst = v;           // read by the next launch: plain store
-            else st_wt(dst, v);            // read by the last-arriving block of this launch: write-through
+            if (MODE != kBwdFold) *dst = v;   // read by the next launch: plain store
+            else st_wt(dst, v);               // read by the last-arriving block of this launch: write-through
           }
         }
       }
@@ -502,7 +511,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
       }
     }
     PMARK(3);
-    if constexpr (FOLD) {
+    if constexpr (MODE == kBwdFold) {
     if (arrive_last(op.tick + kp, kNIG, lflag)) {
       PMARK(4);
       // ---- last group of k slice kp: fold the 16 slabs (fixed order) -> canonical gradient ----
@@ -537,7 +546,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     if (op.ar_nvb > 0 && idx < op.ar_nvb)
       pde::peer_ar_f32_vblock(op.pd, op.ar_buf, op.ar_buf, op.ar_n, 1.f, idx, op.ar_nvb, op.ar_two != 0,
                               reinterpret_cast<uint32_t*>(smem + kL_PEER));
-    }   // FOLD
+    }   // kBwdFold
     PMARK(6);
     return;
   }
@@ -669,13 +678,22 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     const float v = red[c * 36 + tap] + red[(16 + c) * 36 + tap] + red[(32 + c) * 36 + tap] + red[(48 + c) * 36 + tap];
     const int ch = 10 * hh + c;
     const int slot = tap < 25 ? ch * 25 + tap : 512 + ch;
-    if (!FOLD)               // float atomics into replica (b % 16) of the flat buffer, folded by the optimizer
+    if constexpr (MODE == kBwdDefer) {   // float atomics into replica (b % 16), folded by the optimizer
       atomicAdd(op.c1part + (size_t)(b % kC1NRep) * kC1Rep + slot, v);
-    else
-      atomicAdd(reinterpret_cast<unsigned long long*>(op.c1rep + (size_t)(b % kC1NRep) * kC1Rep + slot),
-                (unsigned long long)__float2ll_rn(v * kC1Scale));
+    } else if constexpr (MODE == kBwdExt) {   // this image's partial, plain store; k_conv_grad_fold sums them
+      op.c1img[(size_t)b * kC1Img + hh * 260 + t] = v;
+    } else {
+      // order-free int64 fixed point (2^-40 quantum).  A non-finite or out-of-range partial (|v| >= 2^22
+      // would overflow the 2^62 budget of 16 adders) is not converted: it bumps the flag in unused slot
+      // 511 of replica 0 and the folding block then writes NaN -- divergence stays visible.
+      if (fabsf(v) < 4194304.f)
+        atomicAdd(reinterpret_cast<unsigned long long*>(op.c1rep + (size_t)(b % kC1NRep) * kC1Rep + slot),
+                  (unsigned long long)__float2ll_rn(v * kC1Scale));
+      else
+        atomicAdd(reinterpret_cast<unsigned long long*>(op.c1rep + kC1BadSlot), 1ull);
+    }
   }
-  if (FOLD && arrive_last(op.tick + kTickD, (unsigned)nD, lflag)) {
+  if (MODE == kBwdFold && arrive_last(op.tick + kTickD, (unsigned)nD, lflag)) {
     // ---- last D block: fold the 16 replicas (exact) -> canonical conv1 gradient, re-zero ----
     if (t == 0) __hip_atomic_store(op.tick + kTickD, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // items: weight t (t < 500), bias t - 500 (t < 512), bias 12 + t (second slot, t < 8); all loads
@@ -691,6 +709,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
 #pragma unroll
       for (int r = 0; r < kC1NRep; ++r) q[u][r] = ld_wt64(op.c1rep + (size_t)r * kC1Rep + slot[u]);
     }
+    const bool bad = ld_wt64(op.c1rep + kC1BadSlot) != 0;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && t >= 8) break;
@@ -698,12 +717,234 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
 #pragma unroll
       for (int r = 0; r < kC1NRep; ++r) acc += q[u][r];
       const float gsum = (float)((double)acc * kC1InvScale);
-      op.g[e[u]] = gsum;
+      op.g[e[u]] = bad ? __builtin_nanf("") : gsum;
     }
     __syncthreads();
     for (int i = t; i < kC1NRep * kC1Rep; i += 512) op.c1rep[i] = 0;
   }
   PMARK(6);
+}
+
+// =================================================================================================
+// F3 v2: fc2 (500 -> 10) + log_softmax + cross_entropy(log_softmax) + dlogits + fc2 dgrad + ReLU mask,
+// ONE ROW PER 256-THREAD BLOCK (B blocks: 128 CUs at B = 128, against 32 four-row blocks in lenet.hip's
+// k_head).  Wave w owns hidden units [128w, 128w + 128): lane l holds n0 = 128w + l and n1 = n0 + 64
+// (n1 < 500), so every lane issues its 2 H1 + 20 W2 loads in ONE round trip (22 loads, under the
+// vmcnt limit; the four-row kernel needed 88 per lane and waited twice).  The ten class partials are
+// reduced across the wave by a TRANSPOSED reduction on VALU lane-exchange ops only (no LDS permutes):
+// v_permlane32_swap (10 -> 5 live sums per lane), v_permlane16_swap (5 -> 3), DPP row_mirror (3 -> 2),
+// row_half_mirror (2 -> 1), two quad_perm steps -- 13 exchanges instead of 10 x 6 dependent
+// ds_bpermute butterflies -- then the four waves' class sums meet in 64 B of LDS.  Same math and
+// outputs as k_head (the reference applies cross_entropy to log_softmax output, main.py:89, 147).
+// =================================================================================================
+__device__ __forceinline__ float xswap_sum32(float a, float b) {   // lanes < 32: a(l)+a(l+32); >= 32: b(l-32)+b(l)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xswap_sum16(float a, float b) {   // even rows: a(l)+a(l+16); odd: b(l-16)+b(l)
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// Class held (fully reduced, in lanes with (l & 3) == 0) after head_class_reduce; -1 = padding lane.
+__device__ __forceinline__ int head_class_of_lane(int l) {
+  const int j = ((l >> 3) & 1) * 2 + ((l >> 2) & 1);        // index into the 3 sums of stage 2
+  const int y = j + 3 * ((l >> 4) & 1);                     // index into the 5 sums of stage 1
+  return (j < 3 && y < 5) ? y + 5 * (l >> 5) : -1;
+}
+__device__ __forceinline__ float head_class_reduce(const float (&x)[10], int l) {
+  float y[6];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) y[k] = xswap_sum32(x[k], x[k + 5]);
+  y[5] = 0.f;
+  float z[4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) z[k] = xswap_sum16(y[k], y[k + 3]);
+  z[3] = 0.f;
+  const bool lo8 = (l & 8) == 0, lo4 = (l & 4) == 0;
+  float u[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float send = lo8 ? z[k + 2] : z[k];
+    u[k] = (lo8 ? z[k] : z[k + 2]) + dpp<0x140>(send);                       // row_mirror: i <-> 15 - i
+  }
+  float v = (lo4 ? u[0] : u[1]) + dpp<0x141>(lo4 ? u[1] : u[0]);              // row_half_mirror: i <-> 7 - i
+  v += dpp<0xB1>(v);                                                          // quad_perm(1,0,3,2)
+  v += dpp<0x4E>(v);                                                          // quad_perm(2,3,0,1)
+  return v;
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(256) void k_head2(const float* __restrict__ H1, int B, const float* __restrict__ W2,
+                                               const float* __restrict__ b2, const long long* __restrict__ labels,
+                                               float inv_b, float* __restrict__ logp_out, float* __restrict__ dZ2,
+                                               float* __restrict__ dZ1, float* __restrict__ row_loss,
+                                               int* __restrict__ row_hit, double* __restrict__ loss_sum,
+                                               unsigned long long* __restrict__ correct,
+                                               unsigned long long* __restrict__ prof) {
+  constexpr int kHid = 500, kCls = 10;
+  __shared__ __attribute__((aligned(16))) float part[4][16];
+  PMARK(0);
+  const int row = blockIdx.x, t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int n0 = 128 * w + l, n1 = n0 + 64;                // n0 < 448 + 64 <= 500 always
+  const bool v1 = n1 < kHid;
+  const int n1c = v1 ? n1 : kHid - 1;
+  const float* hrow = H1 + (size_t)row * kHid;
+  const float h0 = hrow[n0];
+  const float h1r = hrow[n1c];
+  float wa[kCls], wb[kCls], bias[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    wa[c] = W2[c * kHid + n0];
+    wb[c] = W2[c * kHid + n1c];
+  }
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) bias[c] = b2[c];
+  const int y = (int)labels[row];
+  // every load above is issued before any use: one round trip (the scheduler would otherwise start
+  // the dot products after the first few loads and wait again for each later batch)
+  __builtin_amdgcn_sched_barrier(0);
+  const float h1 = v1 ? h1r : 0.f;
+  float x[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) x[c] = fmaf(h1, wb[c], h0 * wa[c]);
+  const float red = head_class_reduce(x, l);
+  const int cls = head_class_of_lane(l);
+  if ((l & 3) == 0 && cls >= 0) part[w][cls] = red;
+  __syncthreads();
+  PMARK(2);
+  float4 pv[4][3];                                   // 12 broadcast b128 reads, one wait
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pv[q][k] = reinterpret_cast<const float4*>(part[q])[k];
+  float z[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    const float* a0 = &pv[0][c >> 2].x;
+    const float* a1 = &pv[1][c >> 2].x;
+    const float* a2 = &pv[2][c >> 2].x;
+    const float* a3 = &pv[3][c >> 2].x;
+    z[c] = (a0[c & 3] + a1[c & 3]) + (a2[c & 3] + a3[c & 3]) + bias[c];
+  }
+  float m = z[0];
+#pragma unroll
+  for (int c = 1; c < kCls; ++c) m = fmaxf(m, z[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) se += expf(z[c] - m);
+  const float lse = logf(se);
+  float lp[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) lp[c] = z[c] - m - lse;
+  float m2 = lp[0];
+  int pred = 0;
+#pragma unroll
+  for (int c = 1; c < kCls; ++c) {
+    if (lp[c] > m2) { m2 = lp[c]; pred = c; }
+  }
+  float se2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) se2 += expf(lp[c] - m2);
+  const float lse2 = logf(se2);
+  float lpy = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) lpy = (c == y) ? lp[c] - m2 - lse2 : lpy;
+  const float loss = -lpy;
+  const int hit = pred == y ? 1 : 0;
+  if (t == 0) {
+    if (row_loss) {
+      row_loss[row] = loss;
+      row_hit[row] = hit;
+    } else if (loss_sum) {
+      atomicAdd(loss_sum, (double)loss);
+      atomicAdd(correct, (unsigned long long)hit);
+    }
+  }
+  if (logp_out && t < kCls) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) v = (c == t) ? lp[c] : v;
+    logp_out[(size_t)row * kCls + t] = v;
+  }
+  if (!dZ1) return;
+  float dz[kCls], sdl = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    const float dl = (expf(lp[c] - m2 - lse2) - (c == y ? 1.f : 0.f)) * inv_b;
+    dz[c] = dl;
+    sdl += dl;
+  }
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) dz[c] = dz[c] - expf(lp[c]) * sdl;
+  if (t < kCls) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) v = (c == t) ? dz[c] : v;
+    dZ2[(size_t)row * kCls + t] = v;
+  }
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    s0 = fmaf(dz[c], wa[c], s0);
+    s1 = fmaf(dz[c], wb[c], s1);
+  }
+  float* drow = dZ1 + (size_t)row * kHid;
+  drow[n0] = h0 > 0.f ? s0 : 0.f;
+  if (v1) drow[n1] = h1 > 0.f ? s1 : 0.f;
+  PMARK(1);
+}
+
+// Ext-mode fold (the comm path's canonical conv gradients, deterministic: fixed summation order).
+// Blocks [0, kFoldC2): conv2 -- thread i of the 25088-float slab image sums the 16 slabs in group
+// order (16 loads in flight per thread).  Blocks [kFoldC2, +kFoldC1): conv1 -- 16 outputs per block,
+// thread (o = t & 15, part = t >> 4) sums images part, part + 16, ... in order, then the 16 parts are
+// added in part order through LDS.
+constexpr int kFoldC2 = (kSlab + 255) / 256;        // 98
+constexpr int kFoldC1 = (kC1Img + 15) / 16;         // 33
+__global__ __launch_bounds__(256) void k_conv_grad_fold(const float* __restrict__ slab, const float* __restrict__ c1img,
+                                                        int B, float* __restrict__ g, long long c1w, long long c1b,
+                                                        long long c2w, long long c2b) {
+  const int t = threadIdx.x;
+  if (blockIdx.x < kFoldC2) {
+    const int i = blockIdx.x * 256 + t;
+    const int ic = min(i, kSlab - 1);
+    float q[kNIG];
+#pragma unroll
+    for (int r = 0; r < kNIG; ++r) q[r] = slab[(size_t)r * kSlab + ic];
+    float s = q[0];
+#pragma unroll
+    for (int r = 1; r < kNIG; ++r) s += q[r];
+    if (i < 25000) g[c2w + i] = s;
+    else if (i >= kSlabBias && i < kSlabBias + 50) g[c2b + (i - kSlabBias)] = s;
+    return;
+  }
+  __shared__ float red[16][17];
+  const int o = (blockIdx.x - kFoldC2) * 16 + (t & 15), part = t >> 4, oc = min(o, kC1Img - 1);
+  float s = 0.f;
+  constexpr int kMaxPer = 8;                         // B <= 128 images: 8 per part
+  float q[kMaxPer];
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int b = part + 16 * k;
+    q[k] = c1img[(size_t)min(b, B - 1) * kC1Img + oc];
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k)
+    if (part + 16 * k < B) s += q[k];
+  red[part][t & 15] = s;
+  __syncthreads();
+  if (t < 16 && o < kC1Img) {
+    float a = red[0][t];
+#pragma unroll
+    for (int p = 1; p < 16; ++p) a += red[p][t];
+    const int hh = o / 260, rem = o - hh * 260, c = rem / 26, tap = rem - c * 26, ch = 10 * hh + c;
+    if (tap < 25) g[c1w + ch * 25 + tap] = a;
+    else g[c1b + ch] = a;
+  }
 }
 
 __global__ void k_pack_w2_v2(const float* __restrict__ w2, float* __restrict__ dst) {
@@ -751,7 +992,9 @@ hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* 
   op.tick = o->tick;
   op.g = o->g;
   op.c1w = o->c1w; op.c1b = o->c1b; op.c2w = o->c2w; op.c2b = o->c2b;
-  op.defer = o->defer;
+  op.c1img = o->c1img;
+  const int mode = o->defer == 1 ? kBwdDefer : (o->defer == 2 ? kBwdExt : kBwdFold);
+  if (mode == kBwdExt && op.c1img == nullptr) return hipErrorInvalidValue;
   if (o->peer_dev != nullptr && o->ar_buf != nullptr && o->ar_n > 0) {
     std::memcpy(&op.pd, o->peer_dev, sizeof(op.pd));
     op.ar_buf = o->ar_buf;
@@ -765,13 +1008,36 @@ hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* 
   hipLaunchKernelGGL((k_conv_bwd2<P, F>), dim3(nblk), dim3(512), 0, st, Xb, P1, A1, dP2m, A2, W2c, B, op, row_loss, \
                      row_hit, loss_sum, correct, ga, dbg, P ? prof : nullptr)
   if (prof) {
-    if (op.defer) PDE_BWD2_LAUNCH(true, false);
-    else PDE_BWD2_LAUNCH(true, true);
+    if (mode == kBwdDefer) PDE_BWD2_LAUNCH(true, kBwdDefer);
+    else if (mode == kBwdExt) PDE_BWD2_LAUNCH(true, kBwdExt);
+    else PDE_BWD2_LAUNCH(true, kBwdFold);
   } else {
-    if (op.defer) PDE_BWD2_LAUNCH(false, false);
-    else PDE_BWD2_LAUNCH(false, true);
+    if (mode == kBwdDefer) PDE_BWD2_LAUNCH(false, kBwdDefer);
+    else if (mode == kBwdExt) PDE_BWD2_LAUNCH(false, kBwdExt);
+    else PDE_BWD2_LAUNCH(false, kBwdFold);
   }
 #undef PDE_BWD2_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_conv_grad_fold(const float* slab, const float* c1img, int B, float* g, long long c1w, long long c1b,
+                                    long long c2w, long long c2b, hipStream_t st) {
+  if (B < 1 || B > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_conv_grad_fold, dim3(kFoldC2 + kFoldC1), dim3(256), 0, st, slab, c1img, B, g, c1w, c1b, c2w, c2b);
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_head2(const float* H1, int B, const float* W2, const float* b2, const long long* labels,
+                           float inv_b, float* logp_out, float* dZ2, float* dZ1, float* row_loss, int* row_hit,
+                           double* loss_sum, unsigned long long* correct, hipStream_t st) {
+  if (B < 1) return hipSuccess;
+  unsigned long long* prof = pde_lenet_prof_slot(2);
+  if (prof)
+    hipLaunchKernelGGL(k_head2<true>, dim3(B), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2, dZ1,
+                       row_loss, row_hit, loss_sum, correct, prof);
+  else
+    hipLaunchKernelGGL(k_head2<false>, dim3(B), dim3(256), 0, st, H1, B, W2, b2, labels, inv_b, logp_out, dZ2, dZ1,
+                       row_loss, row_hit, loss_sum, correct, nullptr);
   return hipGetLastError();
 }
 

@@ -328,6 +328,20 @@ void lenet_gather(const at::Tensor& X, const at::Tensor& labels, const OptT& idx
             "lenet_gather");
 }
 
+void lenet_conv_grad_fold(const at::Tensor& slab, const at::Tensor& c1img, int64_t B, const at::Tensor& g, int64_t c1w,
+                          int64_t c1b, int64_t c2w, int64_t c2b) {
+  TORCH_CHECK(B >= 1 && B <= 128, "conv_grad_fold: batch must be in [1, 128]");
+  check_cuda(slab, "slab", F32, 16 * 25088);
+  check_cuda(c1img, "c1img", F32, B * 520);
+  check_cuda(g, "grads", F32);
+  const int64_t n = g.numel();
+  TORCH_CHECK(c1w >= 0 && c1w + 500 <= n && c1b >= 0 && c1b + 20 <= n && c2w >= 0 && c2w + 25000 <= n && c2b >= 0 &&
+                  c2b + 50 <= n, "conv_grad_fold: conv gradient slots outside the flat buffer");
+  hip_check(pde_lenet_conv_grad_fold(ptr<float>(slab), ptr<float>(c1img), (int)B, ptr<float>(g), c1w, c1b, c2w, c2b,
+                                     cur_stream()),
+            "lenet_conv_grad_fold");
+}
+
 void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& dP2m,
                      const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& slab,
                      const at::Tensor& c1rep, const at::Tensor& c1part, const at::Tensor& tick, const at::Tensor& g, int64_t c1w, int64_t c1b,
@@ -335,7 +349,7 @@ void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tenso
                      const OptT& loss_sum, const OptT& correct, const OptT& gX, const OptT& glabels, const OptT& gidx,
                      const OptT& gctr, int64_t gnbatches, int64_t gstride, const OptT& gXdst, const OptT& gYdst,
                      const OptT& grows, const OptT& peer_dev, const OptT& ar_buf, int64_t ar_two, int64_t defer,
-                     int64_t dbg) {
+                     int64_t dbg, const OptT& c1img) {
   TORCH_CHECK(B >= 1 && B <= 128, "conv_bwd2: batch must be in [1, 128] (16 image groups of <= 8 images)");
   check_cuda(Xb, "Xb", F32, B * 784);
   check_cuda(P1, "P1", F32, B * 2880);
@@ -360,7 +374,13 @@ void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tenso
   o.tick = reinterpret_cast<unsigned*>(tick.data_ptr<int32_t>());
   o.g = ptr<float>(g);
   o.c1w = c1w; o.c1b = c1b; o.c2w = c2w; o.c2b = c2b;
-  o.defer = defer ? 1 : 0;
+  TORCH_CHECK(defer >= 0 && defer <= 2, "conv_bwd2: defer must be 0 (fold), 1 (defer) or 2 (ext)");
+  o.defer = (int)defer;
+  if (defer == 2) {
+    TORCH_CHECK(c1img.has_value(), "conv_bwd2: ext mode needs the per-image conv1 partial buffer");
+    check_cuda(*c1img, "c1img", F32, B * 520);
+    o.c1img = ptr<float>(*c1img);
+  }
   if (peer_dev.has_value()) {
     TORCH_CHECK(peer_dev->numel() == (int64_t)sizeof(pde::PeerDev), "bad peer device args");
     check_cuda(*ar_buf, "ar_buf", F32);
@@ -598,6 +618,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_pack_w2_v2", &lenet_pack_w2_v2);
   m.def("lenet_conv_fwd2", &lenet_conv_fwd2, py::arg("Xb"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wp"),
         py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("zero") = py::none());
+  m.def("lenet_conv_grad_fold", &lenet_conv_grad_fold);
   m.def("lenet_conv_bwd2", &lenet_conv_bwd2, py::arg("Xb"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("slab"), py::arg("c1rep"), py::arg("c1part"), py::arg("tick"),
         py::arg("g"),
@@ -606,7 +627,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("gidx") = py::none(), py::arg("gctr") = py::none(), py::arg("gnbatches") = 1, py::arg("gstride") = 0,
         py::arg("gXdst") = py::none(), py::arg("gYdst") = py::none(), py::arg("grows") = py::none(),
         py::arg("peer_dev") = py::none(), py::arg("ar_buf") = py::none(), py::arg("ar_two") = 0, py::arg("defer") = 0,
-        py::arg("dbg") = 0);
+        py::arg("dbg") = 0, py::arg("c1img") = py::none());
   m.def("lenet_gather", &lenet_gather, py::arg("X"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
         py::arg("nbatches"), py::arg("B"), py::arg("Xdst"), py::arg("Ydst"), py::arg("rows_dst"));
   m.def("lenet_set_prof", &lenet_set_prof, py::arg("buf") = py::none());

@@ -226,6 +226,7 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("scale"), py::arg("two"), py::arg("stream"))
       .def("debug_skip_stage", &PeerAllReduce::debug_skip_stage)
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
+      .def("error_async", &PeerAllReduce::error_async)
       .def("reset_error", &PeerAllReduce::reset_error)
       .def("set_timeout_ms", &PeerAllReduce::set_timeout_ms)
       .def("set_one_shot_max_bytes", &PeerAllReduce::set_one_shot_max_bytes)

@@ -64,6 +64,9 @@ class PeerAllReduce {
   // this rank's stage buffer as it was two calls ago): the self-test must catch it.
   void debug_skip_stage(int n) { debug_skip_stage_ = n; }
   int64_t error();
+  // Host-mapped mirror of the time-out latch: non-zero once any barrier wait of this rank timed out.
+  // A plain host load, no device synchronisation (a kernel still queued has not reported yet).
+  int64_t error_async() const;
   void reset_error();
   void set_timeout_ms(int64_t ms) { timeout_ticks_ = ms * 100000; }   // s_memrealtime runs at 100 MHz
   void set_one_shot_max_bytes(int64_t b) { one_shot_max_ = b; }
@@ -79,6 +82,8 @@ class PeerAllReduce {
   uint8_t* flags_ = nullptr;    // own flag region (uncached)
   uint8_t* region_ = nullptr;   // own data region: stage0 | stage1 | res0 | res1
   uint32_t* ctrl_ = nullptr;    // local (not shared): [0] call counter, [1] done counter, [2] error count
+  volatile uint32_t* err_host_ = nullptr;   // pinned host word: 1 once a barrier timed out (kernel-written)
+  uint32_t* err_dev_ = nullptr;             // its device address
   uint8_t* peers_[kPeerMaxRanks] = {};
   uint8_t* peer_flags_[kPeerMaxRanks] = {};
   bool opened_ = false;

@@ -32,6 +32,7 @@ struct Args {
   const vec_t* in;
   vec_t* out;
   uint32_t* ctrl;                 // [0] completed calls, [1] blocks done in this call, [2] timeouts
+  uint32_t* err_host;             // host-mapped mirror of ctrl[2] != 0 (read by the host without a sync)
   int64_t n4;                     // 16-byte vectors
   int64_t tail;                   // trailing elements (< elements per vector)
   int64_t chunk4;                 // two-shot chunk (vectors); == n4 for one-shot
@@ -55,8 +56,12 @@ __device__ __forceinline__ uint8_t* res_ptr(uint8_t* region, int64_t cap, uint32
 // Block-level barrier between block b of every rank: publish `target` into every peer's flag slot
 // for this rank, wait until every peer published it into ours.  Every thread first drains its own
 // stores (vmcnt(0)); the signalling store is a system-scope release after the block barrier.
+// *bad (LDS, block-uniform after the closing __syncthreads): set when this call's communicator was
+// already poisoned or a wait timed out here -- the block then writes NaN instead of a partial sum,
+// so a rank that went on without its peers never hands out plausible-looking wrong gradients.
 template <int W>
-__device__ __forceinline__ void peer_barrier(const Args& a, int phase, uint32_t target, bool failed) {
+__device__ __forceinline__ void peer_barrier(const Args& a, int phase, uint32_t target, bool failed,
+                                             uint32_t* bad) {
   __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): this wave's stores have landed
   __syncthreads();
   const int t = threadIdx.x;
@@ -74,6 +79,8 @@ __device__ __forceinline__ void peer_barrier(const Args& a, int phase, uint32_t 
         spins = 0;
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {   // dead / hung peer
           __hip_atomic_fetch_add(a.ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          *bad = 1u;
           break;
         }
       }
@@ -96,6 +103,7 @@ struct F32Op {
     return mkvec(__float_as_uint(acc[0] * s), __float_as_uint(acc[1] * s), __float_as_uint(acc[2] * s),
                       __float_as_uint(acc[3] * s));
   }
+  static __device__ __forceinline__ vec_t nan_vec() { return mkvec(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u); }
   static constexpr int kAcc = 4;
   static constexpr int kPerVec = 4;
   static __device__ __forceinline__ void tail_add(float& acc, const uint8_t* p, int64_t i) {
@@ -133,6 +141,7 @@ struct BF16Op {
     return mkvec(pk(acc[0] * s, acc[1] * s), pk(acc[2] * s, acc[3] * s), pk(acc[4] * s, acc[5] * s),
                       pk(acc[6] * s, acc[7] * s));
   }
+  static __device__ __forceinline__ vec_t nan_vec() { return mkvec(0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u); }
   static constexpr int kAcc = 8;
   static constexpr int kPerVec = 8;
   static __device__ __forceinline__ void tail_add(float& acc, const uint8_t* p, int64_t i) {
@@ -160,7 +169,7 @@ __device__ __forceinline__ vec_t sum_ranks(const vec_t (&v)[W], float scale) {
 // thread's grid-stride share, two vectors per iteration: 2W independent loads in flight.
 template <int W, typename Op>
 __device__ __forceinline__ void reduce_range(const Args& a, uint32_t par, int64_t lo, int64_t len, int64_t t0,
-                                             int64_t stride, vec_t* res) {
+                                             int64_t stride, vec_t* res, bool bad) {
   const vec_t* st[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) st[p] = reinterpret_cast<const vec_t*>(stage_ptr(a.data[p], a.cap, par)) + lo;
@@ -173,8 +182,8 @@ __device__ __forceinline__ void reduce_range(const Args& a, uint32_t par, int64_
       v0[p] = st[p][i];
       v1[p] = st[p][jj];
     }
-    const vec_t r0 = sum_ranks<W, Op>(v0, a.scale);
-    const vec_t r1 = sum_ranks<W, Op>(v1, a.scale);
+    const vec_t r0 = bad ? Op::nan_vec() : sum_ranks<W, Op>(v0, a.scale);
+    const vec_t r1 = bad ? Op::nan_vec() : sum_ranks<W, Op>(v1, a.scale);
     a.out[lo + i] = r0;
     if (res) res[lo + i] = r0;
     if (j < len) {
@@ -186,10 +195,11 @@ __device__ __forceinline__ void reduce_range(const Args& a, uint32_t par, int64_
 
 template <int W, bool TWO, typename Op>
 __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
-  __shared__ uint32_t s_call, s_failed;
+  __shared__ uint32_t s_call, s_failed, s_bad;
   if (threadIdx.x == 0) {
     s_call = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_failed = __hip_atomic_load(a.ctrl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_bad = s_failed;
   }
   __syncthreads();
   const uint32_t call = s_call;
@@ -227,21 +237,24 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
   if (blockIdx.x == 0 && threadIdx.x < a.tail && !a.skip_stage)
     Op::tail_copy(reinterpret_cast<uint8_t*>(my_stage), reinterpret_cast<const uint8_t*>(a.in),
                   tail_off + threadIdx.x);
-  peer_barrier<W>(a, 0, target, failed);
+  peer_barrier<W>(a, 0, target, failed, &s_bad);
+  bool bad = s_bad != 0;
 
   if (blockIdx.x == 0 && threadIdx.x < a.tail) {   // tail: every rank reduces it itself, same order
     float acc = 0.f;
     for (int p = 0; p < W; ++p) Op::tail_add(acc, stage_ptr(a.data[p], a.cap, par), tail_off + threadIdx.x);
-    Op::tail_store(reinterpret_cast<uint8_t*>(a.out), tail_off + threadIdx.x, acc * a.scale);
+    Op::tail_store(reinterpret_cast<uint8_t*>(a.out), tail_off + threadIdx.x, bad ? __builtin_nanf("") : acc * a.scale);
   }
   if (!TWO) {
-    reduce_range<W, Op>(a, par, 0, a.n4, t0, stride, nullptr);
+    reduce_range<W, Op>(a, par, 0, a.n4, t0, stride, nullptr, bad);
   } else {
     // 2. reduce this rank's chunk from every peer's stage into own res[par] (+ own output)
     const int64_t lo = (int64_t)a.rank * a.chunk4;
     const int64_t len = (lo + a.chunk4 <= a.n4) ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
-    reduce_range<W, Op>(a, par, lo, len, t0, stride, reinterpret_cast<vec_t*>(res_ptr(a.data[a.rank], a.cap, par)));
-    peer_barrier<W>(a, 1, target, failed);
+    reduce_range<W, Op>(a, par, lo, len, t0, stride, reinterpret_cast<vec_t*>(res_ptr(a.data[a.rank], a.cap, par)),
+                        bad);
+    peer_barrier<W>(a, 1, target, failed, &s_bad);
+    bad = s_bad != 0;
     // 3. gather every chunk from its owner's res[par] (W loads in flight; own chunk already in out)
     for (int64_t i = t0; i < a.chunk4; i += stride) {
       vec_t v[W];
@@ -253,7 +266,7 @@ __global__ void __launch_bounds__(kThreads) peer_allreduce_kernel(Args a) {
 #pragma unroll
       for (int q = 0; q < W; ++q) {
         const int64_t g = (int64_t)q * a.chunk4 + i;
-        if (q != a.rank && g <= last) a.out[g] = v[q];
+        if (q != a.rank && g <= last) a.out[g] = bad ? Op::nan_vec() : v[q];
       }
     }
   }
@@ -323,6 +336,13 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_b
   hip_check(hipExtMallocWithFlags(&c, 256, hipDeviceMallocUncached), "hipExtMallocWithFlags(ctrl)");
   ctrl_ = static_cast<uint32_t*>(c);
   hip_check(hipMemset(ctrl_, 0, 256), "hipMemset");
+  void* eh = nullptr;
+  hip_check(hipHostMalloc(&eh, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc(err)");
+  err_host_ = static_cast<volatile uint32_t*>(eh);
+  std::memset(eh, 0, 64);
+  void* ed = nullptr;
+  hip_check(hipHostGetDevicePointer(&ed, eh, 0), "hipHostGetDevicePointer(err)");
+  err_dev_ = static_cast<uint32_t*>(ed);
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_[rank_] = region_;
   peer_flags_[rank_] = flags_;
@@ -349,6 +369,9 @@ void PeerAllReduce::close() {
   (void)hipFree(region_);
   (void)hipFree(flags_);
   (void)hipFree(ctrl_);
+  if (err_host_ != nullptr) (void)hipHostFree(const_cast<uint32_t*>(err_host_));
+  err_host_ = nullptr;
+  err_dev_ = nullptr;
   region_ = nullptr;
   flags_ = nullptr;
   ctrl_ = nullptr;
@@ -396,6 +419,7 @@ void PeerAllReduce::launch(uintptr_t in, uintptr_t out, int64_t count, float sca
   a.in = reinterpret_cast<const vec_t*>(in);
   a.out = reinterpret_cast<vec_t*>(out);
   a.ctrl = ctrl_;
+  a.err_host = err_dev_;
   a.n4 = count / per_vec;
   a.tail = count - a.n4 * per_vec;
   a.cap = cap_;
@@ -439,6 +463,7 @@ std::string PeerAllReduce::device_args() const {
     d.data[p] = p < world_ ? peers_[p] : nullptr;
   }
   d.ctrl = ctrl_;
+  d.err_host = err_dev_;
   d.cap = cap_;
   d.timeout = timeout_ticks_;
   d.rank = rank_;
@@ -458,6 +483,7 @@ void PeerAllReduce::device_probe_f32(uintptr_t in, uintptr_t out, int64_t count,
     d.data[p] = p < world_ ? peers_[p] : nullptr;
   }
   d.ctrl = ctrl_;
+  d.err_host = err_dev_;
   d.cap = cap_;
   d.timeout = timeout_ticks_;
   d.rank = rank_;
@@ -478,9 +504,15 @@ int64_t PeerAllReduce::error() {
   return v;
 }
 
+int64_t PeerAllReduce::error_async() const {
+  return err_host_ != nullptr ? (int64_t)*err_host_ : 0;
+}
+
 void PeerAllReduce::reset_error() {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipMemset(ctrl_ + 2, 0, 4), "hipMemset");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (err_host_ != nullptr) *err_host_ = 0;
 }
 
 }  // namespace pde

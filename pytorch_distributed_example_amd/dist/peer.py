@@ -130,6 +130,11 @@ class PeerAllReduce:
     def error(self) -> int:
         return int(self.native.error()) if self.native is not None else 0
 
+    def error_async(self) -> int:
+        """Time-out latch as mirrored to host memory by the kernels: no device synchronisation (a call
+        still queued has not reported yet).  After a time-out every call writes NaN, never a partial sum."""
+        return int(self.native.error_async()) if self.native is not None else 0
+
     def _self_test(self):
         """Both algorithms of the host kernel (f32 and bf16, ragged sizes) and the device-side protocol
         of pde_peer_dev.h (f32, one- and two-shot), against the exact answer.  Every call gets data of

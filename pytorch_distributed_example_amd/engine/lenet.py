@@ -81,13 +81,19 @@ class LeNetTrainStep:
         #   "defer" (W = 1): the conv backward leaves 16 conv2 slabs (plain stores) and 16 conv1 replicas
         #           (float atomics) in the flat buffer; the optimizer's fold blocks sum them in fixed order
         #           -- no reduction seam on the chain (measured: an in-launch fold + Adam is 2-3 us slower);
-        #   "fold"  (comm path): the last-arriving blocks of the conv backward fold them inside the launch,
-        #           conv2 slabs in group order and conv1 as int64 fixed-point sums (order-free), so the
-        #           all-reduced conv bucket is exactly the conv parameters and bit-reproducible.
-        # PDE_LENET_BWD_MODE=fold forces the comm-path reduction at W = 1 (A/B runs, tests).
+        #   "ext"   (comm path default): the conv backward stores 16 conv2 slabs and one conv1 partial per
+        #           image with plain stores (no atomics, no arrival tickets), and a small fold launch
+        #           (k_conv_grad_fold) sums them in fixed order into the canonical slots, so the
+        #           all-reduced conv bucket is exactly the conv parameters and bit-reproducible
+        #           (round 3's in-launch "fold" cost 4.4 us on the chain: profiles/r3_lenet/phases_fold.txt);
+        #   "fold"  the in-launch reduction (last-arriving W block per k slice; conv1 as int64 fixed-point
+        #           sums): used by the "fused" schedules, whose peer side blocks live in that kernel.
+        # PDE_LENET_BWD_MODE=fold|ext forces a comm-path reduction at W = 1 (A/B runs, tests).
         mode = os.environ.get("PDE_LENET_BWD_MODE", "defer")
-        if self.comm_on:
-            mode = "fold"
+        if mode not in ("defer", "fold", "ext"):
+            raise ValueError(f"PDE_LENET_BWD_MODE must be 'defer', 'fold' or 'ext', not {mode!r}")
+        if self.comm_on and mode == "defer":
+            mode = "ext"
         self.bwd_mode = mode if self.v2 else "v1"
         dev = self.device
         named = [(n, tuple(p.shape)) for n, p in net.named_parameters()]
@@ -126,6 +132,7 @@ class LeNetTrainStep:
             assert o["conv2.weight"] == c1 + C1_STRIDE
             self.slab = torch.zeros(C2_NREP * C2_STRIDE, device=dev, dtype=torch.float32)
             self.c1part = torch.zeros(C1_NREP * C1_STRIDE, device=dev, dtype=torch.float32)   # unused in fold mode
+            self.c1img = torch.zeros(self.B * 520, device=dev, dtype=torch.float32)          # ext mode
             self.zero_view = None
         else:
             assert self.layout.slots["conv1.grad_replicas"].offset == c1 + C1_STRIDE
@@ -246,11 +253,18 @@ class LeNetTrainStep:
         if fused_fc_route is not None:
             kw.update(peer_dev=self._peer_device_args(), ar_buf=self.bucket_grads[0],
                       ar_two=int(fused_fc_route == "peer2"))
-        kw["defer"] = int(self.bwd_mode == "defer")
+        # the fused schedules' peer side blocks live in the in-launch "fold" kernel variant
+        mode = "fold" if fused_fc_route is not None else self.bwd_mode
+        kw["defer"] = {"fold": 0, "defer": 1, "ext": 2}[mode]
+        if mode == "ext":
+            kw["c1img"] = self.c1img
         o = self.off
         self.K.lenet_conv_bwd2(self.Xb[q], self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B, self.slab,
                                self.c1rep, self.c1part, self.tick, self.grads, o["conv1.weight"], o["conv1.bias"],
                                o["conv2.weight"], o["conv2.bias"], **kw)
+        if mode == "ext":      # canonical conv gradients (fixed-order sums) for the conv-bucket all-reduce
+            self.K.lenet_conv_grad_fold(self.slab, self.c1img, B, self.grads, o["conv1.weight"], o["conv1.bias"],
+                                        o["conv2.weight"], o["conv2.bias"])
 
     def _launch(self, B: int):
         """One step on the current stream: conv_fwd -> fc1 -> head -> fc_bwd -> conv_bwd -> opt.

@@ -37,8 +37,15 @@ Reduction routes (``reduce_route``; bf16 / fp16 gradients):
 ``"auto"`` (default) starts on ``peer`` when the peer path set up on every rank, else ``fp32`` for
 bf16 / fp16 gradients, else ``param``; ``tune_bucket_cap`` times whole training steps per
 (cap, route) on the node and keeps the fastest precise one.  ``PDE_DDP_REDUCE_DTYPE=param`` forces
-torch's behaviour.  (The older ``reduce_dtype=torch.float32`` argument selects ``fp32``.)  Staging
-buffers are allocated on the first bucket that needs them (nothing at world size 1).
+torch's behaviour.  (The older ``reduce_dtype=torch.float32`` argument selects ``fp32``.)  The fp32
+staging buffer is allocated whenever the ``fp32`` route is selected (construction or
+``set_reduce_route``), never inside a backward hook, so a hipGraph capture never allocates it.
+
+Failure detection on the peer route: its barrier waits time out after the process group's timeout
+(as RCCL's watchdog; ``PDE_PEER_TIMEOUT_MS`` overrides), a timed-out call writes NaN instead of a
+partial sum and latches an error word mirrored to host memory, and every later bucket launch and
+every ``_finalize`` reads that word (no device sync) and raises -- ordinary rank skew below the
+timeout (eval or checkpointing on one rank) just waits.
 """
 from __future__ import annotations
 
@@ -113,7 +120,9 @@ class DistributedDataParallel(nn.Module):
             # collective: every rank sets up (or fails) together; any failure -> no peer route anywhere
             from ..dist.peer import PeerAllReduce
             cap = min(int(peer_capacity_mb * (1 << 20)), self.layout.total * named[0][1].element_size())
-            pk = PeerAllReduce(self.process_group, self.device, max(cap, 1 << 16))
+            tmo = os.environ.get("PDE_PEER_TIMEOUT_MS")
+            tmo = int(tmo) if tmo else int(getattr(self.process_group, "timeout_ms", 1800000))
+            pk = PeerAllReduce(self.process_group, self.device, max(cap, 1 << 16), timeout_ms=tmo)
             if pk.ok:
                 self._peer = pk
             else:
@@ -125,6 +134,7 @@ class DistributedDataParallel(nn.Module):
         if reduce_route not in ("peer", "fp32", "param"):
             raise ValueError(f"unknown reduce_route {reduce_route!r}")
         self.reduce_route = reduce_route
+        self._ensure_stage()
         self.set_bucket_cap(bucket_cap_mb)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(n)) for n, p in named]
         self._callback_queued = False
@@ -158,6 +168,21 @@ class DistributedDataParallel(nn.Module):
         if route not in ("peer", "fp32", "param"):
             raise ValueError(route)
         self.reduce_route = route
+        self._ensure_stage()
+
+    def _ensure_stage(self):
+        """fp32 staging (one slot per gradient element, so no bucket's fill races another bucket's
+        in-flight all-reduce or copy-back), allocated outside any hook / graph capture."""
+        if (self._stage is None and self.reduce_route == "fp32" and self.world_size > 1
+                and self._gdt != torch.float32):
+            self._stage = torch.empty(self.layout.total, device=self.device, dtype=torch.float32)
+
+    def check_health(self):
+        """Raise if the xGMI peer route has timed out on this rank (host-mapped latch, no sync)."""
+        if self._peer is not None and self._peer.error_async():
+            raise RuntimeError("DDP: an xGMI peer all-reduce barrier timed out (a peer rank is dead, hung or "
+                               "more than the process-group timeout behind); the gradients of that call are "
+                               "NaN and the communicator is poisoned")
 
     def reduce_routes(self):
         """Routes this DDP can run ("peer" only where the peer path set up on every rank)."""
@@ -216,11 +241,9 @@ class DistributedDataParallel(nn.Module):
             if self.reduce_route == "param" or self._gdt == torch.float32:
                 bk.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
                 return
-            # fp32 staging: one rounding of the all-reduced sum back to the gradient dtype.  One fp32
-            # slot per gradient element (allocated on first use): no bucket's fill can race another
-            # bucket's in-flight all-reduce or copy-back
+            # fp32 staging: one rounding of the all-reduced sum back to the gradient dtype
             if self._stage is None:
-                self._stage = torch.empty(self.layout.total, device=self.device, dtype=torch.float32)
+                raise RuntimeError("fp32 staging buffer missing (route switched without set_reduce_route)")
             st = self._stage[bk.start:bk.end]
             st.copy_(view)
             work = dist.all_reduce(st, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
@@ -238,6 +261,7 @@ class DistributedDataParallel(nn.Module):
         """AVG of one bucket by the xGMI peer kernel (two-shot, fp32 accumulation, one rounding),
         chunked by the peer buffer's capacity, on the group's comm stream after the compute stream."""
         pk = self._peer
+        self.check_health()
         esz = view.element_size()
         chunk = max(8, (pk.capacity_bytes // esz) // 8 * 8)
         n = view.numel()
@@ -266,6 +290,7 @@ class DistributedDataParallel(nn.Module):
             bk.work = None
             bk.pending = len(bk.names)
         self._callback_queued = False
+        self.check_health()
 
     # ------------------------------------------------------------------ misc
     def zero_grad(self, set_to_none: bool = False):

@@ -332,6 +332,41 @@ def case_ddp_peer_bf16(cap_mb="32"):
     dist.destroy_process_group()
 
 
+def case_ddp_peer_skew(sleep_s="6", steps="4"):
+    """rank 1 sleeps ``sleep_s`` before one backward.  Past the peer barrier
+    timeout (PDE_PEER_TIMEOUT_MS, set by the test) the timed-out call must write NaN and DDP must
+    raise at the next bucket launch / finalize -- never return plausible partial sums; below it the
+    ranks just wait and stay bit-identical."""
+    import time
+
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    dev = _shared_gpu_init()
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.Linear(128, 32)).to(dev)
+    ddp = DistributedDataParallel(net, bucket_cap_mb=0.01, reduce_route="peer")
+    assert ddp.reduce_route == "peer", ddp.peer_reason
+    x = torch.randn(16, 64, generator=torch.Generator().manual_seed(R)).to(dev)
+    raised, nan_seen, done = None, False, 0
+    for step in range(int(steps)):
+        try:
+            ddp.zero_grad()
+            if step == 1 and R == 1:
+                time.sleep(float(sleep_s))
+            ddp(x).pow(2).sum().backward()
+            torch.cuda.synchronize()
+            nan_seen = nan_seen or any(not bool(torch.isfinite(p.grad).all()) for p in net.parameters())
+            done += 1
+        except RuntimeError as e:
+            raised = str(e)[:200]
+            break
+    bits = [int(p.grad.view(torch.int32).to(torch.int64).sum().item()) for p in net.parameters()]
+    emit({"rank": R, "raised": raised, "nan_seen": nan_seen, "steps_done": done, "bits": bits,
+          "err": ddp._peer.error_async() if ddp._peer is not None else -1})
+    if raised is None:
+        dist.destroy_process_group()
+
+
 def case_manual_average(backend="gloo", steps="4"):
     """The reference's path: per-parameter all_reduce SUM / W after backward."""
     from pytorch_distributed_example_amd.models import build_net

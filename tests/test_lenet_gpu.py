@@ -278,13 +278,14 @@ def test_engine_v2_tracks_v1():
     assert abs(res[1][1][0] - res[0][1][0]) <= 1e-3 * abs(res[0][1][0]) + 1e-3
 
 
-def test_engine_v2_bit_reproducible(monkeypatch):
-    """Verdict r2 item 6: with the in-launch reduction of the comm path ("fold") the conv weight
-    gradients are reduced in a fixed order -- conv2: 16 slabs summed in group order by the
-    last-arriving block; conv1: int64 fixed-point sums, order-free -- so two identical runs give
-    bit-identical parameters, gradients and moments.  (The W = 1 default "defer" keeps conv1's float
-    atomics into 16 replicas: fastest, reproducible to rounding only.)"""
-    mode = "fold"
+@pytest.mark.parametrize("mode", ["fold", "ext"])
+def test_engine_v2_bit_reproducible(monkeypatch, mode):
+    """Verdict r2 item 6: both comm-path reductions reduce the conv weight gradients in a fixed
+    order -- "fold" (in-launch): conv2 slabs summed in group order by the last-arriving block, conv1
+    as int64 fixed-point sums; "ext" (round 4 default): slabs and per-image conv1 partials stored
+    plainly, summed in fixed order by k_conv_grad_fold -- so two identical runs give bit-identical
+    parameters, gradients and moments.  (The W = 1 default "defer" keeps conv1's float atomics into
+    16 replicas: fastest, reproducible to rounding only.)"""
     monkeypatch.setenv("PDE_LENET_BWD_MODE", mode)
     B, n = 128, 8 * 128
     x, y = _batch(n, seed=31)
@@ -310,7 +311,7 @@ def test_engine_bwd_modes_agree(monkeypatch):
     B, n = 128, 6 * 128
     x, y = _batch(n, seed=33)
     res = []
-    for mode in ("defer", "fold"):
+    for mode in ("defer", "fold", "ext"):
         monkeypatch.setenv("PDE_LENET_BWD_MODE", mode)
         net = build_net(seed=13, device=DEV)
         eng = LeNetTrainStep(net, batch_size=B)
@@ -321,3 +322,29 @@ def test_engine_bwd_modes_agree(monkeypatch):
         torch.cuda.synchronize()
         res.append(torch.cat([p.detach().reshape(-1) for p in net.parameters()]))   # layouts differ by mode
     _mostly_close(res[1], res[0], 1e-7, 2e-5, "fold vs defer")
+    _mostly_close(res[2], res[0], 1e-7, 2e-5, "ext vs defer")
+
+
+@pytest.mark.parametrize("mode", ["fold", "ext"])
+def test_engine_comm_modes_propagate_nonfinite(monkeypatch, mode):
+    """a non-finite gradient must stay non-finite through the comm-path reductions (the
+    int64 fixed-point conv1 fold used to turn NaN into a finite garbage value)."""
+    monkeypatch.setenv("PDE_LENET_BWD_MODE", mode)
+    B, n = 128, 2 * 128
+    x, y = _batch(n, seed=35)
+    net = build_net(seed=14, device=DEV)
+    with torch.no_grad():
+        net.fc2.bias[0] = float("nan")      # logits -> dlogits -> every backward operand
+    eng = LeNetTrainStep(net, batch_size=B)
+    eng.bind_dataset(x.to(DEV), y.to(DEV))
+    eng.set_epoch_indices(torch.arange(n, dtype=torch.int32))
+    eng.step()
+    torch.cuda.synchronize()
+    for name in ("conv1.weight", "conv1.bias", "conv2.weight"):
+        assert not bool(torch.isfinite(eng.g[name]).all()), f"{name}: NaN input gave a finite gradient"
+
+
+def test_engine_rejects_unknown_bwd_mode(monkeypatch):
+    monkeypatch.setenv("PDE_LENET_BWD_MODE", "v1")
+    with pytest.raises(ValueError):
+        LeNetTrainStep(build_net(seed=1, device=DEV), batch_size=128)

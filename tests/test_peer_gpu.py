@@ -90,3 +90,22 @@ def test_ddp_peer_route_bf16_one_rounding(cap_mb):
     assert all(r["peer_error"] == 0 for r in res), res
     assert all(r["max_err_ulp"] <= 1.0 for r in res), [r["max_err_ulp"] for r in res]
     assert all(r["bits"] == res[0]["bits"] for r in res)
+
+
+def test_ddp_peer_timeout_raises_instead_of_corrupting():
+    """a rank more than the peer timeout behind poisons the call (NaN, never a
+    partial sum) and the other rank's DDP raises at its next bucket launch."""
+    rc, res, logs = run_ranks("ddp_peer_skew", 2, "6", "4", extra_env={"PDE_PEER_TIMEOUT_MS": "2500"})
+    r0 = res[0]
+    assert r0 is not None, "\n".join(logs)
+    assert r0["raised"] and "timed out" in r0["raised"], r0
+    assert r0["err"] == 1
+    assert r0["nan_seen"] or r0["steps_done"] <= 1, r0
+
+
+def test_ddp_peer_skew_below_timeout_just_waits():
+    """Ordinary rank skew (2 s) below the timeout: no error, replicas bit-identical."""
+    rc, res, logs = run_ranks("ddp_peer_skew", 2, "2", "3", extra_env={"PDE_PEER_TIMEOUT_MS": "60000"})
+    assert rc == 0, "\n".join(logs)
+    assert all(r["raised"] is None and not r["nan_seen"] and r["err"] == 0 for r in res), res
+    assert res[0]["bits"] == res[1]["bits"]
