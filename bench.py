@@ -76,8 +76,9 @@ def build_parser():
                     help="leave HIP's default host wait policy (default: hipDeviceScheduleSpin, utils/hipsched.py)")
     ap.add_argument("--seq-len", type=int, default=1024, help="gpt2: sequence length")
     ap.add_argument("--model-graph", choices=["auto", "on", "off"], default="auto",
-                    help="resnet18: replay the whole training step (fwd + bwd + SGD) as one captured hipGraph; "
-                         "auto = at W=1 (W>1 keeps the eager DDP path with its overlapped bucket all-reduces)")
+                    help="gpt2 / resnet18: replay the whole training step (fwd + bwd + optimizer, with DDP's "
+                         "bucket all-reduces and buffer broadcast captured as graph nodes at W>1) as one "
+                         "hipGraph; auto = on at every world size, off = eager launches")
     ap.add_argument("--bucket-mb", type=str, default="auto",
                     help="gpt2/resnet18: DDP gradient bucket cap in MB, or 'auto' (timed sweep at W>1)")
     return ap

@@ -30,11 +30,35 @@ def _setup():
     from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         with stdout_to_stderr():                  # RCCL's init banner must not precede the JSON line
             dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
             dist.barrier()
     return torch, dist, rank, world, torch.device("cuda", local_rank)
+
+
+def _w1_comm_group(dist):
+    """A one-rank RCCL process group for the W = 1 rehearsal of the DDP communication path."""
+    if not dist.is_initialized():
+        import socket
+
+        from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+
+
+def _comm_figure_wanted(args, world) -> bool:
+    cf = getattr(args, "comm_figure", "auto")
+    return world == 1 and not getattr(args, "force_comm", False) and cf in ("auto", "on")
+
+
+def _graph_wanted(args) -> bool:
+    """Whole-step hipGraph: on by default at every world size (DDP's collectives are captured as graph
+    nodes, parallel/ddp.py); --model-graph off keeps eager launches."""
+    return getattr(args, "model_graph", "auto") in ("auto", "on")
 
 
 def _cap(args) -> float:
@@ -46,7 +70,7 @@ def _tune(ddp, step, world, args, restore=None) -> dict:
     """W > 1 with --bucket-mb auto: time whole steps per (reduction route, bucket cap) (max over ranks),
     keep the fastest; the trial steps' training state is restored.  Reports the chosen cap and route,
     the per-candidate timings and the gradient bytes each rank hands to the all-reduce per step."""
-    if world <= 1:
+    if not getattr(ddp, "comm_on", False):
         return {"bucket_mb": None, "grad_allreduce": "none"}
     from pytorch_distributed_example_amd.parallel import tune_bucket_cap
     out = {}
@@ -86,8 +110,23 @@ def _timed(torch, dist, world, step, warmup, steps):
     return elapsed
 
 
-def bench_gpt2(args):
-    torch, dist, rank, world, dev = _setup()
+def _capture_step(torch, eager_step, sx, sy, ddp=None):
+    """Capture ``eager_step(sx, sy)`` (forward, loss, backward with the DDP bucket collectives,
+    optimizer) into one hipGraph after two allocator / autograd warm-up steps on a side stream."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            eager_step(sx, sy)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = eager_step(sx, sy)
+    return graph, static_loss
+
+
+def _gpt2_run(args, torch, dist, rank, world, dev, comm):
+    """One timed GPT-2 run (``comm``: DDP wrapper with the full communication path, also at W = 1)."""
     from pytorch_distributed_example_amd.models import GPTConfig, build_gpt2
     from pytorch_distributed_example_amd.optim import AdamWMaster
     from pytorch_distributed_example_amd.parallel import DistributedDataParallel
@@ -96,9 +135,8 @@ def bench_gpt2(args):
     T = args.seq_len
     cfg = GPTConfig(block_size=max(1024, T))
     model = build_gpt2(cfg, seed=args.seed, device=dev)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
-    use_graph = getattr(args, "model_graph", "off") == "on" or (getattr(args, "model_graph", "off") == "auto"
-                                                                and world == 1)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args), force_comm=world == 1) if comm else model
+    use_graph = _graph_wanted(args)
     opt = AdamWMaster(model.decay_groups(0.1), lr=6e-4, betas=(0.9, 0.95), max_grad_norm=1.0,
                       capturable=use_graph)
     # a pool of 256 sequences per rank of a learnable synthetic language, sharded by the framework's
@@ -144,25 +182,18 @@ def bench_gpt2(args):
         losses.append(eager_step(sx, sy))
 
     step0 = opt._step
-    extra = _tune(ddp, step, world, args, restore=list(model.parameters()) + opt.state_tensors())
+    extra = _tune(ddp, step, world, args, restore=list(model.parameters()) + opt.state_tensors()) if comm else \
+        {"bucket_mb": None, "grad_allreduce": "none"}
     opt._step = step0
     if getattr(opt, "capturable", False):
         opt.state_tensors()[-1].fill_(float(step0))
     if use_graph:
-        # the whole step (forward, loss, backward, grad-norm clip, AdamW with its device-side step
-        # count) is captured once into a hipGraph and replayed: ~340 launches per step leave the host
-        # and the inter-kernel gaps shrink.  Each step gathers its batch into the static input first
-        # (inside the timed region).
+        # the whole step (forward, loss, backward with the DDP bucket all-reduces, grad-norm clip, AdamW
+        # with its device-side step count) is captured once into a hipGraph and replayed: ~340 launches
+        # per step leave the host and the inter-kernel gaps shrink.  Each step gathers its batch into
+        # the static input first (inside the timed region).
         next_batch()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):                      # allocator / autograd warm-up outside the capture
-                eager_step(sx, sy)
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = eager_step(sx, sy)
+        graph, static_loss = _capture_step(torch, eager_step, sx, sy)
 
         def step():                                  # noqa: F811 - the graph-replay step
             next_batch()
@@ -170,29 +201,48 @@ def bench_gpt2(args):
             losses.append(static_loss)
 
         graph.replay()                               # first launch of the graph outside the timed window
-        extra["mode"] = "hipgraph (whole step)"
+        extra["mode"] = "hipgraph (whole step" + (", DDP collectives captured)" if comm else ")")
     else:
         extra["mode"] = "eager"
     elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
-    tokens = args.steps * B * T * world
-    tps = tokens / elapsed
-    flops = model.flops_per_token() * tps
+    if comm:
+        ddp.check_health()
+    return {"elapsed": elapsed, "extra": extra, "B": B, "T": T, "flops_per_token": model.flops_per_token(),
+            "last_loss": float(losses[-1])}
+
+
+def bench_gpt2(args):
+    torch, dist, rank, world, dev = _setup()
+    r = _gpt2_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
+    B, T = r["B"], r["T"]
+    tps = args.steps * B * T * world / r["elapsed"]
+    out = {
+        "metric": "tokens/sec (whole node), GPT-2-small DDP",
+        "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic learnable token sequences (next = 31*prev+7+U[0,4) mod V; loss floor ln 4), "
+                "256 per rank sharded by DistributedSampler, reshuffled per epoch, random-init weights",
+        "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
+                   "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **r["extra"]},
+        "model_tflops_per_gpu": round(r["flops_per_token"] * tps / world / 1e12, 1),
+        "last_loss": round(r["last_loss"], 4),
+    }
+    if _comm_figure_wanted(args, world):
+        # the same step with an RCCL communicator and DDP's whole communication path (bucket all-reduces
+        # captured into the step graph) at W = 1: what the W > 1 path costs besides the wire time
+        try:
+            _w1_comm_group(dist)
+            r2 = _gpt2_run(args, torch, dist, rank, world, dev, comm=True)
+            out["w1_rccl_comm"] = {"value": round(args.steps * B * T / r2["elapsed"], 1),
+                                   "ms_per_step": round(r2["elapsed"] / args.steps * 1e3, 3), **r2["extra"]}
+        except Exception as e:   # noqa: BLE001 - the headline stands; report the secondary failure
+            out["w1_rccl_comm"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         from pytorch_distributed_example_amd.utils.stdio import emit_result
-        emit_result({
-            "metric": "tokens/sec (whole node), GPT-2-small DDP",
-            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic learnable token sequences (next = 31*prev+7+U[0,4) mod V; loss floor ln 4), "
-                    "256 per rank sharded by DistributedSampler, reshuffled per epoch, random-init weights",
-            "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
-                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
-                       "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **extra},
-            "model_tflops_per_gpu": round(flops / world / 1e12, 1),
-            "last_loss": round(float(losses[-1]), 4),
-        })
-    if world > 1:
+        emit_result(out)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -5,11 +5,11 @@ from __future__ import annotations
 
 import json
 
-from bench_models import _cap, _setup, _timed, _tune
+from bench_models import (_cap, _capture_step, _comm_figure_wanted, _graph_wanted, _setup, _timed, _tune,
+                          _w1_comm_group)
 
 
-def bench_resnet18(args):
-    torch, dist, rank, world, dev = _setup()
+def _resnet_run(args, torch, dist, rank, world, dev, comm):
     from pytorch_distributed_example_amd import ops
     from pytorch_distributed_example_amd.models import build_resnet18
     from pytorch_distributed_example_amd.optim import SGDMaster
@@ -17,7 +17,7 @@ def bench_resnet18(args):
 
     B = args.batch_size if args.batch_size != 128 else 256
     model = build_resnet18(seed=args.seed, device=dev)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args)) if world > 1 else model
+    ddp = DistributedDataParallel(model, bucket_cap_mb=_cap(args), force_comm=world == 1) if comm else model
     opt = SGDMaster(model.decay_groups(5e-5), lr=0.1, momentum=0.9)
     # 8 batches per rank of class-conditional synthetic images, sharded by the DistributedSampler
     from pytorch_distributed_example_amd.data import DistributedSampler, synthetic_images
@@ -44,22 +44,14 @@ def bench_resnet18(args):
 
     extra = _tune(ddp, step, world, args,
                   restore=list(model.parameters()) + list(model.buffers()) + opt.state_tensors())
-    use_graph = args.model_graph == "on" or (args.model_graph == "auto" and world == 1)
-    if use_graph:
-        # the whole step (forward, loss, backward, SGD with its flat fp32 master / momentum buffers) is
-        # captured once into a hipGraph and replayed: ~230 kernel launches per step leave the host, and
-        # the ~0.3 ms of launch gaps with them.  Each step copies its batch into the static input first
-        # (inside the timed region).  SGDMaster has no host-side step state, so a replay is exact.
+    if _graph_wanted(args):
+        # the whole step (forward with the DDP buffer broadcast, loss, backward with the bucket
+        # all-reduces, SGD with its flat fp32 master / momentum buffers) is captured once into a hipGraph
+        # and replayed: ~230 kernel launches per step leave the host, and the ~0.3 ms of launch gaps with
+        # them.  Each step copies its batch into the static input first (inside the timed region).
+        # SGDMaster has no host-side step state, so a replay is exact.
         sx, sy = X[:B].clone(), Y[:B].clone()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):                      # allocator / autograd warm-up outside the capture
-                eager_step(sx, sy)
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = eager_step(sx, sy)
+        graph, static_loss = _capture_step(torch, eager_step, sx, sy)
 
         def step():                                  # noqa: F811 - the graph-replay step
             i = it[0] % nb
@@ -70,25 +62,43 @@ def bench_resnet18(args):
             losses.append(static_loss)
 
         graph.replay()                               # first launch of the graph outside the timed window
-        extra["mode"] = "hipgraph (whole step)"
+        extra["mode"] = "hipgraph (whole step" + (", DDP collectives captured)" if comm else ")")
     else:
         extra["mode"] = "eager"
     elapsed = _timed(torch, dist, world, step, args.warmup, args.steps)
-    ips = args.steps * B * world / elapsed
+    if comm:
+        ddp.check_health()
+    return {"elapsed": elapsed, "extra": extra, "B": B, "last_loss": float(losses[-1])}
+
+
+def bench_resnet18(args):
+    torch, dist, rank, world, dev = _setup()
+    r = _resnet_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
+    B = r["B"]
+    ips = args.steps * B * world / r["elapsed"]
+    out = {
+        "metric": "images/sec (whole node), ResNet-18 bf16 DDP",
+        "value": round(ips, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic class-conditional 3x224x224 images (class prototype + noise), 8 batches per rank "
+                "sharded by DistributedSampler, random-init weights",
+        "config": {"model": "ResNet-18 (11.69M params, torchvision layout)", "global_batch": B * world,
+                   "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
+                   "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", **r["extra"],
+                   "memory_format": "channels_last"},
+        "last_loss": round(r["last_loss"], 4),
+    }
+    if _comm_figure_wanted(args, world):
+        try:
+            _w1_comm_group(dist)
+            r2 = _resnet_run(args, torch, dist, rank, world, dev, comm=True)
+            out["w1_rccl_comm"] = {"value": round(args.steps * B / r2["elapsed"], 1),
+                                   "ms_per_step": round(r2["elapsed"] / args.steps * 1e3, 3), **r2["extra"]}
+        except Exception as e:   # noqa: BLE001 - the headline stands; report the secondary failure
+            out["w1_rccl_comm"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         from pytorch_distributed_example_amd.utils.stdio import emit_result
-        emit_result({
-            "metric": "images/sec (whole node), ResNet-18 bf16 DDP",
-            "value": round(ips, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic class-conditional 3x224x224 images (class prototype + noise), 8 batches per rank "
-                    "sharded by DistributedSampler, random-init weights",
-            "config": {"model": "ResNet-18 (11.69M params, torchvision layout)", "global_batch": B * world,
-                       "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
-                       "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", **extra,
-                       "memory_format": "channels_last"},
-            "last_loss": round(float(losses[-1]), 4),
-        })
-    if world > 1:
+        emit_result(out)
+    if dist.is_initialized():
         dist.destroy_process_group()

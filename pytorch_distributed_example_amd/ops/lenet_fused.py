@@ -2,10 +2,13 @@
 
 ``Net.forward`` (/root/reference/mnist/main.py:139-147) is
   relu(conv1) -> maxpool2 -> relu(conv2) -> maxpool2 -> view(-1, 800) -> relu(fc1) -> fc2 -> log_softmax
-and is executed here by the fused kernels of ``csrc/kernels/lenet.hip`` (3 launches forward,
-3 backward).  The function returns log-probabilities exactly like the reference model, so any loss
-can follow it; the training engine (``engine/lenet.py``) additionally fuses the loss and runs the
-whole step without autograd.
+and is executed here by the fused kernels of ``csrc/kernels/lenet_v2.hip`` / ``lenet.hip``: the v2
+conv forward (LDS-DMA weight staging, 8-wave MFMA conv1 + conv2) for every batch size, fc1, the
+one-row-per-block head, and in backward the fc backward plus the v2 conv backward with the "ext"
+reduction (slabs and per-image conv1 partials, folded in fixed order by k_conv_grad_fold) for
+B <= 128; only batches above 128 take lenet.hip's first-generation conv backward.  The function
+returns log-probabilities exactly like the reference model, so any loss can follow it; the training
+engine (``engine/lenet.py``) additionally fuses the loss and runs the whole step without autograd.
 """
 from __future__ import annotations
 
@@ -29,7 +32,24 @@ class LeNetWorkspace:
         self.dZ2 = torch.empty(B * 10, **f32)
         self.dP2m = torch.empty(B * 800, **f32)
         self.rows = torch.arange(B, device=device, dtype=torch.int32)
-        self.Wt2 = torch.empty(500 * 64, **f32)
+        self.Wp = torch.zeros(2 * 72 * 256, **f32)       # v2 conv2 weight image (padding stays zero)
+
+
+_SCRATCH = {}
+
+
+def _bwd2_scratch(device, B):
+    """Reduction scratch of the v2 conv backward ("ext" mode): 16 conv2 slabs, per-image conv1
+    partials, and the fold-mode buffers the kernel signature carries (unused here)."""
+    key = (str(device), B)
+    sc = _SCRATCH.get(key)
+    if sc is None:
+        f32 = dict(device=device, dtype=torch.float32)
+        sc = {"slab": torch.zeros(16 * 25088, **f32), "c1img": torch.zeros(B * 520, **f32),
+              "c1rep": torch.zeros(16 * 576, device=device, dtype=torch.int64),
+              "c1part": torch.zeros(16 * 576, **f32), "tick": torch.zeros(32, device=device, dtype=torch.int32)}
+        _SCRATCH[key] = sc
+    return sc
 
 
 def pack_conv2_weight(w2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -50,9 +70,9 @@ class LeNetFunction(torch.autograd.Function):
         xf = x.detach().reshape(B, 784).contiguous()
         if xf.dtype != torch.float32:
             raise TypeError("LeNet fused path is fp32 (the reference model's dtype)")
-        pack_conv2_weight(w2c, ws.Wt2)
-        K.lenet_conv_fwd(xf, None, None, 0, 0, None, B, w1c.detach().contiguous(), b1c.detach().contiguous(), ws.Wt2,
-                         b2c.detach().contiguous(), ws.P1, ws.A1, ws.P2, ws.A2, None, None, None)
+        K.lenet_pack_w2_v2(w2c.detach().contiguous(), ws.Wp)
+        K.lenet_conv_fwd2(xf, B, w1c.detach().contiguous(), b1c.detach().contiguous(), ws.Wp,
+                          b2c.detach().contiguous(), ws.P1, ws.A1, ws.P2, ws.A2)
         K.lenet_fc1_fwd(ws.P2, B, w1f.detach().contiguous(), b1f.detach().contiguous(), ws.H1, None)
         logp = torch.empty(B, 10, device=dev, dtype=torch.float32)
         dummy = torch.zeros(B, device=dev, dtype=torch.long)
@@ -83,8 +103,15 @@ class LeNetFunction(torch.autograd.Function):
         gw1c, gb1c, gw2c, gb2c, gw1f, gb1f, gw2f, gb2f = views
         K.lenet_fc_bwd(ws.P2, ws.H1, ws.dZ1, ws.dZ2, w1f.detach().contiguous(), B, ws.dP2m, gw1f, gb1f, gw2f, gb2f,
                        None, None, None, None)
-        K.lenet_conv_bwd(xf, ws.rows, ws.P1, ws.A1, ws.dP2m, ws.A2, w2c.detach().contiguous(), B, gw1c, gb1c, gw2c,
-                         gb2c)
+        if B <= 128:
+            sc = _bwd2_scratch(dev, B)
+            c1w, c1b, c2w, c2b = 0, 500, 520, 25520           # flat offsets of the views above
+            K.lenet_conv_bwd2(xf, ws.P1, ws.A1, ws.dP2m, ws.A2, w2c.detach().contiguous(), B, sc["slab"], sc["c1rep"],
+                              sc["c1part"], sc["tick"], grads, c1w, c1b, c2w, c2b, defer=2, c1img=sc["c1img"])
+            K.lenet_conv_grad_fold(sc["slab"], sc["c1img"], B, grads, c1w, c1b, c2w, c2b)
+        else:
+            K.lenet_conv_bwd(xf, ws.rows, ws.P1, ws.A1, ws.dP2m, ws.A2, w2c.detach().contiguous(), B, gw1c, gb1c,
+                             gw2c, gb2c)
         return None, gw1c, gb1c, gw2c, gb2c, gw1f, gb1f, gw2f, gb2f
 
 

@@ -41,6 +41,16 @@ torch's behaviour.  (The older ``reduce_dtype=torch.float32`` argument selects `
 staging buffer is allocated whenever the ``fp32`` route is selected (construction or
 ``set_reduce_route``), never inside a backward hook, so a hipGraph capture never allocates it.
 
+hipGraph capture (whole-step graphs at W > 1, ``bench.py --model gpt2|resnet18``): every collective
+of a step is issued on the GPU -- bucket all-reduces from the hooks on the group's comm stream with
+event edges back to the compute stream (RCCL or the peer kernel, whose call counter lives on the
+device), the finalize step only makes the compute stream wait on those events, and the per-forward
+buffer broadcast is ONE collective: RCCL broadcast, or, on a host-only control group (ranks sharing a
+GPU), the peer kernel summing the source rank's buffers with zeros from every other rank (exact).  So
+capturing ``forward + backward + optimizer.step()`` records the communication as graph nodes and a
+replay runs it without Python; ``check_health()`` after replays reports a peer time-out.
+``force_comm=True`` runs the whole communication path at world size 1 (the W = 1 rehearsal figure).
+
 Failure detection on the peer route: its barrier waits time out after the process group's timeout
 (as RCCL's watchdog; ``PDE_PEER_TIMEOUT_MS`` overrides), a timed-out call writes NaN instead of a
 partial sum and latches an error word mirrored to host memory, and every later bucket launch and
@@ -75,7 +85,7 @@ class DistributedDataParallel(nn.Module):
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: float = 25.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  static_graph: bool = False, init_sync: bool = True, reduce_dtype="auto",
-                 reduce_route: str = "auto", peer_capacity_mb: float = 32.0):
+                 reduce_route: str = "auto", peer_capacity_mb: float = 32.0, force_comm: bool = False):
         super().__init__()
         self.module = module
         if process_group is None and not dist.is_initialized():
@@ -83,6 +93,8 @@ class DistributedDataParallel(nn.Module):
         else:
             self.process_group = process_group if process_group is not None else dist.get_default_group()
             self.world_size = dist.get_world_size(self.process_group)
+        # comm_on: the bucket all-reduces run (W > 1, or W = 1 with force_comm and a process group)
+        self.comm_on = self.world_size > 1 or (bool(force_comm) and self.process_group is not None)
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True
         self.find_unused_parameters = find_unused_parameters
@@ -112,9 +124,10 @@ class DistributedDataParallel(nn.Module):
         elif reduce_dtype != "auto" and reduce_dtype != gdt:
             reduce_route = "fp32"
         self._stage = None
+        self._bcast = None
         self._peer = None
         self.peer_reason = ""
-        want_peer = (reduce_route in ("auto", "peer") and self.world_size > 1 and self.device.type == "cuda"
+        want_peer = (reduce_route in ("auto", "peer") and self.comm_on and self.device.type == "cuda"
                      and gdt in (torch.bfloat16, torch.float32) and os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0")
         if want_peer:
             # collective: every rank sets up (or fails) together; any failure -> no peer route anywhere
@@ -173,7 +186,7 @@ class DistributedDataParallel(nn.Module):
     def _ensure_stage(self):
         """fp32 staging (one slot per gradient element, so no bucket's fill races another bucket's
         in-flight all-reduce or copy-back), allocated outside any hook / graph capture."""
-        if (self._stage is None and self.reduce_route == "fp32" and self.world_size > 1
+        if (self._stage is None and self.reduce_route == "fp32" and self.comm_on
                 and self._gdt != torch.float32):
             self._stage = torch.empty(self.layout.total, device=self.device, dtype=torch.float32)
 
@@ -196,11 +209,40 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *inputs, **kwargs):
-        if self.broadcast_buffers and self.world_size > 1:
+        if self.broadcast_buffers and self.comm_on:
             bufs = list(self.module.buffers())
             if bufs:      # e.g. BatchNorm running stats: one coalesced broadcast per dtype, not one per buffer
-                dist.broadcast_coalesced(bufs, self.process_group.ranks[0], group=self.process_group)
+                self._broadcast_buffers(bufs)
         return self.module(*inputs, **kwargs)
+
+    def _broadcast_buffers(self, bufs):
+        """Rank-0 buffers to every rank with collectives that stay on the GPU (hipGraph-capturable):
+        RCCL broadcast when the group has it; otherwise (host-only control group, ranks sharing a GPU)
+        the peer all-reduce of a flat fp32 image that only the source rank fills -- x + 0 + ... + 0 is
+        exactly x.  Integer buffers (BatchNorm's num_batches_tracked) ride along as fp32 (exact below
+        2^24).  Without either, the host-staged broadcast (not capturable)."""
+        g = self.process_group
+        src = g.ranks[0]
+        if getattr(g, "rccl", None) is not None or self._peer is None or bufs[0].device.type != "cuda":
+            dist.broadcast_coalesced(bufs, src, group=g)
+            return
+        if self._bcast is None or self._bcast.numel() != sum(b.numel() for b in bufs):
+            self._bcast = torch.empty(max(8, sum(b.numel() for b in bufs)), device=self.device, dtype=torch.float32)
+        flat = self._bcast
+        o = 0
+        if g.rank() == 0:
+            for b in bufs:
+                flat[o:o + b.numel()].copy_(b.reshape(-1))
+                o += b.numel()
+            flat[o:].zero_()
+        else:
+            flat.zero_()
+        self._peer.native.all_reduce_f32(flat.data_ptr(), flat.data_ptr(), flat.numel(), 1.0, 0,
+                                         torch.cuda.current_stream(self.device).cuda_stream)
+        o = 0
+        for b in bufs:
+            b.copy_(flat[o:o + b.numel()].view_as(b))
+            o += b.numel()
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -221,7 +263,7 @@ class DistributedDataParallel(nn.Module):
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)          # autograd replaced the view (e.g. after zero_grad(set_to_none))
                 p.grad = v
-            if not self.require_backward_grad_sync or self.world_size == 1:
+            if not self.require_backward_grad_sync or not self.comm_on:
                 return
             if not self._callback_queued:
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)

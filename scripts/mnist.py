@@ -12,7 +12,8 @@ rank-0 broadcast), every local rank on GPU 0 (one GPU per local rank).  Kept qui
 
 Additive flags: --engine {auto,fused,autograd}, --ddp {on,off} (off = the reference's per-parameter
 ``average_gradients``), --model {net,mlp}, --optimizer {adam,sgd}, --seed, --train-size,
---test-size, --save/--resume (state_dict compatible), --cprofile PATH, --metrics PATH (JSONL),
+--test-size, --save/--resume (state_dict compatible), --cprofile PATH (default ./stats, like the
+reference's always-on cProfile wrapper; --no-cprofile turns it off), --metrics PATH (JSONL),
 --log-rank0-only, --no-graph, --set-epoch.
 """
 import argparse
@@ -185,7 +186,10 @@ def build_parser():
     parser.add_argument('--test-size', type=int, default=10000)
     parser.add_argument('--save', type=str, default=None)
     parser.add_argument('--resume', type=str, default=None)
-    parser.add_argument('--cprofile', type=str, default=None, help='write a pstats file (rank-suffixed)')
+    parser.add_argument('--cprofile', type=str, default='stats',
+                        help="pstats file of the whole run (reference: cProfile.run('main()', 'stats'), always on); "
+                             "rank-suffixed when several ranks share a directory")
+    parser.add_argument('--no-cprofile', action='store_true', help='run without the cProfile wrapper')
     parser.add_argument('--metrics', type=str, default=None, help='append per-epoch JSONL metrics (rank 0)')
     parser.add_argument('--log-rank0-only', action='store_true')
     parser.add_argument('--no-graph', action='store_true', help='fused engine: launch eagerly (no hipGraph)')
@@ -211,8 +215,9 @@ def main(argv=None):
 
 if __name__ == '__main__':
     argv = sys.argv[1:]
-    if '--cprofile' in argv:
-        path = argv[argv.index('--cprofile') + 1]
+    # like the reference (main.py:241-242) every run is profiled into ./stats unless --no-cprofile
+    if '--no-cprofile' not in argv and '-h' not in argv and '--help' not in argv:
+        path = argv[argv.index('--cprofile') + 1] if '--cprofile' in argv else 'stats'
         rank = os.environ.get("RANK")
         if '-r' in argv or '--rank' in argv:
             k = argv.index('-r') if '-r' in argv else argv.index('--rank')

@@ -601,6 +601,107 @@ def case_ddp_model(model="gpt2", steps="3"):
     dist.destroy_process_group()
 
 
+def case_ddp_graph(model="gpt2", steps="3"):
+    """Verdict r3 next 3: the whole DDP training step (forward with the buffer broadcast, backward with
+    the bucket all-reduces over the xGMI peer route, optimizer) captured as ONE hipGraph at W > 1 and
+    replayed must train exactly like the eager DDP step -- same parameters bit for bit, replicas
+    identical.  W ranks share cuda:0 (gloo control group, peer kernel for every collective)."""
+    from pytorch_distributed_example_amd import ops
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    dev = _shared_gpu_init()
+    g = torch.Generator().manual_seed(77)
+    n = int(steps)
+    if model == "gpt2":
+        from pytorch_distributed_example_amd.models import GPTConfig, build_gpt2
+        from pytorch_distributed_example_amd.optim import AdamWMaster
+        cfg = GPTConfig(block_size=128, vocab_size=1000, padded_vocab=1024, n_layer=2, n_head=2, n_embd=128)
+        net = build_gpt2(cfg, seed=5 + R, device=dev)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=0.5)
+        opt = AdamWMaster(net.decay_groups(0.1), lr=3e-3, max_grad_norm=1.0, capturable=True)
+        data = torch.randint(0, cfg.vocab_size, (n, 2 * W, 129), generator=g)
+        sx = torch.empty(2, 128, device=dev, dtype=torch.long)
+        sy = torch.empty(2, 128, device=dev, dtype=torch.long)
+
+        def load(i):
+            b = data[i, 2 * R:2 * R + 2].to(dev)
+            sx.copy_(b[:, :-1])
+            sy.copy_(b[:, 1:])
+
+        def loss_fn():
+            return ddp(sx, sy)
+    else:
+        from pytorch_distributed_example_amd.models import build_resnet18
+        from pytorch_distributed_example_amd.optim import SGDMaster
+        net = build_resnet18(num_classes=10, seed=5 + R, device=dev)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=4.0)
+        opt = SGDMaster(net.decay_groups(5e-5), lr=0.05, momentum=0.9)
+        xs = torch.randn(n, 4 * W, 3, 64, 64, generator=g)
+        ys = torch.randint(0, 10, (n, 4 * W), generator=g)
+        sx = torch.empty(4, 3, 64, 64, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        sy = torch.empty(4, device=dev, dtype=torch.long)
+
+        def load(i):
+            sx.copy_(xs[i, 4 * R:4 * R + 4].to(dev, torch.bfloat16))
+            sy.copy_(ys[i, 4 * R:4 * R + 4].to(dev))
+
+        def loss_fn():
+            return ops.cross_entropy(ddp(sx), sy)
+    assert ddp.reduce_route == "peer", ddp.peer_reason
+    ones = torch.ones((), device=dev, dtype=torch.float32)
+
+    def step():
+        opt.zero_grad()
+        loss = loss_fn()
+        loss.backward(ones)
+        opt.step()
+        return loss.detach()
+
+    state = list(net.parameters()) + list(net.buffers()) + opt.state_tensors()
+    snap = [t.detach().clone() for t in state]
+    step0 = getattr(opt, "_step", None)
+
+    def restore():
+        with torch.no_grad():
+            for t, s0 in zip(state, snap):
+                t.copy_(s0)
+        if step0 is not None:
+            opt._step = step0
+
+    def bits():
+        torch.cuda.synchronize()
+        return [int(t.detach().contiguous().view(torch.uint8).to(torch.int64).sum().item()) for t in state]
+
+    eager_losses = []
+    for i in range(n):
+        load(i)
+        eager_losses.append(float(step()))
+    eager_bits = bits()
+    restore()
+    load(0)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    restore()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = step()
+    graph_losses = []
+    for i in range(n):
+        load(i)
+        graph.replay()
+        graph_losses.append(float(static_loss))
+    graph_bits = bits()
+    ddp.check_health()
+    emit({"rank": R, "eager_bits": eager_bits, "graph_bits": graph_bits, "eager_losses": eager_losses,
+          "graph_losses": graph_losses, "peer_error": ddp._peer.error()})
+    dist.destroy_process_group()
+
+
 def case_torch_backend(device="cpu"):
     """Reference-style code on ``torch.distributed`` itself with the framework registered as the
     c10d backend "pde": the toy's per-step new_group + deprecated reduce_op loop, the usual

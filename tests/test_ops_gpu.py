@@ -191,7 +191,8 @@ def test_engine_comm_world1_matches_no_comm(mode):
 
 def test_mnist_script_fused_gpu():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/mnist.py"), "-s", "1", "--epochs", "2",
-                          "--train-size", "4096", "--test-size", "1024", "--eval"], capture_output=True, text=True,
+                          "--train-size", "4096", "--test-size", "1024", "--eval", "--no-cprofile"],
+                         capture_output=True, text=True,
                          timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stdout + out.stderr
     lines = out.stdout.splitlines()

@@ -109,3 +109,15 @@ def test_ddp_peer_skew_below_timeout_just_waits():
     assert rc == 0, "\n".join(logs)
     assert all(r["raised"] is None and not r["nan_seen"] and r["err"] == 0 for r in res), res
     assert res[0]["bits"] == res[1]["bits"]
+
+
+@pytest.mark.parametrize("model", ["gpt2", "resnet"])
+def test_ddp_graph_replay_matches_eager(model):
+    """Verdict r3 next 3: capture-safe DDP -- the whole DDP step replayed from one hipGraph at W = 2
+    (peer route, ranks sharing the GPU) is bit-identical to the eager DDP step, replicas identical."""
+    rc, res, logs = run_ranks("ddp_graph", 2, model, "3", extra_env={"PDE_PEER_TIMEOUT_MS": "120000"})
+    assert rc == 0, "\n".join(logs)
+    for r in res:
+        assert r["peer_error"] == 0
+        assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])
+    assert res[0]["graph_bits"] == res[1]["graph_bits"], "replicas diverged"

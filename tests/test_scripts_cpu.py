@@ -51,6 +51,8 @@ def test_toy_via_launcher():
 def _mnist(args, n=None, timeout=300):
     base = [os.path.join(ROOT, "scripts/mnist.py"), "--no-cuda", "--train-size", "1024", "--test-size", "256",
             "--epochs", "2"] + args
+    if "--cprofile" not in args:
+        base.append("--no-cprofile")          # the default (reference parity) writes ./stats
     cmd = [sys.executable] + (["-m", "pytorch_distributed_example_amd.launch", "-n", str(n)] if n else []) + base
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, env=ENV, timeout=timeout)
     assert out.returncode == 0, out.stdout + out.stderr
