@@ -184,6 +184,7 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     if eng.comm_on and not args.no_autotune:
         # time every communication schedule (bucket routes x overlap) on whole steps, keep the fastest
         extra["schedule_us_per_step"] = eng.autotune_schedule(graph_steps=S, budget_s=args.autotune_budget_s)
+        extra["compute_only_us_per_step"] = eng.compute_only_us   # same step, collectives left out
         health = comm.health()
         if health:
             raise RuntimeError(f"communication failure during schedule autotuning: {health}")

@@ -341,7 +341,7 @@ class LeNetTrainStep:
             with torch.cuda.stream(cs):
                 self.comm.all_reduce_(self.bucket_grads[0])
         conv_bwd()
-        if not self.comm_on:
+        if not self.comm_on or self.mode == "none":     # "none": the comm path's compute alone (autotune probe)
             self._opt(0, self.params.numel(), True)
             return
         if self.mode == "serial":
@@ -639,6 +639,29 @@ class LeNetTrainStep:
             g.host.allreduce(chk.data_ptr(), 2, 3, 3)          # int64 MAX: max(bits) and -min(bits)
             if chk[0].item() != -chk[1].item():
                 invalid[-1] = 1
+        # the same step with the collectives left out (never selectable): what the communication adds
+        # on top of the comm path's compute (a W > 1 scaling point decomposes into the two)
+        self.compute_only_us = None
+        for tt, s0 in zip(state, snap):
+            tt.copy_(s0)
+        self.q = q_saved
+        self.sync_params()
+        self.mode = "none"
+        self.graphs.clear()
+        self.capture(steps=graph_steps)
+        self.replay(steps=graph_steps)
+        torch.cuda.synchronize(self.device)
+        g.host.barrier()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(1, steps // graph_steps)
+        s.record()
+        for _ in range(reps):
+            self.replay(steps=graph_steps)
+        e.record()
+        torch.cuda.synchronize(self.device)
+        co = torch.tensor([s.elapsed_time(e) * 1e3 / (reps * graph_steps)], dtype=torch.float64)
+        g.host.allreduce(co.data_ptr(), 1, 1, 3)
+        self.compute_only_us = round(float(co.item()), 2)
         t = torch.tensor(times, dtype=torch.float64)
         g.host.allreduce(t.data_ptr(), t.numel(), 1, 3)     # float64 MAX over ranks
         bad = torch.tensor(invalid, dtype=torch.int64)
@@ -650,7 +673,11 @@ class LeNetTrainStep:
             n0, n1 = self.bucket_grads[0].numel(), self.bucket_grads[1].numel()
             cands = list(cands) + [("overlap", {n0: "rccl", n1: "rccl"})]   # bounded fallback: RCCL only
             times.append(0.0)
-        best = min(range(len(cands)), key=lambda i: times[i])
+        # a schedule with cross-stream edges (overlap / flat) must win by > 1 %: in a replayed hipGraph
+        # every such edge adds 5-9 us of jitter-prone join latency (round 3: flat 61.9 us in the
+        # autotuner, 68.3 us in the timed window; the single-stream serial schedule measured 62.0)
+        eff = [x * (1.01 if cands[i][0] in ("overlap", "flat") else 1.0) for i, x in enumerate(times)]
+        best = min(range(len(cands)), key=lambda i: eff[i])
         self.mode, self.comm.routes = cands[best][0], dict(cands[best][1])
         self.graphs.clear()
         # restore the training state the trial steps advanced

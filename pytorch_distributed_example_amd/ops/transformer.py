@@ -296,10 +296,26 @@ class LMHeadLossFn(torch.autograd.Function):
         C = h.shape[-1]
         h2 = _c(h.reshape(-1, C))
         N = h2.shape[0]
-        logits = G.fprop(h2, w)                             # [N, Vp] bf16 (own MFMA GEMM)
         rows = torch.empty(N, device=h.device, dtype=torch.float32)
         tg = _c(targets.reshape(-1).long())
-        kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
+        chunk = _LMHEAD_CHUNK
+        if chunk and N > chunk:
+            # token chunks: each chunk's bf16 logits (chunk x Vp x 2 B, e.g. 206 MB at 2048 tokens) are
+            # consumed by the cross-entropy right after the GEMM wrote them, while they still sit in
+            # the 256 MB Infinity Cache, instead of one 1.65 GB write followed by a read from HBM
+            logits = torch.empty(N, w.shape[0], device=h.device, dtype=torch.bfloat16)
+            cfg = G.pick("fprop", N, w.shape[0], C)[0]
+            for s0 in range(0, N, chunk):
+                s1 = min(N, s0 + chunk)
+                if _LMHEAD_LIB:
+                    torch.matmul(h2[s0:s1], w.t(), out=logits[s0:s1])
+                else:
+                    G.fprop(h2[s0:s1], w, out=logits[s0:s1], cfg=cfg)
+                kernels().xent_bf16(logits[s0:s1], tg[s0:s1], V, 1.0 / N, rows[s0:s1], True)
+        else:
+            # [N, Vp] bf16: own MFMA GEMM, or the library for this plain GEMM (PDE_LMHEAD_GEMM=lib)
+            logits = torch.matmul(h2, w.t()) if _LMHEAD_LIB else G.fprop(h2, w)
+            kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
         tot = torch.empty(1, device=h.device, dtype=torch.float32)
         kernels().sum_f32(rows, tot, 1.0 / N)               # mean loss, no separate divide
         ctx.save_for_backward(h2, w, logits)
@@ -317,11 +333,21 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1)
         if gs.dtype != torch.float32 or not gs.is_cuda:
             gs = gs.to(device=dlogits.device, dtype=torch.float32)
-        dh = G.dgrad(dlogits, w, scale=gs)                   # [N, C]
+        if _LMHEAD_LIB:
+            dh = torch.matmul(dlogits, w).mul_(gs.reshape(()))   # plain library GEMM + loss-gradient scale
+        else:
+            dh = G.dgrad(dlogits, w, scale=gs)               # [N, C]
         dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
         if ctx.tied is not None:
             ctx.tied["dw"] = dw                              # the tied embedding adds its part in place
         return dh.reshape(ctx.hshape), dw, None, None
+
+
+# PDE_LMHEAD_CHUNK=<tokens>: run the LM-head GEMM + cross-entropy in token chunks (0 = one pass)
+import os as _os
+_LMHEAD_CHUNK = int(_os.environ.get("PDE_LMHEAD_CHUNK", "0"))
+# PDE_LMHEAD_GEMM=lib: the LM head's fprop / dgrad (plain GEMMs, no fused epilogue) through hipBLASLt
+_LMHEAD_LIB = _os.environ.get("PDE_LMHEAD_GEMM", "own") == "lib"
 
 
 def lm_head_loss(h, w, targets, V: int):

@@ -62,30 +62,82 @@ def test_bn_eval_mode():
     assert rel_err(y, yr) < 1e-2
 
 
-def test_resnet18_gpu_matches_cpu():
+def _cos(a, b):
+    return F.cosine_similarity(a.detach().double().flatten().cpu(), b.detach().double().flatten().cpu(), dim=0).item()
+
+
+def _nrel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _resnet_parity(break_layer: bool = False):
+    """ResNet-18 bf16 GPU (fused training kernels) vs an fp32 CPU twin with the SAME bf16-representable
+    weights and inputs, at 112 px and B = 32 (layer4's BatchNorm sees 32 x 4 x 4 samples).  Checks the
+    stem output, every BasicBlock output, the logits (relative L2 error per activation), the loss,
+    every parameter gradient (cosine) and the running statistics.  Returns the list of failures."""
     g = build_resnet18(num_classes=10, seed=0, device=dev)
     c = build_resnet18(num_classes=10, seed=0, dtype=torch.float32)
     with torch.no_grad():
         for pc, pg in zip(c.parameters(), g.parameters()):
             pc.copy_(pg.float())
+        if break_layer:              # the deliberately broken model: one block's BN gamma and beta swapped
+            bn = g.layer2[0].bn1
+            w = bn.weight.detach().clone()
+            bn.weight.copy_(bn.bias)
+            bn.bias.copy_(w)
     torch.manual_seed(2)
-    x = torch.randn(8, 3, 64, 64)
-    y = torch.randint(0, 10, (8,))
-    lg = F.cross_entropy(g(x.to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)).float(), y.to(dev))
-    lc = F.cross_entropy(c(x), y)
+    x = torch.randn(32, 3, 112, 112).to(torch.bfloat16).float()
+    y = torch.randint(0, 10, (32,))
+    acts = {"g": {}, "c": {}}
+    hooks = []
+    for tag, m in (("g", g), ("c", c)):
+        hooks.append(m.layer1.register_forward_pre_hook(
+            lambda mod, inp, tag=tag: acts[tag].__setitem__("stem", inp[0].detach())))
+        for i in range(1, 5):
+            for j, blk in enumerate(getattr(m, f"layer{i}")):
+                hooks.append(blk.register_forward_hook(
+                    lambda mod, inp, out, tag=tag, k=f"layer{i}.{j}": acts[tag].__setitem__(k, out.detach())))
+    try:
+        og = g(x.to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        oc = c(x)
+    finally:
+        for h in hooks:
+            h.remove()
+    lg = F.cross_entropy(og.float(), y.to(dev))
+    lc = F.cross_entropy(oc, y)
     lg.backward()
     lc.backward()
-    assert abs(lg.item() - lc.item()) < 5e-2 * max(1.0, lc.item())
-    # bf16 activations through 17 conv+BN layers (BN over 8 x 2 x 2 samples in layer4 at this input
-    # size): the whole-model gradient agreement is loose; test_basic_block_* checks it tightly
-    cos = {n: F.cosine_similarity(pg.grad.float().flatten().cpu(), pc.grad.flatten(), dim=0).item()
-           for (n, pg), pc in zip(g.named_parameters(), c.parameters())}
-    vals = sorted(cos.values())
-    assert vals[0] > 0.8, cos
-    assert vals[len(vals) // 2] > 0.9, cos
+    fails = []
+    acts["g"]["logits"], acts["c"]["logits"] = og, oc
+    for k, ref in acts["c"].items():
+        e = _nrel(acts["g"][k].float(), ref)
+        bound = 4e-2 if k == "logits" else 3e-2        # bf16 storage: ~2^-9 per layer, random-walk growth
+        if not e < bound:
+            fails.append(f"activation {k}: rel L2 err {e:.3e} >= {bound}")
+    if not abs(lg.item() - lc.item()) < 1e-2 * max(1.0, lc.item()):
+        fails.append(f"loss {lg.item():.5f} vs {lc.item():.5f}")
+    for (n, pg), pc in zip(g.named_parameters(), c.parameters()):
+        cs = _cos(pg.grad.float(), pc.grad)
+        if not cs >= 0.99:
+            fails.append(f"grad {n}: cos {cs:.4f}")
     for (n, bg), bc in zip(g.named_buffers(), c.buffers()):
-        if bg.dtype.is_floating_point:
-            assert rel_err(bg, bc) < 3e-2, n
+        if bg.dtype.is_floating_point and not _nrel(bg, bc) < 2e-2:
+            fails.append(f"buffer {n}: rel err {_nrel(bg, bc):.3e}")
+    return fails
+
+
+def test_resnet18_gpu_matches_cpu():
+    """Verdict r3 weak 5 / next 6: whole-model parity at a realistic shape with per-layer bounds."""
+    fails = _resnet_parity()
+    assert not fails, fails
+
+
+def test_resnet18_parity_catches_broken_layer():
+    """The same checks must fail when a single layer is wrong (swapped BN gamma / beta in layer2.0)."""
+    fails = _resnet_parity(break_layer=True)
+    assert fails, "a swapped BatchNorm gamma/beta in one block went unnoticed"
+    assert any("layer2.0" in f for f in fails), fails
 
 
 @pytest.mark.parametrize("stride,cin,cout", [(1, 64, 64), (2, 64, 128), (1, 64, 128)])
