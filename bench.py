@@ -62,7 +62,7 @@ def build_parser():
                     help="wall-clock budget of the schedule autotuner (candidates left untimed past it)")
     ap.add_argument("--prime-replays", type=int, default=3,
                     help="untimed replays of each captured graph before the warm-up steps")
-    ap.add_argument("--clock-warm-ms", type=float, default=20.0,
+    ap.add_argument("--clock-warm-ms", type=float, default=0.0,
                     help="untimed back-to-back training steps (about this many ms of GPU work) right before the "
                          "W warm-up steps, so the timed window starts at the clock a sustained run holds "
                          "(0 = off; PDE_BENCH_CLOCK_WARM_MS overrides)")
@@ -205,12 +205,10 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
 
 
 def _clock_warm(args, eng, run, S):
-    """Untimed back-to-back training steps (``--clock-warm-ms`` of GPU work, enqueued without a host
-    sync) right before the W warm-up steps.  The GPU raises its clock only under sustained load (a
-    20-step window that follows a few ms of idle priming measured ~59 us/step against 55 us/step in
-    a 2000-step run of the same graphs, profiles/r4_lenet/); a timed window that starts after >= 20 ms
-    of continuous steps runs at the steady-state clock.  These are ordinary training steps: nothing in
-    the timed window changes."""
+    """Optional untimed back-to-back training steps (``--clock-warm-ms`` of GPU work, enqueued without
+    a host sync) right before the W warm-up steps, to start the timed window at a sustained-load clock.
+    Off by default: measured on MI355X it did not move the 20-step window (57.3 / 57.5 us/step with
+    20 ms of warm steps vs 56.8 / 57.9 without, same box, profiles/r4_lenet/)."""
     warm_ms = float(os.environ.get("PDE_BENCH_CLOCK_WARM_MS", args.clock_warm_ms))
     if warm_ms <= 0:
         return

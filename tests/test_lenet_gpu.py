@@ -237,8 +237,8 @@ def test_conv_fwd2_matches_v1_and_torch(B):
     w1, b1 = net.conv1.weight.detach().contiguous(), net.conv1.bias.detach().contiguous()
     w2, b2 = net.conv2.weight.detach().contiguous(), net.conv2.bias.detach().contiguous()
     ws1, ws2 = LeNetWorkspace(B, DEV), LeNetWorkspace(B, DEV)
-    pack_conv2_weight(w2, ws1.Wt2)
-    K.lenet_conv_fwd(xd, None, None, 0, 0, None, B, w1, b1, ws1.Wt2, b2, ws1.P1, ws1.A1, ws1.P2, ws1.A2, None, None,
+    Wt2 = pack_conv2_weight(w2)
+    K.lenet_conv_fwd(xd, None, None, 0, 0, None, B, w1, b1, Wt2, b2, ws1.P1, ws1.A1, ws1.P2, ws1.A2, None, None,
                      None)
     Wp = torch.zeros(2 * 72 * 256, device=DEV)
     K.lenet_pack_w2_v2(w2, Wp)

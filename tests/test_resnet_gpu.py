@@ -140,6 +140,28 @@ def test_resnet18_parity_catches_broken_layer():
     assert any("layer2.0" in f for f in fails), fails
 
 
+@pytest.mark.parametrize("O", [10, 1000])
+def test_resnet_head_matches_torch(O):
+    """Pool + FC head (own kernels; 10 classes run on zero-padded weight rows) vs fp32 PyTorch."""
+    from pytorch_distributed_example_amd.ops.resnet import resnet_head
+    torch.manual_seed(9)
+    x = torch.randn(16, 512, 7, 7).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (0.05 * torch.randn(O, 512)).to(dev, torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(O)).to(dev, torch.bfloat16).requires_grad_()
+    xg = x.detach().clone().requires_grad_()
+    y = resnet_head(xg, w, b)
+    dy = torch.randn(16, O).to(dev, torch.bfloat16)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.linear(F.adaptive_avg_pool2d(xr, 1).flatten(1), wr, br)
+    yr.backward(dy.float())
+    assert y.shape == (16, O)
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(xg.grad, xr.grad) < 3e-2
+    assert rel_err(w.grad, wr.grad) < 3e-2
+    assert rel_err(b.grad, br.grad) < 3e-2
+
+
 @pytest.mark.parametrize("stride,cin,cout", [(1, 64, 64), (2, 64, 128), (1, 64, 128)])
 def test_basic_block_matches_cpu(stride, cin, cout):
     """One BasicBlock (with downsample when strided or widening) at a well-conditioned batch, through
@@ -225,17 +247,15 @@ def test_maxpool3s2_unsupported_raises():
         max_pool3s2(torch.randn(2, 3, 8, 8, device=dev, dtype=torch.bfloat16))
 
 
-@pytest.mark.parametrize("case", ["fp32", "channels", "outfeat"])
+@pytest.mark.parametrize("case", ["fp32", "channels"])
 def test_resnet_head_unsupported_raises(case):
     """Verdict r3 weak 6: resnet_head no longer falls back to ATen on GPU tensors it cannot run."""
     from pytorch_distributed_example_amd.ops.resnet import resnet_head
     C, O, dt = (512, 1000, torch.bfloat16)
     if case == "fp32":
         dt = torch.float32
-    elif case == "channels":
-        C = 100
     else:
-        O = 1001
+        C = 100
     x = torch.randn(2, C, 7, 7, device=dev, dtype=dt)
     w = torch.randn(O, C, device=dev, dtype=dt)
     b = torch.zeros(O, device=dev, dtype=dt)
