@@ -337,7 +337,12 @@ class LMHeadLossFn(torch.autograd.Function):
             dh = torch.matmul(dlogits, w).mul_(gs.reshape(()))   # plain library GEMM + loss-gradient scale
         else:
             dh = G.dgrad(dlogits, w, scale=gs)               # [N, C]
-        dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
+        if _LMHEAD_LIB_W:
+            slot = _grad_out(w)
+            dw = torch.matmul(dlogits.t(), h2, out=slot) if slot is not None else torch.matmul(dlogits.t(), h2)
+            dw.mul_(gs.reshape(()))
+        else:
+            dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
         if ctx.tied is not None:
             ctx.tied["dw"] = dw                              # the tied embedding adds its part in place
         return dh.reshape(ctx.hshape), dw, None, None
@@ -346,8 +351,12 @@ class LMHeadLossFn(torch.autograd.Function):
 # PDE_LMHEAD_CHUNK=<tokens>: run the LM-head GEMM + cross-entropy in token chunks (0 = one pass)
 import os as _os
 _LMHEAD_CHUNK = int(_os.environ.get("PDE_LMHEAD_CHUNK", "0"))
-# PDE_LMHEAD_GEMM=lib: the LM head's fprop / dgrad (plain GEMMs, no fused epilogue) through hipBLASLt
-_LMHEAD_LIB = _os.environ.get("PDE_LMHEAD_GEMM", "own") == "lib"
+# The LM head's fprop / dgrad are plain GEMMs (no epilogue to fuse: the cross-entropy needs whole rows),
+# so they run through hipBLASLt where it is faster on MI355X (in-step, one box: 886 vs 864 K tok/s,
+# profiles/r4_gpt2/); PDE_LMHEAD_GEMM=own keeps the framework's GEMM, =lib3 also moves the wgrad.
+_LMHEAD_MODE = _os.environ.get("PDE_LMHEAD_GEMM", "lib")
+_LMHEAD_LIB = _LMHEAD_MODE in ("lib", "lib3")
+_LMHEAD_LIB_W = _LMHEAD_MODE == "lib3"
 
 
 def lm_head_loss(h, w, targets, V: int):

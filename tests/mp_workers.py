@@ -670,7 +670,7 @@ def case_ddp_graph(model="gpt2", steps="3"):
 
     def bits():
         torch.cuda.synchronize()
-        return [int(t.detach().contiguous().view(torch.uint8).to(torch.int64).sum().item()) for t in state]
+        return [int(t.detach().reshape(-1).contiguous().view(torch.uint8).to(torch.int64).sum().item()) for t in state]
 
     eager_losses = []
     for i in range(n):
@@ -697,8 +697,13 @@ def case_ddp_graph(model="gpt2", steps="3"):
         graph_losses.append(float(static_loss))
     graph_bits = bits()
     ddp.check_health()
+    nb = len(list(net.buffers()))
+    npar = len(list(net.parameters()))
     emit({"rank": R, "eager_bits": eager_bits, "graph_bits": graph_bits, "eager_losses": eager_losses,
-          "graph_losses": graph_losses, "peer_error": ddp._peer.error()})
+          "graph_losses": graph_losses, "peer_error": ddp._peer.error(),
+          # torch-DDP semantics: buffers are broadcast at the START of each forward, then updated from
+          # the local batch, so across ranks only parameters and optimizer state must agree
+          "replicated_bits": graph_bits[:npar] + graph_bits[npar + nb:]})
     dist.destroy_process_group()
 
 

