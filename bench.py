@@ -217,17 +217,25 @@ def _clock_warm(args, eng, run, S):
     run(n, S)
 
 
+_BARRIER_T = {}
+
+
 def _device_barrier(comm, dist):
     """Barrier for the window brackets: an RCCL all-reduce of one element + synchronize when the group
     has RCCL (every rank must arrive; the GPU idles for microseconds, not for a host TCP round trip
     that lets the clocks drop before the timed window), else the host barrier."""
     import torch
 
+    if dist.get_world_size() == 1:          # a barrier over one rank is the device synchronize alone
+        torch.cuda.synchronize()
+        return
     rc = comm.group.rccl if comm is not None else None
     if rc is None:
         dist.barrier()
         return
-    t = torch.zeros(1, device=torch.device("cuda", rc.device))
+    t = _BARRIER_T.get(rc.device)
+    if t is None:
+        t = _BARRIER_T[rc.device] = torch.zeros(1, device=torch.device("cuda", rc.device))
     dist.all_reduce(t)
     torch.cuda.synchronize()
 
