@@ -404,3 +404,31 @@ def test_add_layer_norm_residual_unsupported_raises(case):
     w = torch.ones(768, device=dev, dtype=torch.bfloat16)
     with pytest.raises(NotImplementedError):
         add_layer_norm_residual(x, d, w, torch.zeros_like(w))
+
+
+def test_xent_kernel_matches_torch():
+    """Fused softmax-CE over the padded GPT-2 vocab (the 512-thread register-resident kernel): per-row
+    loss and the in-place dlogits vs fp32 torch, incl. a target in the last (masked) chunk, target 0
+    and an ignored row (-1); padding columns get zero gradient."""
+    from pytorch_distributed_example_amd._ext import kernels
+    torch.manual_seed(11)
+    N, V, Vp = 64, 50257, 50304
+    logits = (3 * torch.randn(N, Vp)).to(dev, torch.bfloat16)
+    tg = torch.randint(0, V, (N,), device=dev)
+    tg[0], tg[1], tg[2] = V - 1, 0, -1
+    ref = logits.float()[:, :V]
+    rows = torch.empty(N, device=dev)
+    scale = 1.0 / N
+    L = logits.clone()
+    kernels().xent_bf16(L, tg, V, scale, rows, True)
+    valid = tg >= 0
+    lse = torch.logsumexp(ref, 1)
+    want_loss = torch.where(valid, lse - ref.gather(1, tg.clamp_min(0)[:, None])[:, 0], torch.zeros_like(lse))
+    assert (rows - want_loss).abs().max().item() < 2e-3
+    g = torch.softmax(ref, 1)
+    g[torch.arange(N, device=dev)[valid], tg[valid]] -= 1
+    g = g * scale * valid[:, None].float()
+    got = L.float()
+    assert rel_err(got[:, :V], g) < 1e-2
+    assert got[:, V:].abs().max().item() == 0.0
+    assert got[2].abs().max().item() == 0.0                # ignored row
