@@ -28,6 +28,7 @@
 #include "pde_hip.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "pde_kernels.h"
@@ -54,13 +55,14 @@ constexpr int kL_TOT = kL_W1 + 528;          // 23904 floats = 93 KB
     }                                                                                         \
   } while (0)
 
-template <bool PROF>
+template <bool PROF, bool VALU1>
 __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb, const float* __restrict__ w1,
                                                    const float* __restrict__ b1, const float* __restrict__ Wp,
                                                    const float* __restrict__ b2, float* __restrict__ P1,
                                                    uint8_t* __restrict__ A1, float* __restrict__ P2,
                                                    uint8_t* __restrict__ A2, float* __restrict__ zero_ptr, int zero_n,
                                                    unsigned long long* __restrict__ prof) {
+  constexpr bool conv1_valu = VALU1;
   __shared__ __attribute__((aligned(16))) float smem[kL_TOT];
   const int b = blockIdx.x, ct = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
   PMARK(0);
@@ -76,15 +78,24 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   if (t < kImg / 4) reinterpret_cast<float4*>(smem + kL_IMG + (t / 7) * kImgRow)[t % 7] = xv;
   if (t < 125) reinterpret_cast<float4*>(smem + kL_W1)[t] = wv;
   if (t < 20) smem[kL_W1 + 500 + t] = bv1;
-  // ---- then the conv2 weight image by LDS-DMA: 72 x 1 KB, exactly 9 per wave ----
+  // ---- then the conv2 weight image: 72 x 1 KB, exactly 9 per wave.  conv1_valu: into registers,
+  // written to LDS after conv1 (the LDS-DMA fill ran ~4.6 us from the block start, longer than the
+  // VALU conv1); else by LDS-DMA, which lands under the 3.7 us MFMA conv1 ----
+  float4 wr[9];
   {
     const float* wsrc = Wp + (size_t)ct * kWpHalf;
+    if constexpr (conv1_valu) {
+      // issued after the phase-0 barrier below (inline asm: the compiler would otherwise sink these loads
+      // to their use after conv1, and its vmcnt bookkeeping must not see them before the image wait)
+    } else {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int c = w + 8 * i;
-      __builtin_amdgcn_global_load_lds(wsrc + c * 256 + l * 4, smem + kL_W + c * 256, 16, 0, 0);
+      for (int i = 0; i < 9; ++i) {
+        const int c = w + 8 * i;
+        __builtin_amdgcn_global_load_lds(wsrc + c * 256 + l * 4, smem + kL_W + c * 256, 16, 0, 0);
+      }
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
   // gradient-buffer zeroing (atomic targets of the backward) drains while conv1 computes
   if (zero_ptr) {
     const int nb = gridDim.x * gridDim.y, bid = ct * gridDim.x + b;
@@ -93,7 +104,67 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   // barrier without draining the LDS-DMA (a __syncthreads() would wait vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (conv1_valu) {
+    // conv2 weight image into registers, in flight under conv1 (which touches LDS only); explicitly
+    // waited for (vmcnt(0)) just before the LDS writes after conv1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float* wsrc = Wp + (size_t)ct * kWpHalf + w * 256 + l * 4;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wr[i]) : "v"(wsrc + i * 8 * 256) : "memory");
+  }
   PMARK(1);
+  // ---- phase 1: conv1 (1->20, 5x5) + bias + ReLU + 2x2 max-pool on the VALU ----
+  // 480 threads: thread = (channel c, pooled row ph, half of the row): a 6 x 16 input window in
+  // registers (24 ds_read_b128), the channel's 25 weights, then 6 pooled outputs x 4 sub-positions x
+  // 25 taps = 600 FMAs from registers.  (The 32x32x2 f32 MFMA form padded 20 channels to 32 and 25
+  // taps to 26 -- 1.66x the FMAs at the same per-SIMD f32 rate -- and took 3.7 us of the block.)
+  if constexpr (conv1_valu) {
+    const float* xin = smem + kL_IMG;
+    const float* w1s = smem + kL_W1;
+    float* xs = smem + kL_XS;
+    uint8_t* codes = reinterpret_cast<uint8_t*>(smem + kL_CODE);
+    if (t < 480) {
+      const int c = t / 24, rem = t - c * 24, ph = rem >> 1, hf = rem & 1;
+      float win[6][16];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 v4 = *reinterpret_cast<const float4*>(xin + (2 * ph + r) * kImgRow + 12 * hf + 4 * k);
+          win[r][4 * k + 0] = v4.x;
+          win[r][4 * k + 1] = v4.y;
+          win[r][4 * k + 2] = v4.z;
+          win[r][4 * k + 3] = v4.w;
+        }
+      float wt[25];
+#pragma unroll
+      for (int k = 0; k < 25; ++k) wt[k] = w1s[c * 25 + k];
+      const float bch = w1s[500 + c];
+#pragma unroll
+      for (int pw = 0; pw < 6; ++pw) {
+        float best = 0.f;
+        int code = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int dy = q >> 1, dx = q & 1;
+          float acc = 0.f;
+#pragma unroll
+          for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 5; ++kw) acc = fmaf(win[dy + kh][2 * pw + dx + kw], wt[kh * 5 + kw], acc);
+          const float v = fmaxf(acc + bch, 0.f);
+          if (q == 0 || v > best) {            // first maximum in scan order (ATen)
+            best = v;
+            code = q;
+          }
+        }
+        const int pq = ph * 12 + 6 * hf + pw;
+        xs[c * 144 + pq] = best;
+        codes[c * 144 + pq] = (uint8_t)code;
+      }
+    }
+  } else {
   // ---- phase 1: conv1 (1->20, 5x5) + bias + ReLU + 2x2 max-pool on v_mfma_f32_32x32x2_f32 ----
   // C[m][ch] = sum_tap im2col[m][tap] * W1[ch][tap], m = 4 * pooled_pos + (dy*2+dx): accumulator rows
   // 4g..4g+3 are the 4 sub-positions of one pooled position -> pooled in registers.  (Measured and
@@ -145,6 +216,12 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
         }
       }
     }
+  }
+  }   // conv1_valu
+  if constexpr (conv1_valu) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 9; ++i) *reinterpret_cast<float4*>(smem + kL_W + (w + 8 * i) * 256 + l * 4) = wr[i];
   }
   PMARK(2);
   // conv1 output visible + this wave's LDS-DMA landed, then every wave's (barrier)
@@ -960,12 +1037,22 @@ hipError_t pde_lenet_conv_fwd2(const float* Xb, int B, const float* w1, const fl
                                const float* b2, float* P1, uint8_t* A1, float* P2, uint8_t* A2, float* zero_ptr,
                                int zero_n, hipStream_t st) {
   unsigned long long* prof = pde_lenet_prof_slot(0);
-  if (prof)
-    hipLaunchKernelGGL(k_conv_fwd2<true>, dim3(B, 2), dim3(512), 0, st, Xb, w1, b1, Wp, b2, P1, A1, P2, A2, zero_ptr,
-                       zero_n, prof);
-  else
-    hipLaunchKernelGGL(k_conv_fwd2<false>, dim3(B, 2), dim3(512), 0, st, Xb, w1, b1, Wp, b2, P1, A1, P2, A2, zero_ptr,
-                       zero_n, nullptr);
+  // conv1 on the VALU (default) or on 32x32x2 f32 MFMA tiles (PDE_LENET_CONV1=mfma, A/B runs)
+  static const int valu = [] {
+    const char* e = getenv("PDE_LENET_CONV1");
+    return (e != nullptr && e[0] == 'm') ? 0 : 1;
+  }();
+#define PDE_CF2_LAUNCH(P, V)                                                                                  \
+  hipLaunchKernelGGL((k_conv_fwd2<P, V>), dim3(B, 2), dim3(512), 0, st, Xb, w1, b1, Wp, b2, P1, A1, P2, A2, zero_ptr, \
+                     zero_n, P ? prof : nullptr)
+  if (prof) {
+    if (valu) PDE_CF2_LAUNCH(true, true);
+    else PDE_CF2_LAUNCH(true, false);
+  } else {
+    if (valu) PDE_CF2_LAUNCH(false, true);
+    else PDE_CF2_LAUNCH(false, false);
+  }
+#undef PDE_CF2_LAUNCH
   return hipGetLastError();
 }
 
