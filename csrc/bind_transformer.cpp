@@ -147,6 +147,13 @@ void f32_to_bf16(const at::Tensor& x, const at::Tensor& y) {
   hip_check(pde_f32_to_bf16(ptr<float>(x), y.data_ptr(), x.numel(), cur_stream()), "f32_to_bf16");
 }
 
+void scale_bf16(const at::Tensor& x, const at::Tensor& s) {
+  check_cuda(x, "x", BF16);
+  check_cuda(s, "s", F32, 1);
+  TORCH_CHECK(x.numel() % 8 == 0, "scale_bf16: numel % 8");
+  hip_check(pde_scale_bf16(x.data_ptr(), ptr<float>(s), x.numel(), cur_stream()), "scale_bf16");
+}
+
 int64_t colsum_bf16_splits(int64_t C) { return pde_colsum_bf16_splits((int)C); }
 
 void colsum_bf16(const at::Tensor& x, const at::Tensor& part, const at::Tensor& out) {
@@ -298,6 +305,7 @@ void register_transformer(pybind11::module& m) {
         py::arg("step"), py::arg("decay_blk") = py::none(), py::arg("clip_sumsq") = py::none(),
         py::arg("max_norm") = 1.0, py::arg("step_dev") = py::none());
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("scale_bf16", &scale_bf16);
   m.def("sum_f32", &sum_f32, py::arg("x"), py::arg("out"), py::arg("scale") = 1.0);
   m.def("token_batch", &token_batch);
   m.def("colsum_bf16_splits", &colsum_bf16_splits);

@@ -133,6 +133,7 @@ hipError_t pde_adamw_master(float* master, void* p16, const void* g16, float* m,
                             const uint8_t* decay_blk, const float* clip_sumsq, float max_norm, const float* step_dev,
                             hipStream_t st);
 hipError_t pde_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
+hipError_t pde_scale_bf16(void* x, const float* s, int64_t n, hipStream_t st);   // x *= s[0], n % 8 == 0
 hipError_t pde_sum_f32(const float* x, int n, float* out, float scale, hipStream_t st);
 hipError_t pde_token_batch(const int64_t* pool, const int64_t* rows, int B, int T, int64_t* x, int64_t* y,
                            hipStream_t st);

@@ -239,6 +239,11 @@ int64_t CommWatchdog::pending() {
 
 void CommWatchdog::loop() {
   hipSetDevice(comm_->device());
+  // The polls below must not count as unsafe calls against a capture another thread runs in the
+  // default (global) mode -- a hipEventQuery there invalidates that capture. Relaxed mode exempts
+  // this thread; the events it queries are never part of a capture (watch() skips capturing streams).
+  hipStreamCaptureMode relaxed = hipStreamCaptureModeRelaxed;
+  hipThreadExchangeStreamCaptureMode(&relaxed);
   std::unique_lock<std::mutex> lk(mu_);
   while (!stop_) {
     if (items_.empty()) {

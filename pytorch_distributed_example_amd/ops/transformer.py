@@ -334,13 +334,14 @@ class LMHeadLossFn(torch.autograd.Function):
         if gs.dtype != torch.float32 or not gs.is_cuda:
             gs = gs.to(device=dlogits.device, dtype=torch.float32)
         if _LMHEAD_LIB:
-            dh = torch.matmul(dlogits, w).mul_(gs.reshape(()))   # plain library GEMM + loss-gradient scale
+            dh = torch.matmul(dlogits, w)                    # plain library GEMM, then the loss-gradient
+            kernels().scale_bf16(dh, gs)                     # scale (device scalar, vectorised, in place)
         else:
             dh = G.dgrad(dlogits, w, scale=gs)               # [N, C]
         if _LMHEAD_LIB_W:
             slot = _grad_out(w)
             dw = torch.matmul(dlogits.t(), h2, out=slot) if slot is not None else torch.matmul(dlogits.t(), h2)
-            dw.mul_(gs.reshape(()))
+            kernels().scale_bf16(dw, gs)
         else:
             dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
         if ctx.tied is not None:

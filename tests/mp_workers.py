@@ -601,7 +601,7 @@ def case_ddp_model(model="gpt2", steps="3"):
     dist.destroy_process_group()
 
 
-def case_ddp_graph(model="gpt2", steps="3"):
+def case_ddp_graph(model="gpt2", steps="3", route="auto", backend="gloo"):
     """Verdict r3 next 3: the whole DDP training step (forward with the buffer broadcast, backward with
     the bucket all-reduces over the xGMI peer route, optimizer) captured as ONE hipGraph at W > 1 and
     replayed must train exactly like the eager DDP step -- same parameters bit for bit, replicas
@@ -609,15 +609,20 @@ def case_ddp_graph(model="gpt2", steps="3"):
     from pytorch_distributed_example_amd import ops
     from pytorch_distributed_example_amd.parallel import DistributedDataParallel
 
-    dev = _shared_gpu_init()
+    if backend == "nccl":          # one rank per GPU over RCCL (W = 1 here: force_comm runs the comm path)
+        _init("nccl")
+        dev = _dev("nccl")
+    else:
+        dev = _shared_gpu_init()
     g = torch.Generator().manual_seed(77)
     n = int(steps)
+    fc = dict(force_comm=True, reduce_route=route) if backend == "nccl" else {}
     if model == "gpt2":
         from pytorch_distributed_example_amd.models import GPTConfig, build_gpt2
         from pytorch_distributed_example_amd.optim import AdamWMaster
         cfg = GPTConfig(block_size=128, vocab_size=1000, padded_vocab=1024, n_layer=2, n_head=2, n_embd=128)
         net = build_gpt2(cfg, seed=5 + R, device=dev)
-        ddp = DistributedDataParallel(net, bucket_cap_mb=0.5)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=0.5, **fc)
         opt = AdamWMaster(net.decay_groups(0.1), lr=3e-3, max_grad_norm=1.0, capturable=True)
         data = torch.randint(0, cfg.vocab_size, (n, 2 * W, 129), generator=g)
         sx = torch.empty(2, 128, device=dev, dtype=torch.long)
@@ -634,7 +639,7 @@ def case_ddp_graph(model="gpt2", steps="3"):
         from pytorch_distributed_example_amd.models import build_resnet18
         from pytorch_distributed_example_amd.optim import SGDMaster
         net = build_resnet18(num_classes=10, seed=5 + R, device=dev)
-        ddp = DistributedDataParallel(net, bucket_cap_mb=4.0)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=4.0, **fc)
         opt = SGDMaster(net.decay_groups(5e-5), lr=0.05, momentum=0.9)
         xs = torch.randn(n, 4 * W, 3, 64, 64, generator=g)
         ys = torch.randint(0, 10, (n, 4 * W), generator=g)
@@ -647,7 +652,10 @@ def case_ddp_graph(model="gpt2", steps="3"):
 
         def loss_fn():
             return ops.cross_entropy(ddp(sx), sy)
-    assert ddp.reduce_route == "peer", ddp.peer_reason
+    if backend != "nccl":
+        assert ddp.reduce_route == "peer", ddp.peer_reason
+    elif route != "auto":
+        assert ddp.reduce_route == route, ddp.reduce_route
     ones = torch.ones((), device=dev, dtype=torch.float32)
 
     def step():
@@ -700,7 +708,8 @@ def case_ddp_graph(model="gpt2", steps="3"):
     nb = len(list(net.buffers()))
     npar = len(list(net.parameters()))
     emit({"rank": R, "eager_bits": eager_bits, "graph_bits": graph_bits, "eager_losses": eager_losses,
-          "graph_losses": graph_losses, "peer_error": ddp._peer.error(),
+          "graph_losses": graph_losses, "peer_error": ddp._peer.error() if ddp._peer is not None else 0,
+          "route": ddp.reduce_route,
           # torch-DDP semantics: buffers are broadcast at the START of each forward, then updated from
           # the local batch, so across ranks only parameters and optimizer state must agree
           "replicated_bits": graph_bits[:npar] + graph_bits[npar + nb:]})

@@ -121,3 +121,15 @@ def test_ddp_graph_replay_matches_eager(model):
         assert r["peer_error"] == 0
         assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])
     assert res[0]["replicated_bits"] == res[1]["replicated_bits"], "replicas diverged"
+
+
+@pytest.mark.parametrize("model,route", [("gpt2", "fp32"), ("gpt2", "param"), ("resnet", "param")])
+def test_ddp_graph_replay_rccl_routes(model, route):
+    """The RCCL reduction routes inside a captured DDP step (one rank over RCCL, force_comm): the fp32
+    staging route (copy, all-reduce, copy-back on the comm stream) and torch's in-dtype route replay
+    bit-identically to the eager DDP step."""
+    rc, res, logs = run_ranks("ddp_graph", 1, model, "3", route, "nccl")
+    assert rc == 0, "\n".join(logs)
+    r = res[0]
+    assert r["route"] == route
+    assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])

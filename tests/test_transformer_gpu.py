@@ -432,3 +432,15 @@ def test_xent_kernel_matches_torch():
     assert rel_err(got[:, :V], g) < 1e-2
     assert got[:, V:].abs().max().item() == 0.0
     assert got[2].abs().max().item() == 0.0                # ignored row
+
+
+def test_scale_bf16_matches_torch():
+    """In-place bf16 scale by a device scalar (LM-head dgrad loss-gradient scale): matches the fp32
+    product rounded once to bf16, over a grid-stride tail (n8 not a multiple of the block)."""
+    from pytorch_distributed_example_amd._ext import kernels
+    torch.manual_seed(12)
+    x = torch.randn(1000 * 8 + 8 * 37, device=dev).to(torch.bfloat16)
+    s = torch.tensor([0.3712], device=dev)
+    want = (x.float() * s).to(torch.bfloat16)
+    kernels().scale_bf16(x, s)
+    assert torch.equal(x, want)
