@@ -72,6 +72,24 @@ def _env_overrides() -> None:
 
 _env_overrides()
 
+
+def _lib_fprop_keys():
+    """Plain fprops (bias epilogue only: no GELU, nothing a library GEMM cannot do) whose (N, K) is listed
+    run through hipBLASLt (``F.linear``) instead of the own kernel.  Default: GPT-2's two output
+    projections (attn.c_proj 768x768, mlp.c_proj 768x3072), where the library measured faster in-step
+    (869.6 / 872.7 -> 878.5 / 881.4 K tok/s same box, profiles/r4_gpt2/fprop_lib_ab.txt; adding c_attn
+    2304x768 did not help further).  PDE_GEMM_FPROP_LIB="N:K,..." / "all" / "none" overrides."""
+    import os
+    spec = os.environ.get("PDE_GEMM_FPROP_LIB", "768:768,768:3072").strip()
+    if spec == "all":
+        return "all"
+    if spec in ("", "none"):
+        return set()
+    return {tuple(int(v) for v in x.split(":")) for x in spec.split(",") if x.strip()}
+
+
+_FPROP_LIB = _lib_fprop_keys()
+
 _SCRATCH: Dict[Tuple, torch.Tensor] = {}
 
 
@@ -125,6 +143,8 @@ def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     _chk(w, "w")
     M, K = x2.shape
     N = w.shape[0]
+    if not gelu and out is None and cfg is None and (_FPROP_LIB == "all" or (N, K) in _FPROP_LIB):
+        return torch.nn.functional.linear(x2, w, bias)       # plain library GEMM (hipBLASLt)
     c = pick("fprop", M, N, K)[0] if cfg is None else cfg
     y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16) if out is None else out
     if gelu:
