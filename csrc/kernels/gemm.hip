@@ -1114,6 +1114,307 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
   }
 }
 
+// ============================================================================ 8-phase main loop
+// 256 x 256 tile, 8 waves as 2 (M) x 4 (N) of 128 x 64, v_mfma_f32_16x16x32_bf16, K staged 64 deep in
+// TWO LDS buffers (A and B images as in k_gemm16: toff() layout, LDS-DMA fill, conflict-free row reads,
+// transposed operands as [64 k][64] images read with ds_read_b64_tr_b16), each buffer split into four
+// REGIONS restaged independently (cdna_hip_programming.md §5, "The 256² 8-phase template", T3+T4): a
+// K-tile is four phases, one C quadrant x K = 64 (16 MFMAs) per phase, and each phase issues ONE region
+// (16 KB: two LDS-DMA instructions per lane) once the region's last reader is >= 2 phases back -- about a
+// K-tile of DMA stays in flight and the counted wait never drains the queue inside the loop.
+//   A regions: A0 = m-blocks 0..3 of both wave rows (row image: tile rows 0-63 / 128-191; transposed:
+//              images 0 and 2), A1 = m-blocks 4..7
+//   B regions: row image (TB = 0): B0 = n-blocks 0..1 of every wave (cols 64w + 0..31), B1 = 2..3;
+//              transposed (TB = 1, a 64-column image per wave): B0 = images 0-1, B1 = images 2-3
+//   phase 1: read A0 (8 fragments) + n-blocks 0..1; MFMA (m 0..3) x (n 0..1)
+//   phase 2: read n-blocks 2..3;                    MFMA (m 0..3) x (n 2..3)
+//   phase 3: read A1 (8);                           MFMA (m 4..7) x (n 2..3)
+//   phase 4: (registers);                           MFMA (m 4..7) x (n 0..1)
+//   issues: phase 1 B1 of K-tile kt+1 (TB = 0) / B1 of kt+1 (TB = 1: both B regions are last read in
+//           phase 2, so B0 goes out in phase 4 and B1 in the next phase 1), phase 2 A1 of kt+1,
+//           phase 3 A0 of kt+2, phase 4 B0 of kt+2.
+// The wait in each phase retires the slot issued 4 (TB = 0: vmcnt(8)) or 3 (TB = 1: vmcnt(6)) phases
+// earlier; a region is read at least one phase after the wait that retired it (a barrier every wave
+// passed behind its own wait).  Operand forms, split-K slabs and the bias-gradient MFMA (against a ones
+// fragment, m-blocks 0..3 by waves 0 / 1 in phase 1, 4..7 by waves 2 / 3 in phase 3: k-steps split over
+// the two) as k_gemm16; a K-contiguous operand needs K % 64 == 0 (no masked tail).
+template <bool TA, bool TB, int EPI, bool CS>
+__global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
+  constexpr int WM = 2, WN = 4, TM = 8, TN = 4, NT = 512;
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256
+  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 KB per K-tile
+  constexpr int RS = BN * 2 + 16;
+  constexpr int TILE_BYTES = EPI == kSlab ? 0 : BM * RS;
+  constexpr int EPI_BYTES = TILE_BYTES + (CS ? 2 * BM * 4 : 0);
+  constexpr int SMEM = EPI_BYTES > 2 * STAGE ? EPI_BYTES : 2 * STAGE;
+  constexpr int VMW = TB ? 6 : 8;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.mtiles * a.ntiles;
+  const int split = id / ntile, rem = id - split * ntile;
+  constexpr int G = 8;
+  const int grp = rem / (G * a.ntiles), r2 = rem - grp * (G * a.ntiles);
+  const int gsz = min(G, a.mtiles - grp * G);
+  const int mt = grp * G + r2 % gsz, nt = r2 / gsz;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kbeg = split * a.kper;
+  const int KT = (min(a.K, kbeg + a.kper) - kbeg + 63) >> 6;
+
+  // ---- LDS-DMA: region r's two wave-instructions per wave (u = 0, 1) fill 8-row group g of the images ----
+  const int lrow = glds_row(l);
+  uint32_t goff[4][2];
+  int gldso[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool isA = r < 2;
+      const bool tr = isA ? TA : TB;
+      int g;
+      if (tr) g = (isA ? 2 * u + r : 2 * (r - 2) + u) * 8 + w;    // image q = (A: 2u + r | B: 2(r-2) + u)
+      else if (isA) g = u * 16 + 8 * r + w;
+      else {
+        const int x = 8 * u + w;
+        g = (x >> 2) * 8 + (x & 3) + 4 * (r - 2);
+      }
+      const int ch = glds_chunk(l, g & 1);
+      gldso[r][u] = (isA ? 0 : ABYTES) + g * 1024;
+      const int lim = isA ? a.M : a.N, ld = isA ? a.lda : a.ldb, o0 = isA ? m0 : n0;
+      if (tr) {
+        const int k = kbeg + 8 * (g & 7) + lrow, c = o0 + 64 * (g >> 3) + 8 * ch;
+        goff[r][u] = c < lim ? (uint32_t)(((size_t)k * ld + c) * 2) : kOOB;
+      } else {
+        const int row = o0 + 8 * g + lrow;
+        goff[r][u] = row < lim ? (uint32_t)(((size_t)row * ld + kbeg + 8 * ch) * 2) : kOOB;
+      }
+    }
+  const uint32_t astep = TA ? (uint32_t)a.lda * 128u : 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  // region r of K-tile kt into buffer kt & 1 (nothing past the last K-tile of this split)
+  auto issue = [&](int r, int kt) {
+    if (kt >= KT) return;
+    const char* base = smem + (kt & 1) * STAGE;
+    const uint32_t ko = (uint32_t)kt * (r < 2 ? astep : bstep);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) glds16(r < 2 ? ar : br, base + gldso[r][u], goff[r][u] + ko);
+  };
+
+  // ---- fragment lane bases ----
+  const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+  const uint32_t abase = lds0 + (uint32_t)toff(wm * WTM + prow, l >> 4);
+  const uint32_t bbase = lds0 + (uint32_t)toff(wn * WTN + prow, l >> 4) + ABYTES;
+  // transposed fragments: 16-column block c of a 64-column image = base (c & 1) + 512 * (c >> 1) (the
+  // chunk's swizzle depends on bit 0 of the block only); the second image of a wave row is +8192
+  uint2 tab[TA ? 2 : 1], tbb[TB ? 2 : 1];
+  if constexpr (TA) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) tab[i] = add2(tr16_lane_off(wm * WTM + 16 * i), lds0);
+  }
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tbb[j] = add2(tr16_lane_off(wn * WTN + 16 * j), lds0 + ABYTES);
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[CS ? 4 : 1];
+#pragma unroll
+  for (int i = 0; i < (CS ? 4 : 1); ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool cs_on = CS && a.colsum != nullptr && nt == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3f80;
+  bf16x8 fa[4][2], fb[TN][2];
+
+  if (KT > 0) {
+    // prologue: the six slots before phase 0 (K-tile 0's four regions, K-tile 1's A0 and B0)
+    if constexpr (!TB) { issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0); issue(0, 1); issue(2, 1); }
+    else { issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0); issue(0, 1); issue(2, 1); }
+    // phase 0 reads K-tile 0's A0 + B0 (TB = 0) or A0 + B0 + B1 (TB = 1)
+    if (KT > 1) {
+      if constexpr (TB) wait_vm<6>();
+      else wait_vm<8>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+
+    auto phase = [&](auto BUF_, auto PH_, int kt) {
+      constexpr int BUF = decltype(BUF_)::value, PH = decltype(PH_)::value;
+      constexpr uint32_t BO = BUF * STAGE;
+      auto rdA = [&](auto I_, int s2) -> bf16x8 {
+        constexpr int i = decltype(I_)::value;
+        constexpr int TO = (i >> 2) * 8192 + ((i >> 1) & 1) * 512;
+        if constexpr (TA) return s2 ? trpair<4096 + TO>(add2(tab[i & 1], BO)) : trpair<TO>(add2(tab[i & 1], BO));
+        else return s2 ? rd128<2048 * i + 512>(abase + BO) : rd128<2048 * i>(abase + BO);
+      };
+      auto rdB = [&](auto J_, int s2) -> bf16x8 {
+        constexpr int j = decltype(J_)::value;
+        constexpr int TO = (j >> 1) * 512;
+        if constexpr (TB) return s2 ? trpair<4096 + TO>(add2(tbb[j & 1], BO)) : trpair<TO>(add2(tbb[j & 1], BO));
+        else return s2 ? rd128<2048 * j + 512>(bbase + BO) : rd128<2048 * j>(bbase + BO);
+      };
+      if constexpr (PH == 1 || PH == 3) {
+        static_for<0, 4>([&](auto I_) {
+          constexpr int i = decltype(I_)::value + (PH == 3 ? 4 : 0);
+          fa[i & 3][0] = rdA(std::integral_constant<int, i>{}, 0);
+          fa[i & 3][1] = rdA(std::integral_constant<int, i>{}, 1);
+        });
+      }
+      if constexpr (PH == 1 || PH == 2) {
+        static_for<0, 2>([&](auto J_) {
+          constexpr int j = decltype(J_)::value + (PH == 2 ? 2 : 0);
+          fb[j][0] = rdB(std::integral_constant<int, j>{}, 0);
+          fb[j][1] = rdB(std::integral_constant<int, j>{}, 1);
+        });
+      }
+      if constexpr (PH == 1) issue(3, kt + 1);
+      else if constexpr (PH == 2) issue(1, kt + 1);
+      else if constexpr (PH == 3) issue(0, kt + 2);
+      else issue(2, kt + 2);
+      if (kt + 2 < KT) wait_vm<VMW>();        // steady state: every slot of the last four was issued
+      else wait_vm<0>();                      // tail: fewer slots in flight, drain
+      __builtin_amdgcn_s_barrier();
+      lgkm_fence();
+      __builtin_amdgcn_s_setprio(1);
+      constexpr int I0 = (PH <= 2) ? 0 : 4, J0 = (PH == 1 || PH == 4) ? 0 : 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            acc[I0 + i][J0 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[J0 + j][s2], fa[i][s2], acc[I0 + i][J0 + j], 0, 0, 0);
+      if constexpr (CS && (PH == 1 || PH == 3)) {
+        const int sel = wn - (PH == 3 ? 2 : 0);                    // wave-uniform: 0 / 1 take k-step 0 / 1
+        if (cs_on && (sel == 0 || sel == 1)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, sel ? fa[i][1] : fa[i][0], accb[i], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    };
+    // the two wave rows run one barrier apart: on every SIMD (waves w and w + 4) one wave's MFMAs overlap
+    // the other's fragment reads / DMA issue (the template's stagger; a region is still restaged >= 2
+    // phases after its last read and read >= 1 phase after its wait, which is what the stagger needs)
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < KT; kt += 2) {
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, kt);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{}, kt);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{}, kt);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{}, kt);
+      if (kt + 1 < KT) {
+        phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, kt + 1);
+        phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, kt + 1);
+        phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{}, kt + 1);
+        phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{}, kt + 1);
+      }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the two rows
+  }
+  __syncthreads();
+  // ---- epilogue (k_gemm16's layout: lane l holds row mrow and columns pcol .. +3 of each 16x16 tile) ----
+  const int mrow = TA ? q16 : prow;
+  const int pcol = TB ? 4 * (l >> 4) : (int)((0x4c80u >> (4 * (l >> 4))) & 0xfu);   // {0, 8, 12, 4}[l >> 4]
+  if constexpr (EPI == kSlab) {
+    float* out = reinterpret_cast<float*>(a.C) + (size_t)split * a.M * a.ldc;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + 16 * i + mrow;
+      if (m < a.M) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WTN + 16 * j + pcol;
+          if (n < a.N)
+            *reinterpret_cast<float4*>(out + (size_t)m * a.ldc + n) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+  } else {
+    const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+    const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nl = wn * WTN + 16 * j + pcol;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = wm * WTM + 16 * i + mrow;
+        const float v[4] = {(acc[i][j][0] + bv[0]) * sc, (acc[i][j][1] + bv[1]) * sc, (acc[i][j][2] + bv[2]) * sc,
+                            (acc[i][j][3] + bv[3]) * sc};
+        *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+      }
+    }
+  }
+  if constexpr (CS) {
+    // waves 0 / 1 hold m-blocks 0..3, waves 2 / 3 m-blocks 4..7 (k-steps split between the pair): lanes
+    // 0..15 store their row sums into slot (wn & 1), the two slots are added below
+    if (cs_on && l < 16) {
+      float* csl = reinterpret_cast<float*>(smem + TILE_BYTES);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) csl[(wn & 1) * BM + wm * WTM + 16 * (i + 4 * (wn >> 1)) + mrow] = accb[i][0];
+    }
+  }
+  if constexpr (EPI != kSlab || CS) __syncthreads();
+  if constexpr (CS) {
+    if (cs_on && t < BM && m0 + t < a.M) {
+      const float* csl = reinterpret_cast<const float*>(smem + TILE_BYTES);
+      a.colsum[(size_t)split * a.M + m0 + t] = csl[t] + csl[BM + t];
+    }
+  }
+  if constexpr (EPI != kSlab) {
+    constexpr int CPR = BN / 8;
+    bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
+#pragma unroll 4
+    for (int c = t; c < BM * CPR; c += NT) {
+      const int row = c / CPR, cc = c - row * CPR;
+      const int m = m0 + row, n = n0 + 8 * cc;
+      if (m < a.M && n < a.N) {
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+        const size_t o = (size_t)m * a.ldc + n;
+        if constexpr (EPI == kBf16) {
+          *reinterpret_cast<uint4*>(C + o) = v;
+        } else if constexpr (EPI == kGeluBwd) {
+          const uint4 g = *reinterpret_cast<const uint4*>(a.aux + o);
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, gw[4] = {g.x, g.y, g.z, g.w};
+          uint32_t r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+            r[e] = pack_bf2(pr.x, pr.y);
+          }
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(r[0], r[1], r[2], r[3]);
+        } else {
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+          uint32_t ya[4], da[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            pde_f2 d;
+            const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+            ya[e] = pack_bf2(y.x, y.y);
+            da[e] = pack_bf2(d.x, d.y);
+          }
+          *reinterpret_cast<uint4*>(C + o) = make_uint4(ya[0], ya[1], ya[2], ya[3]);
+          *reinterpret_cast<uint4*>(a.C2 + o) = make_uint4(da[0], da[1], da[2], da[3]);
+        }
+      }
+    }
+  }
+}
+
 // dW (bf16 [M][N] contiguous) = sum of the fp32 slabs [S][M][N]; blocks past the dW range fold the
 // bias-gradient partials [S][M] into db (bf16) the same way
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int S, int64_t mn,
@@ -1173,7 +1474,10 @@ template <> struct Cfg<15> { static constexpr int V = 3, TM = 2, TN = 4, WM = 4,
 //           every operand layout and epilogue
 template <> struct Cfg<16> { static constexpr int V = 4, TM = 4, TN = 6, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
 template <> struct Cfg<17> { static constexpr int V = 4, TM = 4, TN = 8, WM = 4, WN = 2, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 18;
+//   18: the 8-phase loop (k_gemm8p) at 256x256, every operand layout and epilogue; a K-contiguous operand
+//       needs K % 64 == 0 (a call with a K tail runs 17)
+template <> struct Cfg<18> { static constexpr int V = 5, TM = 8, TN = 4, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 19;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -1190,12 +1494,18 @@ int num_cu() {
 template <int CFG, bool TA, bool TB, int EPI, bool CS>
 hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   using C = Cfg<CFG>;
-  constexpr int FR = C::V == 4 ? 16 : 32;               // MFMA fragment rows (k_gemm16: 16x16 tiles)
+  constexpr int FR = C::V >= 4 ? 16 : 32;               // MFMA fragment rows (k_gemm16 / k_gemm8p: 16x16 tiles)
   constexpr int BM = C::WM * C::TM * FR, BN = C::WN * C::TN * FR;
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 4) {
+  if constexpr (C::V == 5) {
+    if ((TA && TB) || a.K % 64 == 0) {
+      hipLaunchKernelGGL((k_gemm8p<TA, TB, EPI, CS>), dim3(grid), dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 4) {
     hipLaunchKernelGGL((k_gemm16<C::TM, C::TN, C::WM, C::WN, TA, TB, EPI, CS>), dim3(grid),
                        dim3(64 * C::WM * C::WN), 0, st, a);
     return hipGetLastError();
@@ -1238,7 +1548,8 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 14: return launch_cfg<14, TA, TB, EPI, CS>(a, splits, st);
     case 15: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
     case 16: return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
+    case 17: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -1252,7 +1563,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                                     {256, 256}, {256, 192}, {256, 256}};
+                                     {256, 256}, {256, 192}, {256, 256}, {256, 256}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];

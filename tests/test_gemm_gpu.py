@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(18))
+CFGS = list(range(19))
 
 
 def rel_err(a, b):
@@ -25,11 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 18
+    assert K.gemm_num_cfgs() == 19
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
                                                      (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
-                                                     (256, 256), (256, 192), (256, 256)]
+                                                     (256, 256), (256, 192), (256, 256), (256, 256)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -149,3 +149,47 @@ def test_persistent_multi_tile(cfg, M, N, K):
     assert rel_err(dx, rd) < 1e-2
     dxg = G.dgrad(dy, w2, dgelu=dgelu, cfg=cfg)
     assert rel_err(dxg, rd * dgelu.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(4100, 2312, 768), (1000, 3072, 3072), (256, 256, 64), (700, 520, 1216)])
+def test_gemm8p_fprop(M, N, K):
+    """cfg 18, the 8-phase fprop loop (four half-tile regions per K-tile buffer restaged as soon as their
+    readers are two phases back, counted vmcnt): ragged M / N tiles, one K-tile, odd K-tile counts, the
+    GPT-2 c_attn / mlp shapes; bias and GELU epilogues against fp32 torch."""
+    x, w, b = _bf(M, K, seed=40), _bf(N, K, scale=0.03, seed=41), _bf(N, seed=42)
+    rp = F.linear(x.float(), w.float(), b.float())
+    assert rel_err(G.fprop(x, w, b, cfg=18), rp) < 1e-2
+    act, dgelu = G.fprop(x, w, b, gelu=True, cfg=18)
+    rq = rp.clone().requires_grad_()
+    ref = F.gelu(rq, approximate="tanh")
+    ref.backward(torch.ones_like(ref))
+    assert rel_err(act, ref) < 2e-2 and rel_err(dgelu, rq.grad) < 2e-2
+    # bit-identical to the 2-phase 16x16x32 loop at the same tile (same k order per accumulator)
+    assert torch.equal(G.fprop(x, w, b, cfg=18), G.fprop(x, w, b, cfg=17))
+
+
+@pytest.mark.parametrize("M,N,K", [(4100, 776, 2304), (1000, 3072, 768), (300, 200, 192)])
+def test_gemm8p_dgrad(M, N, K):
+    """cfg 18 with the transposed B operand (dgrad: two B regions of two 64-column images, vmcnt(6)):
+    plain and GELU-backward epilogues vs fp32 torch, bit-identical to cfg 17."""
+    dy, w = _bf(M, K, seed=43), _bf(K, N, scale=0.03, seed=44)
+    dx = G.dgrad(dy, w, cfg=18)
+    assert rel_err(dx, dy.float() @ w.float()) < 1e-2
+    assert torch.equal(dx, G.dgrad(dy, w, cfg=17))
+    dgelu = _bf(M, N, seed=45)
+    dxg = G.dgrad(dy, w, dgelu=dgelu, cfg=18)
+    assert torch.equal(dxg, G.dgrad(dy, w, dgelu=dgelu, cfg=17))
+
+
+@pytest.mark.parametrize("T,N,K,splits", [(4096, 2304, 768, 3), (2048, 768, 3072, 2), (1000, 392, 200, 1),
+                                          (300, 520, 264, 2)])
+def test_gemm8p_wgrad(T, N, K, splits):
+    """cfg 18 with both operands transposed (split-K fp32 slabs, the bias gradient from the ones-MFMA
+    spread over waves 0-3): dW and db vs fp32 torch and bit-identical to cfg 17; token counts that are
+    not multiples of 64 end at the operands' buffer bounds."""
+    dy, x = _bf(T, N, scale=0.1, seed=46), _bf(T, K, seed=47)
+    dw, db = G.wgrad(dy, x, want_db=True, cfg=18, splits=splits)
+    assert rel_err(dw, dy.float().t() @ x.float()) < 1e-2
+    assert rel_err(db, dy.float().sum(0)) < 1e-2
+    dw17, db17 = G.wgrad(dy, x, want_db=True, cfg=17, splits=splits)
+    assert torch.equal(dw, dw17) and torch.equal(db, db17)

@@ -81,8 +81,8 @@ def main():
             dw = torch.empty(out, fin, device=dev, dtype=torch.bfloat16)
             lib = timeit(lambda: torch.matmul(dy.t(), x, out=dw), a.iters)
             res = {}
-            for cfg in [c for c in CFGS if c in (0, 3, 4, 6, 9, 10, 11, 12, 13, 16, 17)]:
-                for s in (1, 2, 4, 5, 6, 7, 8, 9, 12, 16, 20):
+            for cfg in [c for c in CFGS if c in (0, 3, 4, 6, 9, 10, 11, 12, 13, 16, 17, 18)]:
+                for s in (1, 2, 4, 5, 6, 7, 8, 9, 12, 16, 20, 26):
                     if name == "lm_head" and s > 2:
                         continue
                     res[f"{cfg}/{s}"] = timeit(lambda: G.wgrad(dy, x, dw=dw, want_db=name != "lm_head", cfg=cfg,
