@@ -693,25 +693,38 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     // col2im as a gather (fixed summation order) + ReLU mask of P1.  (Measured and rejected: each lane
     // adding its 16 T values into dP1 with LDS atomics straight from the accumulator, no T image and
     // no gather pass -- ds_add_f32 made the step 91 us instead of 55.5, profiles/r3_lenet/.)
+    // All 25 taps of an output are read before any is summed (clamped rows / columns, so every read is
+    // unconditional and its address is a per-row + per-column register pair plus an immediate); the
+    // taps outside the 8 x 8 window are then dropped in the sum, in the same (kh, kw) order as before.
+    // (Summing as the reads came made hipcc wait for every ds_read: 52 waits per pass, ~2.8 us.)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int o = t + 512 * r;
       if (o < 720) {
         const int cl = o / 144, pos = o - cl * 144, ih = pos / 12, iw = pos - ih * 12;
+        int rowo[5], colo[5];
+        bool rok[5], cok[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const int oh = ih - k, ow = iw - k;
+          rok[k] = oh >= 0 && oh < 8;
+          cok[k] = ow >= 0 && ow < 8;
+          rowo[k] = cl * 1600 + min(max(oh, 0), 7) * 8;
+          colo[k] = min(max(ow, 0), 7);
+        }
+        float tv[25];
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) tv[kh * 5 + kw] = T[rowo[kh] + colo[kw] + (kh * 5 + kw) * 64];
+        const int c = 5 * p + cl;
+        const float pm = p1s[c * 144 + pos];
         float sacc = 0.f;
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh) {
-          const int oh = ih - kh;
+        for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) {
-            const int ow = iw - kw;
-            const bool ok = oh >= 0 && oh < 8 && ow >= 0 && ow < 8;
-            const float tv = T[ok ? (cl * 25 + kh * 5 + kw) * 64 + oh * 8 + ow : 0];
-            sacc += ok ? tv : 0.f;
-          }
-        }
-        const int c = 5 * p + cl;
-        dp1[c * 145 + pos] = p1s[c * 144 + pos] > 0.f ? sacc : 0.f;
+          for (int kw = 0; kw < 5; ++kw) sacc += (rok[kh] && cok[kw]) ? tv[kh * 5 + kw] : 0.f;
+        dp1[c * 145 + pos] = pm > 0.f ? sacc : 0.f;
       }
     }
     lds_barrier();
@@ -734,14 +747,30 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     const int lsub = lg & 1;
     const float* xp = xs + (6 * kq + th) * 28 + tw + lg;
     f32x4 acc0 = {0.f}, acc1 = {0.f};
+    // operands of 12 k-steps read before their MFMAs (unconditional reads: the gradient is selected by
+    // the code afterwards; a conditional read made hipcc branch and wait around every step)
 #pragma unroll
-    for (int s2 = 0; s2 < 36; ++s2) {
-      const int rr = (4 * s2) / 24, cq = (4 * s2) % 24;       // pos = 144kq + 4s + lg
-      const int qo = (rr >> 1) * 12 + cq / 2, sub = (rr & 1) * 2 + lsub;
-      const float a = (cdp[qo] == sub ? dpp[qo] : 0.f) * cmask;
-      const float bv = xp[rr * 28 + cq] * tmask + tone;
-      if (s2 & 1) acc1 = mfma16x16x4(a, bv, acc1);
-      else acc0 = mfma16x16x4(a, bv, acc0);
+    for (int chn = 0; chn < 3; ++chn) {
+      uint8_t cv[12];
+      float dv[12], xv[12];
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        const int s2 = 12 * chn + q;
+        const int rr = (4 * s2) / 24, cq = (4 * s2) % 24;     // pos = 144kq + 4s + lg
+        const int qo = (rr >> 1) * 12 + cq / 2;
+        cv[q] = cdp[qo];
+        dv[q] = dpp[qo];
+        xv[q] = xp[rr * 28 + cq];
+      }
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        const int s2 = 12 * chn + q;
+        const int rr = (4 * s2) / 24, sub = (rr & 1) * 2 + lsub;
+        const float a = (cv[q] == sub ? dv[q] : 0.f) * cmask;
+        const float bv = xv[q] * tmask + tone;
+        if (s2 & 1) acc1 = mfma16x16x4(a, bv, acc1);
+        else acc0 = mfma16x16x4(a, bv, acc0);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(kq * 16 + lg * 4 + r) * 36 + nt * 16 + (l & 15)] = acc0[r] + acc1[r];
