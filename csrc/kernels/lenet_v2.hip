@@ -126,34 +126,49 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
     uint8_t* codes = reinterpret_cast<uint8_t*>(smem + kL_CODE);
     if (t < 480) {
       const int c = t / 24, rem = t - c * 24, ph = rem >> 1, hf = rem & 1;
-      float win[6][16];
+      // the window as column PAIRS, so the two horizontal sub-positions (dx = 0, 1) of a pooling window
+      // run as one packed FMA (v_pk_fma_f32: the f32 VALU's full rate, half the issue slots of
+      // scalar FMAs); odd pairs (x[2i+1], x[2i+2]) are built once per row from the even ones
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      f2v ev[6][8];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float4 v4 = *reinterpret_cast<const float4*>(xin + (2 * ph + r) * kImgRow + 12 * hf + 4 * k);
-          win[r][4 * k + 0] = v4.x;
-          win[r][4 * k + 1] = v4.y;
-          win[r][4 * k + 2] = v4.z;
-          win[r][4 * k + 3] = v4.w;
+          ev[r][2 * k] = f2v{v4.x, v4.y};
+          ev[r][2 * k + 1] = f2v{v4.z, v4.w};
         }
+      auto pr = [&](int r, int i) -> f2v {       // (x[r][i], x[r][i + 1]), i compile-time
+        return (i & 1) ? f2v{ev[r][i >> 1].y, ev[r][(i >> 1) + 1].x} : ev[r][i >> 1];
+      };
       float wt[25];
 #pragma unroll
       for (int k = 0; k < 25; ++k) wt[k] = w1s[c * 25 + k];
       const float bch = w1s[500 + c];
+      // a[pw][dy] = (sub-position (dy, 0), (dy, 1)); each output's FMA chain runs kh-major, kw-minor as
+      // the scalar form did (bit-identical sums)
+      f2v a[6][2];
+#pragma unroll
+      for (int pw = 0; pw < 6; ++pw) a[pw][0] = a[pw][1] = f2v{0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int pw = 0; pw < 6; ++pw)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const f2v wv2 = f2v{wt[kh * 5 + kw], wt[kh * 5 + kw]};
+            a[pw][0] = __builtin_elementwise_fma(pr(kh, 2 * pw + kw), wv2, a[pw][0]);
+            a[pw][1] = __builtin_elementwise_fma(pr(kh + 1, 2 * pw + kw), wv2, a[pw][1]);
+          }
 #pragma unroll
       for (int pw = 0; pw < 6; ++pw) {
+        const float qv[4] = {a[pw][0].x, a[pw][0].y, a[pw][1].x, a[pw][1].y};
         float best = 0.f;
         int code = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int dy = q >> 1, dx = q & 1;
-          float acc = 0.f;
-#pragma unroll
-          for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-            for (int kw = 0; kw < 5; ++kw) acc = fmaf(win[dy + kh][2 * pw + dx + kw], wt[kh * 5 + kw], acc);
-          const float v = fmaxf(acc + bch, 0.f);
+          const float v = fmaxf(qv[q] + bch, 0.f);
           if (q == 0 || v > best) {            // first maximum in scan order (ATen)
             best = v;
             code = q;
