@@ -67,27 +67,44 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   const int b = blockIdx.x, ct = blockIdx.y, t = threadIdx.x, l = t & 63, w = t >> 6;
   PMARK(0);
   // ---- phase 0: register loads first (image, conv1 weights, this wave's conv2 biases) ----
-  const float4 xv = reinterpret_cast<const float4*>(Xb + (size_t)b * kImg)[min(t, kImg / 4 - 1)];
-  const float4 wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
-  const float bv1 = b1[min(t, 19)];
   const int cotile = w >> 2, pxt = w & 3, kq = l >> 4, j = l & 15;
   const int co_base = ct * 32 + cotile * 16 + kq * 4;          // + r: the accumulator row's channel
+  float4 xv, wv;
+  float bv1;
   float bias2[4];
+  float4 wr[9];
+  if constexpr (conv1_valu) {
+    // EVERY global load before conv1 is inline asm, the conv2 weight image (9 x 16 B per lane) issued
+    // right behind the image and conv1 weights, so the weights are in flight from the block start;
+    // hipcc never sees these loads, so none of its vmcnt waits can drain the weights early -- the
+    // first three are retired by the explicit vmcnt(9), the weights by a vmcnt(0) after conv1
+    const float* xsrc = Xb + (size_t)b * kImg + 4 * min(t, kImg / 4 - 1);
+    const float* w1src = w1 + 4 * min(t, 124);
+    const float* b1src = b1 + min(t, 19);
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(xv) : "v"(xsrc) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wv) : "v"(w1src) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(bv1) : "v"(b1src) : "memory");
+    const float* wsrc = Wp + (size_t)ct * kWpHalf + w * 256 + l * 4;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) bias2[r] = b2[min(co_base + r, 49)];
+    for (int i = 0; i < 9; ++i)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wr[i]) : "v"(wsrc + i * 8 * 256) : "memory");
+    asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  } else {
+    xv = reinterpret_cast<const float4*>(Xb + (size_t)b * kImg)[min(t, kImg / 4 - 1)];
+    wv = reinterpret_cast<const float4*>(w1)[min(t, 124)];
+    bv1 = b1[min(t, 19)];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias2[r] = b2[min(co_base + r, 49)];
+  }
   if (t < kImg / 4) reinterpret_cast<float4*>(smem + kL_IMG + (t / 7) * kImgRow)[t % 7] = xv;
   if (t < 125) reinterpret_cast<float4*>(smem + kL_W1)[t] = wv;
   if (t < 20) smem[kL_W1 + 500 + t] = bv1;
-  // ---- then the conv2 weight image: 72 x 1 KB, exactly 9 per wave.  conv1_valu: into registers,
-  // written to LDS after conv1 (the LDS-DMA fill ran ~4.6 us from the block start, longer than the
-  // VALU conv1); else by LDS-DMA, which lands under the 3.7 us MFMA conv1 ----
-  float4 wr[9];
+  // ---- then the conv2 weight image: 72 x 1 KB, exactly 9 per wave.  conv1_valu: into registers
+  // (issued above), written to LDS after conv1 (the LDS-DMA fill ran ~4.6 us from the block start,
+  // longer than the VALU conv1); else by LDS-DMA, which lands under the 3.7 us MFMA conv1 ----
   {
     const float* wsrc = Wp + (size_t)ct * kWpHalf;
-    if constexpr (conv1_valu) {
-      // issued after the phase-0 barrier below (inline asm: the compiler would otherwise sink these loads
-      // to their use after conv1, and its vmcnt bookkeeping must not see them before the image wait)
-    } else {
+    if constexpr (!conv1_valu) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         const int c = w + 8 * i;
@@ -104,15 +121,6 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
   // barrier without draining the LDS-DMA (a __syncthreads() would wait vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if constexpr (conv1_valu) {
-    // conv2 weight image into registers, in flight under conv1 (which touches LDS only); explicitly
-    // waited for (vmcnt(0)) just before the LDS writes after conv1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const float* wsrc = Wp + (size_t)ct * kWpHalf + w * 256 + l * 4;
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(wr[i]) : "v"(wsrc + i * 8 * 256) : "memory");
-  }
   PMARK(1);
   // ---- phase 1: conv1 (1->20, 5x5) + bias + ReLU + 2x2 max-pool on the VALU ----
   // 480 threads: thread = (channel c, pooled row ph, half of the row): a 6 x 16 input window in
@@ -237,6 +245,9 @@ __global__ __launch_bounds__(512) void k_conv_fwd2(const float* __restrict__ Xb,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 9; ++i) *reinterpret_cast<float4*>(smem + kL_W + (w + 8 * i) * 256 + l * 4) = wr[i];
+    // the conv2 biases are needed only by the epilogue: loaded now, they land under conv2
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias2[r] = b2[min(co_base + r, 49)];
   }
   PMARK(2);
   // conv1 output visible + this wave's LDS-DMA landed, then every wave's (barrier)
