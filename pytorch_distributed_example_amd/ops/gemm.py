@@ -51,10 +51,13 @@ _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
     ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (15, 1),
     ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (15, 1),
     ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
-    ("dgrad", 3072, 768): (15, 1), ("dgrad", 768, 50304): (9, 1),
-    # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/)
-    ("wgrad", 2304, 768): (9, 7), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (9, 5),
-    ("wgrad", 768, 3072): (9, 5), ("wgrad", 50304, 768): (11, 2),
+    # round 4: the 8-phase loop (cfg 18) where it measured fastest (profiles/r4_gemm/
+    # summary_8phase_v2_staggered.txt): the GELU-backward dgrad, the LM-head dgrad and the long-K wgrads
+    ("dgrad", 3072, 768): (18, 1), ("dgrad", 768, 50304): (18, 1),
+    # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/; 256x256 tiles
+    # for cfg 18: 36 tiles x 7, 27 x 9)
+    ("wgrad", 2304, 768): (18, 9), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (18, 7),
+    ("wgrad", 768, 3072): (18, 7), ("wgrad", 50304, 768): (18, 1),
 }
 
 

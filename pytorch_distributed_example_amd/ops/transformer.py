@@ -333,7 +333,7 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1)
         if gs.dtype != torch.float32 or not gs.is_cuda:
             gs = gs.to(device=dlogits.device, dtype=torch.float32)
-        if _LMHEAD_LIB:
+        if _LMHEAD_LIB_D:
             dh = torch.matmul(dlogits, w)                    # plain library GEMM, then the loss-gradient
             kernels().scale_bf16(dh, gs)                     # scale (device scalar, vectorised, in place)
         else:
@@ -352,11 +352,14 @@ class LMHeadLossFn(torch.autograd.Function):
 # PDE_LMHEAD_CHUNK=<tokens>: run the LM-head GEMM + cross-entropy in token chunks (0 = one pass)
 import os as _os
 _LMHEAD_CHUNK = int(_os.environ.get("PDE_LMHEAD_CHUNK", "0"))
-# The LM head's fprop / dgrad are plain GEMMs (no epilogue to fuse: the cross-entropy needs whole rows),
-# so they run through hipBLASLt where it is faster on MI355X (in-step, one box: 886 vs 864 K tok/s,
-# profiles/r4_gpt2/); PDE_LMHEAD_GEMM=own keeps the framework's GEMM, =lib3 also moves the wgrad.
-_LMHEAD_MODE = _os.environ.get("PDE_LMHEAD_GEMM", "lib")
-_LMHEAD_LIB = _LMHEAD_MODE in ("lib", "lib3")
+# The LM head's fprop / dgrad are plain GEMMs (no epilogue to fuse: the cross-entropy needs whole rows):
+# the fprop runs through hipBLASLt, faster on MI355X (in-step, one box: 886 vs 864 K tok/s with both on
+# the library, profiles/r4_gpt2/); the dgrad on the own 8-phase GEMM with the loss-gradient scale in its
+# epilogue (1027 vs 1057 + 9.5 us, profiles/r4_gemm/).  PDE_LMHEAD_GEMM=lib puts the dgrad on the library
+# too, =own keeps both on the framework's GEMM, =lib3 also moves the wgrad.
+_LMHEAD_MODE = _os.environ.get("PDE_LMHEAD_GEMM", "mixed")
+_LMHEAD_LIB = _LMHEAD_MODE in ("lib", "lib3", "mixed")       # fprop on hipBLASLt
+_LMHEAD_LIB_D = _LMHEAD_MODE in ("lib", "lib3")               # dgrad too ("mixed": the own 8-phase dgrad)
 _LMHEAD_LIB_W = _LMHEAD_MODE == "lib3"
 
 
