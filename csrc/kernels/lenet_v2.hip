@@ -719,37 +719,35 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
     // col2im as a gather (fixed summation order) + ReLU mask of P1.  (Measured and rejected: each lane
     // adding its 16 T values into dP1 with LDS atomics straight from the accumulator, no T image and
     // no gather pass -- ds_add_f32 made the step 91 us instead of 55.5, profiles/r3_lenet/.)
-    // All 25 taps of an output are read before any is summed (clamped rows / columns, so every read is
-    // unconditional and its address is a per-row + per-column register pair plus an immediate); the
-    // taps outside the 8 x 8 window are then dropped in the sum, in the same (kh, kw) order as before.
-    // (Summing as the reads came made hipcc wait for every ds_read: 52 waits per pass, ~2.8 us.)
+    // All 25 taps of an output are read before any is summed, each at ONE per-output base address plus
+    // an immediate: tap (kh, kw) of output (ih, iw) is T[25 cl + 5 kh + kw][8 (ih - kh) + (iw - kw)]
+    // = base + 312 kh + 63 kw with base = 1600 cl + 8 ih + iw -- an out-of-window tap reads a
+    // neighbouring in-bounds T entry (the offset is >= 0 and < 128 x 64) that the sum then drops, in
+    // the same (kh, kw) order as the masked form.  (Summing as the reads came made hipcc wait for
+    // every ds_read; per-tap clamped addresses cost ~190 VALU per output, this form ~100.)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int o = t + 512 * r;
       if (o < 720) {
         const int cl = o / 144, pos = o - cl * 144, ih = pos / 12, iw = pos - ih * 12;
-        int rowo[5], colo[5];
-        bool rok[5], cok[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int oh = ih - k, ow = iw - k;
-          rok[k] = oh >= 0 && oh < 8;
-          cok[k] = ow >= 0 && ow < 8;
-          rowo[k] = cl * 1600 + min(max(oh, 0), 7) * 8;
-          colo[k] = min(max(ow, 0), 7);
-        }
+        const float* tb = T + cl * 1600 + 8 * ih + iw;
         float tv[25];
 #pragma unroll
         for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) tv[kh * 5 + kw] = T[rowo[kh] + colo[kw] + (kh * 5 + kw) * 64];
+          for (int kw = 0; kw < 5; ++kw) tv[kh * 5 + kw] = tb[312 * kh + 63 * kw];
         const int c = 5 * p + cl;
         const float pm = p1s[c * 144 + pos];
         float sacc = 0.f;
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
+        for (int kh = 0; kh < 5; ++kh) {
+          const bool rok = ih >= kh && ih < kh + 8;
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) sacc += (rok[kh] && cok[kw]) ? tv[kh * 5 + kw] : 0.f;
+          for (int kw = 0; kw < 5; ++kw) {
+            const bool ok = rok && iw >= kw && iw < kw + 8;
+            sacc += ok ? tv[kh * 5 + kw] : 0.f;
+          }
+        }
         dp1[c * 145 + pos] = pm > 0.f ? sacc : 0.f;
       }
     }
