@@ -762,9 +762,10 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
   {
     const int nt = w & 1, kq = w >> 1;
     const int c = l & 15, cc = min(c, 9);
-    const float cmask = c < 10 ? 1.f : 0.f;
+    const bool cin = c < 10;
     const int tap = nt * 16 + (l & 15);
-    const float tmask = tap < 25 ? 1.f : 0.f, tone = tap == 25 ? 1.f : 0.f;
+    const bool tin = tap < 25;
+    const float tone = tap == 25 ? 1.f : 0.f;
     const int tc = min(tap, 24), th = tc / 5, tw = tc - th * 5;
     const float* dpp = dp1 + cc * 145 + 36 * kq + (lg >> 1);
     const uint8_t* cdp = c1s + cc * 148 + 36 * kq + (lg >> 1);
@@ -790,8 +791,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd2(const float* __restrict__ Xb,
       for (int q = 0; q < 12; ++q) {
         const int s2 = 12 * chn + q;
         const int rr = (4 * s2) / 24, sub = (rr & 1) * 2 + lsub;
-        const float a = (cv[q] == sub ? dv[q] : 0.f) * cmask;
-        const float bv = xv[q] * tmask + tone;
+        const float a = (cv[q] == sub && cin) ? dv[q] : 0.f;     // one select: code match and channel < 10
+        const float bv = tin ? xv[q] : tone;                        // tap < 25: the image; 25: ones; else 0
         if (s2 & 1) acc1 = mfma16x16x4(a, bv, acc1);
         else acc0 = mfma16x16x4(a, bv, acc0);
       }
