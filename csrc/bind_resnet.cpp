@@ -58,7 +58,7 @@ void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at:
 void bn_bwd(const at::Tensor& dy, const OptT& y, const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& mean,
             const at::Tensor& rstd, const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dgamma,
             const at::Tensor& dbeta, const at::Tensor& dx, const OptT& dres, bool relu, const OptT& scale,
-            const OptT& shift) {
+            const OptT& shift, int64_t pre_nblk) {
   const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
   check_c(C);
   check_same(x, dy, "dy");
@@ -79,13 +79,16 @@ void bn_bwd(const at::Tensor& dy, const OptT& y, const at::Tensor& x, const at::
   check_cuda(gamma, "gamma", BF16, C);
   check_cuda(mean, "mean", F32, C);
   check_cuda(rstd, "rstd", F32, C);
-  check_cuda(part, "part", F32, (int64_t)pde_bn_blocks((int)M, (int)C) * 2 * C);
+  // pre_nblk > 0: part holds the dgrad epilogue's reduction partials (conv_dgrad bn_* arguments)
+  TORCH_CHECK(pre_nblk <= 0 || (relu && !yp && !dr), "bn_bwd: pre-summed partials need relu, y=None and no dres");
+  check_cuda(part, "part", F32,
+             (pre_nblk > 0 ? pde_bn_part_rows((int)pre_nblk) : (int64_t)pde_bn_blocks((int)M, (int)C)) * 2 * C);
   check_cuda(coef, "coef", F32, 3 * C);
   check_cuda(dgamma, "dgamma", BF16, C);
   check_cuda(dbeta, "dbeta", BF16, C);
   hip_check(pde_bn_bwd(dy.data_ptr(), yp, x.data_ptr(), (int)M, (int)C, gamma.data_ptr(), ptr<float>(mean),
                        ptr<float>(rstd), sc, sf, ptr<float>(part), ptr<float>(coef), dgamma.data_ptr(),
-                       dbeta.data_ptr(), dx.data_ptr(), dr, relu, cur_stream()),
+                       dbeta.data_ptr(), dx.data_ptr(), dr, relu, (int)pre_nblk, cur_stream()),
             "bn_bwd");
 }
 
@@ -266,10 +269,38 @@ void conv_fprop(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, c
 // input (dy [B, Cout, OH, OW], weight [Cout, C, 1, 1], bf16 scratch for its transpose) accumulated into dx
 // in the same pass (extra K stages of the even-pixel phase) instead of a second dgrad + residual add
 // wt_ready: wt (and ds_wt) already hold the transposed weights (conv_wtrans_batch), no transpose here
+// rows of BN-backward partials conv_dgrad(..., bn_x=...) writes (0: not available for this conv)
+int64_t conv_dgrad_bn_rows(const at::Tensor& dx, const at::Tensor& w, int64_t stride, int64_t pad) {
+  const ConvGeom g = conv_geom(dx, w, stride, pad);
+  return pde_conv_dgrad_bnb_rows((int)g.Bn, (int)g.H, (int)g.W, (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride,
+                                 (int)pad);
+}
+
+// bn_x / bn_scale / bn_shift / bn_mean / bn_rstd / bn_part (optional, stride 1): dx is the gradient of
+// relu(bn(bn_x)); the epilogue also sums that BN's backward partials (sum d, sum d * xhat) into
+// bn_part [bn_part_rows(conv_dgrad_bn_rows)][2][C], consumed by bn_bwd(..., pre_nblk=rows)
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt, const at::Tensor& dx,
                 int64_t stride, int64_t pad, const OptT& res, const OptT& ds_dy, const OptT& ds_w, const OptT& ds_wt,
-                bool wt_ready) {
+                bool wt_ready, const OptT& bn_x, const OptT& bn_scale, const OptT& bn_shift, const OptT& bn_mean,
+                const OptT& bn_rstd, const OptT& bn_part) {
   const ConvGeom g = conv_geom(dx, w, stride, pad);
+  const void* bx = nullptr;
+  const float *bsc = nullptr, *bsh = nullptr, *bmu = nullptr, *brs = nullptr;
+  float* bpart = nullptr;
+  if (bn_x.has_value() && bn_x->defined()) {
+    check_same(dx, *bn_x, "bn_x");
+    const int64_t rows = conv_dgrad_bn_rows(dx, w, stride, pad);
+    TORCH_CHECK(rows > 0, "conv dgrad: fused BN-backward partials need a stride-1 convolution");
+    bsc = optr<float>(bn_scale, "bn_scale", F32, g.C);
+    bsh = optr<float>(bn_shift, "bn_shift", F32, g.C);
+    bmu = optr<float>(bn_mean, "bn_mean", F32, g.C);
+    brs = optr<float>(bn_rstd, "bn_rstd", F32, g.C);
+    bpart = optr<float>(bn_part, "bn_part", F32, pde_bn_part_rows((int)rows) * 2 * g.C);
+    TORCH_CHECK(bsc && bsh && bmu && brs && bpart, "conv dgrad: bn_x needs bn_scale / shift / mean / rstd / part");
+    TORCH_CHECK(!(ds_dy.has_value() && ds_dy->defined()) && !(res.has_value() && res->defined()),
+                "conv dgrad: bn_x excludes a downsample source and a residual");
+    bx = bn_x->data_ptr();
+  }
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == BF16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   dy.size(0) == g.Bn && dy.size(1) == g.N && dy.size(2) == g.OH && dy.size(3) == g.OW,
               "conv dgrad: dy must be channels-last bf16 [B, Cout, OH, OW]");
@@ -306,8 +337,8 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& wt,
     wt2 = ds_wt->data_ptr();
   }
   hip_check(pde_conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), rp, dy2, wt2, (int)g.Bn, (int)g.H, (int)g.W,
-                           (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW,
-                           cur_stream()),
+                           (int)g.C, (int)g.N, (int)g.R, (int)g.S, (int)stride, (int)pad, (int)g.OH, (int)g.OW, bx,
+                           bsc, bsh, bmu, brs, bpart, cur_stream()),
             "conv_dgrad");
 }
 
@@ -406,7 +437,8 @@ void register_resnet(pybind11::module& m) {
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("part"), py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dx"),
-        py::arg("dres"), py::arg("relu"), py::arg("scale") = py::none(), py::arg("shift") = py::none());
+        py::arg("dres"), py::arg("relu"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
+        py::arg("pre_nblk") = 0);
   m.def("sgd_master", &sgd_master);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("avgpool_fwd", &avgpool_fwd);
@@ -426,7 +458,10 @@ void register_resnet(pybind11::module& m) {
   m.def("conv_fprop", &conv_fprop);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt"), py::arg("dx"), py::arg("stride"),
         py::arg("pad"), py::arg("res") = py::none(), py::arg("ds_dy") = py::none(), py::arg("ds_w") = py::none(),
-        py::arg("ds_wt") = py::none(), py::arg("wt_ready") = false);
+        py::arg("ds_wt") = py::none(), py::arg("wt_ready") = false, py::arg("bn_x") = py::none(),
+        py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none(), py::arg("bn_mean") = py::none(),
+        py::arg("bn_rstd") = py::none(), py::arg("bn_part") = py::none());
+  m.def("conv_dgrad_bn_rows", &conv_dgrad_bn_rows);
   m.def("conv_wtrans_batch", &conv_wtrans_batch, py::arg("desc"), py::arg("total"), py::arg("counters") = py::none());
   m.def("conv_wgrad_splits", &conv_wgrad_splits);
   m.def("conv_wgrad", &conv_wgrad);

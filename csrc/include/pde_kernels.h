@@ -156,9 +156,12 @@ hipError_t pde_conv_fprop(const void* x, const void* w, void* y, float* stats, i
 hipError_t pde_conv_wtrans(const void* w, void* wt, int N, int T, int C, hipStream_t st);
 hipError_t pde_conv_wtrans_batch(const void* desc, int nconv, int total, long long* ctr, int ncnt, hipStream_t st);
 int pde_conv_wtdesc_bytes();
+// bx..bpart (optional, stride 1): BN-backward partials of dx fused into the epilogue (conv.hip BnbArgs)
+int pde_conv_dgrad_bnb_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad);
 hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, const void* dy2, const void* wt2,
                           int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW,
-                          hipStream_t st);
+                          const void* bx, const float* bsc, const float* bsh, const float* bmu, const float* brs,
+                          float* bpart, hipStream_t st);
 int pde_conv_wgrad_splits2(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW);
 int pde_conv_wgrad_splits(int Bn, int OH, int OW, int N, int T, int C);
 hipError_t pde_sum_slabs_bf16(const float* part, int S, int64_t n, void* out, hipStream_t st);
@@ -193,7 +196,7 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
                       float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk, hipStream_t st);
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, const float* scale, const float* shift, float* part, float* coef,
-                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, hipStream_t st);
+                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, int pre_nblk, hipStream_t st);
 int pde_bnpool_part_floats(int N, int H, int W, int C);
 hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift, void* p, void* arg, void* ysel,
                           int N, int C, int H, int W, int OH, int OW, hipStream_t st);

@@ -67,6 +67,78 @@ struct Phase {
 __host__ __device__ inline int pack_tap(int dh, int dw, int widx) {
   return (dh & 0xff) | ((dw & 0xff) << 8) | (widx << 16);
 }
+
+// Optional BatchNorm-backward partials of a dgrad OUTPUT (X != nullptr): when the convolution's input
+// was relu(bn(X)) (a BasicBlock's conv2 input a1 = relu(bn1(y1))), the dgrad output is bn1's dA, and
+// its backward reduction -- per channel (sum d, sum d * xhat), d = dA * (X*sc + sh > 0), xhat =
+// (X - mu) * rs -- is summed here, in the store loop, from the rounded bf16 output and one 16-B read
+// of X per chunk, into part[mtile][2][NC] (the k_bn_bwd_reduce<2> format): no separate pass re-reading
+// dA.  Same per-element math as k_bn_bwd_reduce<2>; per-tile sums in a fixed order (deterministic).
+struct BnbArgs {
+  const bf16_t* X;
+  const float *sc, *sh, *mu, *rs;
+  float* part;
+};
+
+// Store-loop side: this thread's 8 channels (chunk n8 = first channel) of one output row.
+struct BnbAcc {
+  float s[8], q[8], sc[8], sh[8], mu[8], rs[8];
+  // per-channel constants: issue early (an epilogue-time load stalls the block one memory latency)
+  __device__ __forceinline__ void init(const BnbArgs& z, int n8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = z.sc[n8 + e];
+      sh[e] = z.sh[n8 + e];
+      mu[e] = z.mu[n8 + e];
+      rs[e] = z.rs[n8 + e];
+    }
+    reset();
+  }
+  __device__ __forceinline__ void reset() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  }
+  __device__ __forceinline__ void add(uint4 out, uint4 xin) {
+    float g[8], x[8];
+    unpack8(out, g);
+    unpack8(xin, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = x[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f;
+      s[e] += d;
+      q[e] += d * (x[e] - mu[e]) * rs[e];
+    }
+  }
+  // Fold the lanes of each wave that share this chunk (lane % CPR), then the waves through LDS
+  // red[NW][2][BN]; threads < 2 BN write row `row` of part.  Call from every thread of the block.
+  template <int CPR, int NW, int BN>
+  __device__ __forceinline__ void flush(float* red, const BnbArgs& z, size_t row, int NC, int n0) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += __shfl_xor(s[e], off, 64);
+        q[e] += __shfl_xor(q[e], off, 64);
+      }
+    if (l < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(w * 2 + 0) * BN + l * 8 + e] = s[e];
+        red[(w * 2 + 1) * BN + l * 8 + e] = q[e];
+      }
+    }
+    __syncthreads();
+    if (t < 2 * BN) {
+      const int which = t / BN, n = t % BN;
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) a += red[(k * 2 + which) * BN + n];
+      z.part[(row * 2 + which) * NC + n0 + n] = a;
+    }
+  }
+};
+
 struct IgemmArgs {
   const bf16_t* A;      // gather source NHWC [Bn][IH][IW][CA]
   const bf16_t* W;      // [NC][T][CA]
@@ -79,6 +151,7 @@ struct IgemmArgs {
   const bf16_t* W2;
   uint32_t a2_bytes, w2_bytes;
   float* stats;         // optional [mtiles][2][NC] (single-phase launches)
+  BnbArgs bnb;          // optional BN-backward partials of the output (single-phase launches)
   uint32_t a_bytes, w_bytes;
   int Bn, IH, IW, CA;
   int OH, OW, NC, T;
@@ -102,7 +175,8 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128, STAGE = ABYTES + BBYTES;
   constexpr int RS = BN * 2 + 16;                    // epilogue LDS row stride (bytes)
   constexpr int EPI = BM * RS + 2 * WM * BN * 4;
-  constexpr int SMEM = NST * STAGE > EPI ? NST * STAGE : EPI;
+  constexpr int EPIR = EPI + 4 * 2 * BN * 4;         // + the BN-backward fold red[4][2][BN]
+  constexpr int SMEM = NST * STAGE > EPIR ? NST * STAGE : EPIR;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -236,6 +310,9 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   }
 
   // ---- epilogue: bf16 tile through LDS, coalesced NHWC rows; optional BN partial stats ----
+  const bool bnb = a.bnb.X != nullptr;
+  BnbAcc za;
+  if (bnb) za.init(a.bnb, n0 + (t % (BN / 8)) * 8);  // a thread's chunk is fixed (kThreads % CPR == 0)
   char* ot = smem;
   float* sst = reinterpret_cast<float*>(smem + BM * RS);   // [WM][2][BN]
 #pragma unroll
@@ -265,27 +342,42 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
     }
   __syncthreads();
   constexpr int CPR = BN / 8;                        // 16-B chunks per output row
+  constexpr int EU = BM * CPR / kThreads;
+  // the epilogue's second input (residual gradient R, or the BN input X; never both) is prefetched
+  // for every chunk before the first store: loads issued inside the store loop were serialised behind
+  // the stores (possible aliasing), one memory latency per chunk
+  const bf16_t* pf = bnb ? a.bnb.X : a.R;
+  size_t oo[EU];
+  uint4 pre[EU];
 #pragma unroll
-  for (int u = 0; u < BM * CPR / kThreads; ++u) {
+  for (int u = 0; u < EU; ++u) {
     const int c = t + kThreads * u, row = c / CPR, cc = c % CPR;
-    const int m = m0 + row;
-    if (m < Mq) {
-      const int b = fdiv(m, P.Hq * P.Wq, P.inv_hw), r2 = m - b * (P.Hq * P.Wq);
-      const int hq = fdiv(r2, P.Wq, P.inv_w);
-      const int oh = hq * a.sO + P.ph, ow = (r2 - hq * P.Wq) * a.sO + P.pw;
+    const int m = min(m0 + row, Mq - 1);               // rows past Mq are never stored
+    const int b = fdiv(m, P.Hq * P.Wq, P.inv_hw), r2 = m - b * (P.Hq * P.Wq);
+    const int hq = fdiv(r2, P.Wq, P.inv_w);
+    const int oh = hq * a.sO + P.ph, ow = (r2 - hq * P.Wq) * a.sO + P.pw;
+    oo[u] = (((size_t)b * a.OH + oh) * a.OW + ow) * a.NC + n0 + cc * 8;
+    if (pf) pre[u] = *reinterpret_cast<const uint4*>(pf + oo[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < EU; ++u) {
+    const int c = t + kThreads * u, row = c / CPR, cc = c % CPR;
+    if (m0 + row < Mq) {
       uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
-      const size_t o = (((size_t)b * a.OH + oh) * a.OW + ow) * a.NC + n0 + cc * 8;
+      const size_t o = oo[u];
       if (a.R) {                                       // the other consumer's gradient, added once
         float f[8], r[8];
         unpack8(v, f);
-        unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+        unpack8(pre[u], r);
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += r[e];
         v = pack8(f);
       }
       *reinterpret_cast<uint4*>(a.Y + o) = v;
+      if (bnb) za.add(v, pre[u]);
     }
   }
+  if (bnb) za.flush<CPR, 4, BN>(reinterpret_cast<float*>(smem + EPI), a.bnb, (size_t)mt, a.NC, n0);
   if (a.stats && t < 2 * BN) {
     const int which = t / BN, n = t % BN;
     float s = 0.f;
@@ -496,6 +588,7 @@ struct HconvArgs {
   bf16_t* Y;            // NHWC [Bn][H][W][NC]
   const bf16_t* R;      // optional, like Y: Y = bf16(acc) + R
   float* stats;         // optional [Bn * rtiles][2][NC]
+  BnbArgs bnb;          // optional BN-backward partials of the output, [Bn * rtiles][2][NC]
   uint32_t a_bytes, w_bytes;
   int Bn, H, W, CA, NC;
   int TH, rtiles, ntiles;
@@ -531,7 +624,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   constexpr int BI = BN / 32, BBYTES = BN * 128;
   constexpr int RS = BN * 2 + 16;
   constexpr int EPIB = BM * RS + 2 * WM * BN * 4;
-  constexpr int SMEM = HBYTES + 2 * BBYTES > EPIB ? HBYTES + 2 * BBYTES : EPIB;
+  constexpr int EPIR = EPIB + 4 * 2 * BN * 4;        // + the BN-backward fold red[4][2][BN]
+  constexpr int SMEM = HBYTES + 2 * BBYTES > EPIR ? HBYTES + 2 * BBYTES : EPIR;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char* halo = smem;
   char* bimg = smem + HBYTES;
@@ -585,12 +679,27 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
       glds16(wr, bimg + buf * BBYTES + (4 * v + w) * 1024, wrow[v] + (uint32_t)((wi * a.CA + c0) * 2));
   };
 
+  // the epilogue's second input (residual gradient or BN input, never both): loaded with the last
+  // channel chunk's halo, so it lands under that chunk's MFMAs instead of stalling the epilogue
+  constexpr int CPR = BN / 8, EU = BM * CPR / kThreads;
+  const size_t obase = ((size_t)b * a.H + oh0) * a.W;     // first output pixel of the block
+  const bool bnb = a.bnb.X != nullptr;
+  const bf16_t* pf = bnb ? a.bnb.X : a.R;
+  uint4 pre[EU];
+  BnbAcc za;
   for (int cc = 0; cc < CPT; ++cc) {
     const int c0 = cc * 64;
     if (cc > 0) __syncthreads();                       // every wave is done with the previous chunk
 #pragma unroll
     for (int u = 0; u < HU; ++u)
       if (w + 4 * u < HG) glds16(ar, halo + (w + 4 * u) * 1024, hoff[u] == kOOB ? kOOB : hoff[u] + c0 * 2);
+    if (pf && cc == CPT - 1) {
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int c = t + kThreads * u, row = min(c / CPR, npx - 1);
+        pre[u] = *reinterpret_cast<const uint4*>(pf + (obase + row) * a.NC + n0 + (c % CPR) * 8);
+      }
+    }
     issue_b(0, c0, 0);
     for (int tp = 0; tp < 9; ++tp) {
       wait_vm<0>();
@@ -619,6 +728,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   __syncthreads();                                     // every wave is done with the halo / weights
 
   // ---- epilogue (as k_igemm): bf16 tile through LDS, masked BN partials, coalesced NHWC rows ----
+  if (bnb) za.init(a.bnb, n0 + (t % CPR) * 8);        // lands under the tile conversion below
   char* ot = smem;
   float* sst = reinterpret_cast<float*>(smem + BM * RS);   // [WM][2][BN]
 #pragma unroll
@@ -647,10 +757,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
       }
     }
   __syncthreads();
-  constexpr int CPR = BN / 8;
-  const size_t obase = ((size_t)b * a.H + oh0) * a.W;     // first output pixel of the block
 #pragma unroll
-  for (int u = 0; u < BM * CPR / kThreads; ++u) {
+  for (int u = 0; u < EU; ++u) {
     const int c = t + kThreads * u, row = c / CPR, cc = c % CPR;
     if (row < npx) {
       uint4 v = *reinterpret_cast<const uint4*>(ot + row * RS + cc * 16);
@@ -658,14 +766,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
       if (a.R) {
         float f[8], r[8];
         unpack8(v, f);
-        unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+        unpack8(pre[u], r);
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += r[e];
         v = pack8(f);
       }
       *reinterpret_cast<uint4*>(a.Y + o) = v;
+      if (bnb) za.add(v, pre[u]);
     }
   }
+  if (bnb) za.flush<CPR, 4, BN>(reinterpret_cast<float*>(smem + EPIB), a.bnb, (size_t)mt, a.NC, n0);
   if (a.stats && t < 2 * BN) {
     const int which = t / BN, n = t % BN;
     float s = 0.f;
@@ -722,6 +832,9 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
   };
 
   const int wm = w, lr = l & 31, lh = l >> 5;            // 8 x 1 waves of 32 x 64
+  const bool bnb = a.bnb.X != nullptr;
+  BnbAcc za;
+  if (bnb) za.init(a.bnb, (t & 7) * 8);                 // a thread's chunk is the same in every tile
   issue_halo(blockIdx.x, 0);
   int it = 0;
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
@@ -730,6 +843,19 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
     const int rows = min(a.TH, a.H - oh0), npx = rows * a.W;
     wait_vm<0>();                                      // this tile's halo (and the weights) landed
     __builtin_amdgcn_s_barrier();                      // ... for every wave; the other buffer is free
+    // the epilogue's second input (residual gradient or BN input, never both) for this tile: issued
+    // before the next halo's DMA and consumed after the MFMAs, so it lands under them (one CU streams
+    // ~25 GB/s: a 32 KB tile read in the epilogue itself stalled the block ~1.3 us per tile)
+    const size_t obase = ((size_t)b * a.H + oh0) * a.W;
+    const bf16_t* pf = bnb ? a.bnb.X : a.R;
+    uint4 pre[4];
+    if (pf) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = t + kT64 * u, row = min(c >> 3, npx - 1);
+        pre[u] = *reinterpret_cast<const uint4*>(pf + (obase + row) * 64 + (c & 7) * 8);
+      }
+    }
     if (tile + (int)gridDim.x < ntile) issue_halo(tile + gridDim.x, buf ^ 1);
     const char* halo = smem + WB + buf * HB;
     int hbase[1];
@@ -782,7 +908,7 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
       }
     }
     __syncthreads();
-    const size_t obase = ((size_t)b * a.H + oh0) * a.W;
+    if (bnb) za.reset();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {                      // 256 rows x 8 chunks of 16 B
       const int c = t + kT64 * u, row = c >> 3, cc = c & 7;
@@ -792,14 +918,17 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
         if (a.R) {
           float f[8], r[8];
           unpack8(v, f);
-          unpack8(*reinterpret_cast<const uint4*>(a.R + o), r);
+          unpack8(pre[u], r);
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] += r[e];
           v = pack8(f);
         }
         *reinterpret_cast<uint4*>(a.Y + o) = v;
+        if (bnb) za.add(v, pre[u]);
       }
     }
+    // BN-backward fold through sst (unused without fprop stats: [8 waves][2][64] floats)
+    if (bnb) za.flush<8, 8, 64>(sst, a.bnb, (size_t)tile, 64, 0);
     if (a.stats && t < 128) {
       const int which = t >> 6, n = t & 63;
       float sum = 0.f;
@@ -1014,7 +1143,7 @@ int hconv_geom(int Bn, int H, int W, int C, int NC, int R, int S, int stride, in
 }
 
 hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, float* stats, int Bn, int H, int W,
-                        int CA, int NC, const int* taps, hipStream_t st) {
+                        int CA, int NC, const int* taps, hipStream_t st, const BnbArgs* bnb = nullptr) {
   HconvArgs a{};
   int TH = 0, rtiles = 0;
   const int BM = hconv_geom(Bn, H, W, CA, NC, 3, 3, 1, 1, TH, rtiles);
@@ -1024,6 +1153,7 @@ hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, f
   a.Y = (bf16_t*)Y;
   a.R = (const bf16_t*)R;
   a.stats = stats;
+  if (bnb) a.bnb = *bnb;
   a.a_bytes = (uint32_t)((size_t)Bn * H * W * CA * 2);
   a.w_bytes = (uint32_t)((size_t)NC * 9 * CA * 2);
   a.Bn = Bn; a.H = H; a.W = W; a.CA = CA; a.NC = NC;
@@ -1188,21 +1318,36 @@ int pde_conv_wtdesc_bytes() { return (int)sizeof(WtDesc); }
 // dy2 / wt2 (optional): a 1x1 / stride-2 / pad-0 convolution of the same input with the same output
 // shape (a ResNet downsample) whose input gradient is accumulated in the same pass: its dy2 [Bn][OH][OW][N]
 // and transposed weights wt2 [C][1][N] are K stages of the (0, 0) phase (the only input pixels it reads)
+// rows of BN-backward partials a stride-1 dgrad with `bnb` writes: one per M tile of its kernel
+int pde_conv_dgrad_bnb_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad) {
+  if (stride != 1) return 0;
+  int TH = 0, rtiles = 0;
+  if (hconv_geom(Bn, H, W, N, C, R, S, stride, pad, TH, rtiles)) return Bn * rtiles;
+  return pde_conv_fprop_mtiles(Bn * H * W, C);
+}
+
+// bx / bsc / bsh / bmu / brs / bpart (optional, bx != nullptr; stride 1 only): BN-backward partials
+// of dX for a BN + ReLU whose input was bx (BnbArgs), into bpart[pde_conv_dgrad_bnb_rows][2][C]
 hipError_t pde_conv_dgrad(const void* dy, const void* wt, void* dx, const void* res, const void* dy2, const void* wt2,
                           int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW,
-                          hipStream_t st) {
+                          const void* bx, const float* bsc, const float* bsh, const float* bmu, const float* brs,
+                          float* bpart, hipStream_t st) {
   if (C % 64 || N % 64 || R * S > 9 || stride < 1 || stride > 2) return hipErrorInvalidValue;
   if (dy2 && (stride != 2 || !wt2 || (H - 1) / 2 + 1 != OH || (W - 1) / 2 + 1 != OW)) return hipErrorInvalidValue;
+  BnbArgs z{(const bf16_t*)bx, bsc, bsh, bmu, brs, bpart};
+  // (the epilogue prefetches one second input: the residual gradient or the BN input, not both)
+  if (bx && (stride != 1 || dy2 || res || !bsc || !bsh || !bmu || !brs || !bpart)) return hipErrorInvalidValue;
   {
     // stride-1 3x3 / pad-1: the input gradient is the flipped-tap conv of dy with Wt (halo path)
     int TH = 0, rtiles = 0;
     if (!dy2 && OH == H && OW == W && hconv_geom(Bn, H, W, N, C, R, S, stride, pad, TH, rtiles)) {
       int taps[9];
       for (int k = 0; k < 9; ++k) taps[k] = pack_tap(1 - k / 3, 1 - k % 3, k);
-      return launch_hconv(dy, wt, dx, res, nullptr, Bn, H, W, N, C, taps, st);
+      return launch_hconv(dy, wt, dx, res, nullptr, Bn, H, W, N, C, taps, st, bx ? &z : nullptr);
     }
   }
   IgemmArgs a{};
+  if (bx) a.bnb = z;
   a.A = (const bf16_t*)dy;
   a.W = (const bf16_t*)wt;
   a.Y = (bf16_t*)dx;

@@ -752,23 +752,35 @@ hipError_t pde_bnpool_bwd(const void* dp, const void* arg, const void* y, const 
 
 // relu with y == nullptr: the ReLU mask is recomputed from x with the forward's scale / shift (no
 // residual in the forward), so y is not read
+// pre_nblk > 0: `part` already holds [pre_nblk][2][C] reduction partials (summed by the dgrad epilogue
+// that produced dy, conv.hip BnbArgs; relu == 2 semantics, no dres) and is sized
+// pde_bn_part_rows(pre_nblk) x 2C: the reduce pass is skipped
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, const float* scale, const float* shift, float* part, float* coef,
-                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, hipStream_t st) {
+                      void* dgamma, void* dbeta, void* dx, void* dres, int relu, int pre_nblk, hipStream_t st) {
   if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
   if (relu && !y && (!scale || !shift)) return hipErrorInvalidValue;
   relu = !relu ? 0 : (y ? 1 : 2);
+  if (pre_nblk > 0 && (relu != 2 || dres)) return hipErrorInvalidValue;
   const int CP = C / 8, RP = 256 / CP;
-  const int nblk = pde_bn_blocks(M, C);
+  int nblk = pre_nblk > 0 ? pre_nblk : pde_bn_blocks(M, C);
   const int rpb = (M + nblk - 1) / nblk;
   // ReLU after a residual add: the reduce pass writes the masked gradient as dres, and the apply pass
   // reads it back as its (unmasked) dy -- 7 tensor passes instead of 8 (the apply no longer reads dy
   // and y, and writes one tensor)
   const bool res_first = relu == 1 && dres;
-  auto red = relu == 0 ? k_bn_bwd_reduce<0> : relu == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>;
-  hipLaunchKernelGGL(red, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)dy,
-                     (const uint4*)y, (const uint4*)x, mean, rstd, scale, shift, M, C, rpb, part,
-                     res_first ? (uint4*)dres : (uint4*)nullptr);
+  if (pre_nblk <= 0) {
+    auto red = relu == 0 ? k_bn_bwd_reduce<0> : relu == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>;
+    hipLaunchKernelGGL(red, dim3(nblk), dim3(256), (size_t)RP * 2 * C * sizeof(float), st, (const uint4*)dy,
+                       (const uint4*)y, (const uint4*)x, mean, rstd, scale, shift, M, C, rpb, part,
+                       res_first ? (uint4*)dres : (uint4*)nullptr);
+  } else if (nblk > kFoldThreshold) {   // thousands of per-tile rows: pre-fold as the forward does
+    float* folded = part + (size_t)nblk * 2 * C;
+    hipLaunchKernelGGL(k_fold_rows, dim3((2 * C + 255) / 256, kFoldRows), dim3(256), 0, st, part, nblk, 2 * C,
+                       (nblk + kFoldRows - 1) / kFoldRows, folded);
+    part = folded;
+    nblk = kFoldRows;
+  }
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, nblk, C, M,
                      (const bf16_t*)gamma, mean, rstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef);
   const int64_t n8 = (int64_t)M * CP;

@@ -4,7 +4,9 @@
 Forward:  y = relu(bn(x) + res)   -- 3 launches: partial stats, per-channel finalize (+ running-stat
           update), one streaming apply pass.
 Backward: dy' = dy * (y > 0); dres = dy'; dx = BN backward of dy'  -- reduce, finalize (writes
-          dgamma / dbeta), one streaming apply pass that also emits dres.
+          dgamma / dbeta), one streaming apply pass that also emits dres.  In a BasicBlock, bn1's
+          reduce is summed by conv2's dgrad epilogue instead (``_conv_bwd(..., bn=)``,
+          PDE_RESNET_BNB_FUSE; profiles/r4_models/bnb/README.md).
 Convolutions with C_in, C_out multiples of 64 and kernels up to 3x3 (every ResNet-18 conv but the
 3-channel stem) are implicit GEMMs on bf16 MFMA (``csrc/kernels/conv.hip``): fprop, phase-split
 dgrad and split-K wgrad; the stem has its own MFMA kernels (``csrc/kernels/stem.hip``).  A GPU
@@ -187,14 +189,20 @@ def _bn_fwd(x, part, nblk, gamma, beta, rm, rv, momentum, eps, res, relu):
     return y, mean, rstd, scale, shift
 
 
-def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shift=None):
+def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shift=None, pre=None):
     """``y=None`` with the forward's ``scale`` / ``shift``: the ReLU mask is recomputed from ``x`` (BN
-    without residual), so the backward passes read two tensors instead of three."""
+    without residual), so the backward passes read two tensors instead of three.  ``pre = (part, nblk)``:
+    the reduction partials were already summed by the dgrad epilogue that produced ``dy``
+    (``_conv_bwd(..., bn=...)``), so only the finalize and the apply pass run."""
     K = kernels()
     C = x.shape[1]
     M = x.numel() // C
     dev = x.device
-    part = torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev, dtype=torch.float32)
+    pre_nblk = 0
+    if pre is not None:
+        part, pre_nblk = pre
+    else:
+        part = torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev, dtype=torch.float32)
     coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
     dgamma = flat_grad_slot(gamma)
     dgamma = torch.empty(C, device=dev, dtype=gamma.dtype) if dgamma is None else dgamma
@@ -202,7 +210,7 @@ def _bn_bwd(dy, y, x, gamma, beta, mean, rstd, relu, want_dres, scale=None, shif
     dbeta = torch.empty(C, device=dev, dtype=gamma.dtype) if dbeta is None else dbeta
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if want_dres else None
-    K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, relu, scale, shift)
+    K.bn_bwd(dy, y, x, gamma, mean, rstd, part, coef, dgamma, dbeta, dx, dres, relu, scale, shift, pre_nblk)
     return dx, dgamma, dbeta, dres
 
 
@@ -244,12 +252,19 @@ def _take_wt(w):
     return v
 
 
-def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None, wt=None, ds_wt=None):
+def _bnb_enabled() -> bool:
+    return os.environ.get("PDE_RESNET_BNB_FUSE", "1") != "0"
+
+
+def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None, wt=None, ds_wt=None, bn=None):
     """(dx [+ res, fused into the dgrad epilogue] [+ the input gradient of a 1x1 / stride-2 downsample
     ``ds = (ds_dy, ds_w)`` of the same input, as extra K stages of the same dgrad pass], dw).
-    ``wt`` / ``ds_wt``: transposed weights already made by ``DgradWeights`` (else transposed here)."""
+    ``wt`` / ``ds_wt``: transposed weights already made by ``DgradWeights`` (else transposed here).
+    ``bn = (bx, scale, shift, mean, rstd)``: ``x`` was ``relu(bn(bx))``; the dgrad epilogue also sums that
+    BN's backward partials -- returned as a third value ``(part, nblk)`` for ``_bn_bwd(..., pre=)``."""
     K = kernels()
     dx = None
+    pre = None
     if need_dx:
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         ready = wt is not None and (ds is None or ds_wt is not None)
@@ -258,6 +273,13 @@ def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None, wt=None, d
             ds_wt = torch.empty(ds[1].numel(), device=w.device, dtype=w.dtype) if ds is not None else None
         if ds is not None:
             K.conv_dgrad(dy, w, wt, dx, stride, pad, res, ds[0], ds[1], ds_wt, wt_ready=ready)
+        elif bn is not None:
+            rows = K.conv_dgrad_bn_rows(x, w, stride, pad)
+            part = torch.empty(K.bn_part_rows(rows) * 2 * x.shape[1], device=x.device, dtype=torch.float32)
+            bx, sc, sh, mu, rs = bn
+            K.conv_dgrad(dy, w, wt, dx, stride, pad, res, wt_ready=ready, bn_x=bx, bn_scale=sc, bn_shift=sh,
+                         bn_mean=mu, bn_rstd=rs, bn_part=part)
+            pre = (part, rows)
         else:
             K.conv_dgrad(dy, w, wt, dx, stride, pad, res, wt_ready=ready)
     splits = K.conv_wgrad_splits(x, w, stride, pad)
@@ -266,7 +288,7 @@ def _conv_bwd(dy, x, w, stride, pad, need_dx=True, res=None, ds=None, wt=None, d
     if dw is None or not dw.is_contiguous(memory_format=torch.channels_last):
         dw = torch.empty_like(w, memory_format=torch.channels_last)
     K.conv_wgrad(dy, x, w, part, splits, dw, stride, pad)
-    return dx, dw
+    return (dx, dw, pre) if bn is not None else (dx, dw)
 
 
 class BasicBlockFn(torch.autograd.Function):
@@ -302,9 +324,13 @@ class BasicBlockFn(torch.autograd.Function):
         dout = _cl(dout)
         wt1, wt2, wtd = ctx.wts
         dy2, dg2, db2, dres = _bn_bwd(dout, out, y2, g2, b2, m2, s2, True, True)
-        da1, dw2 = _conv_bwd(dy2, a1, w2, 1, 1, wt=wt2)
-        # bn1 has no residual: its ReLU mask comes from y1 with the forward's scale / shift (a1 not read)
-        dy1, dg1, db1, _ = _bn_bwd(da1, None, y1, g1, b1, m1, s1, True, False, sc1, sh1)
+        # bn1 has no residual: its ReLU mask comes from y1 with the forward's scale / shift (a1 not read);
+        # its backward reduction is summed in conv2's dgrad epilogue (no pass re-reading da1)
+        if _bnb_enabled():
+            da1, dw2, pre1 = _conv_bwd(dy2, a1, w2, 1, 1, wt=wt2, bn=(y1, sc1, sh1, m1, s1))
+        else:
+            (da1, dw2), pre1 = _conv_bwd(dy2, a1, w2, 1, 1, wt=wt2), None
+        dy1, dg1, db1, _ = _bn_bwd(da1, None, y1, g1, b1, m1, s1, True, False, sc1, sh1, pre=pre1)
         dwd = dgd = dbd = None
         if wd is not None:
             dyd, dgd, dbd, _ = _bn_bwd(dres, idt, yd, gd, bd, md, sd, False, False)

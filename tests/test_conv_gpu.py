@@ -162,6 +162,67 @@ def test_conv_dgrad_residual_accumulate(B, C, H, W, N, k, s, p):
     assert torch.equal(dx1, (dx0.float() + res.float()).to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("B,C,H,W,N,k", [
+    (4, 64, 56, 56, 64, 3),     # k_hconv64 (layer1)
+    (24, 64, 56, 56, 64, 3),    # k_hconv64, 336 partial rows: the finalize's pre-fold
+    (2, 128, 28, 28, 128, 3),   # k_hconv<128, 128> (layer2)
+    (3, 64, 17, 23, 128, 3),    # k_hconv<256, 64>, ragged row tiles
+    (2, 512, 7, 7, 512, 3),     # k_igemm<128, 128> (layer4)
+    (3, 64, 9, 7, 128, 1),      # k_igemm<256, 64>, 1x1
+])
+def test_conv_dgrad_bn_partials(B, C, H, W, N, k):
+    """BN-backward reduction fused into the dgrad epilogue (conv.hip BnbArgs): dx unchanged (bitwise),
+    the partials == fp32 sums of d = dx * (bx*scale + shift > 0) and d * xhat, and bn_bwd from the
+    pre-summed partials == bn_bwd with its own reduce pass."""
+    torch.manual_seed(13)
+    K = kernels()
+    p = k // 2
+    dy = cl(torch.randn(B, N, H, W, device=dev).to(torch.bfloat16))
+    w = cl((torch.randn(N, C, k, k, device=dev) / (C * k * k) ** 0.5).to(torch.bfloat16))
+    bx = cl((torch.randn(B, C, H, W, device=dev) * 2 + 0.3).to(torch.bfloat16))
+    mean = torch.randn(C, device=dev) * 0.1 + 0.3
+    rstd = torch.rand(C, device=dev) + 0.5
+    gamma = (torch.rand(C, device=dev) + 0.5).to(torch.bfloat16)
+    beta = (torch.randn(C, device=dev) * 0.1).to(torch.bfloat16)
+    scale = gamma.float() * rstd
+    shift = beta.float() - mean * scale
+    wt = torch.empty(w.numel(), device=dev, dtype=w.dtype)
+    dx0 = torch.empty_like(bx)
+    K.conv_dgrad(dy, w, wt, dx0, 1, p)
+    rows = K.conv_dgrad_bn_rows(bx, w, 1, p)
+    assert rows > 0
+    part = torch.full((K.bn_part_rows(rows) * 2 * C,), float("nan"), device=dev)
+    dx = torch.empty_like(bx)
+    K.conv_dgrad(dy, w, wt, dx, 1, p, wt_ready=True, bn_x=bx, bn_scale=scale, bn_shift=shift, bn_mean=mean,
+                 bn_rstd=rstd, bn_part=part)
+    assert torch.equal(dx, dx0)
+    st = part[: rows * 2 * C].view(rows, 2, C).double().sum(0).cpu()
+    xf = bx.permute(0, 2, 3, 1).reshape(-1, C).double().cpu()
+    gf = dx.permute(0, 2, 3, 1).reshape(-1, C).double().cpu()
+    d = torch.where(xf * scale.double().cpu() + shift.double().cpu() > 0, gf, torch.zeros_like(gf))
+    ref_s = d.sum(0)
+    ref_q = (d * (xf - mean.double().cpu()) * rstd.double().cpu()).sum(0)
+    assert torch.allclose(st[0], ref_s, rtol=1e-4, atol=1e-2 + 1e-5 * d.abs().sum().item() / C)
+    assert torch.allclose(st[1], ref_q, rtol=1e-4, atol=1e-2 + 1e-5 * d.abs().sum().item() / C)
+    # bn_bwd: pre-summed partials vs the reduce pass
+    M = B * H * W
+    outs = []
+    for pre in (True, False):
+        pp = part if pre else torch.empty(K.bn_blocks(M, C) * 2 * C, device=dev)
+        coef = torch.empty(3 * C, device=dev)
+        dg = torch.empty(C, device=dev, dtype=torch.bfloat16)
+        db = torch.empty(C, device=dev, dtype=torch.bfloat16)
+        dxx = torch.empty_like(bx)
+        K.bn_bwd(dx, None, bx, gamma, mean, rstd, pp, coef, dg, db, dxx, None, True, scale, shift,
+                 rows if pre else 0)
+        outs.append((dg.float(), db.float(), dxx.float(), coef))
+    (g1, b1, x1, c1), (g2, b2, x2, c2) = outs
+    assert torch.allclose(g1, g2, rtol=1e-2, atol=1e-2 * g2.abs().max().item())
+    assert torch.allclose(b1, b2, rtol=1e-2, atol=1e-2 * b2.abs().max().item())
+    assert torch.allclose(c1, c2, rtol=1e-3, atol=1e-4 * c2.abs().max().item())
+    assert max_rel(x1, x2) < 1e-2
+
+
 @pytest.mark.parametrize("B,C,H,W,N", [(4, 64, 56, 56, 128), (3, 128, 14, 14, 256), (2, 64, 9, 7, 64)])
 def test_conv_dgrad_fused_downsample(B, C, H, W, N):
     """3x3 / s2 / p1 dgrad with a 1x1 / s2 / p0 downsample's input gradient as extra K stages of the
