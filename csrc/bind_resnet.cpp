@@ -27,18 +27,29 @@ void check_c(int64_t C) {
 
 int64_t bn_blocks(int64_t M, int64_t C) { return pde_bn_blocks((int)M, (int)C); }
 
-void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta,
+// y None: statistics / finalize only (mean, rstd, scale, shift and the running stats; no apply pass)
+// res_scale / res_shift (optional, with res): the residual is a BatchNorm input normalised on the fly,
+// y = relu(x*scale + shift + res*res_scale + res_shift) (a ResNet downsample branch, never materialised)
+void bn_fwd(const at::Tensor& x, const OptT& res, const OptT& y, const at::Tensor& gamma, const at::Tensor& beta,
             double eps, double momentum, const OptT& run_mean, const OptT& run_var, const at::Tensor& part,
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& scale, const at::Tensor& shift, bool relu,
-            bool training, int64_t pre_nblk) {
+            bool training, int64_t pre_nblk, const OptT& res_scale, const OptT& res_shift) {
   const int64_t M = nhwc_rows(x, "x"), C = x.size(1);
   check_c(C);
-  check_same(x, y, "y");
+  void* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_same(x, *y, "y");
+    yp = y->data_ptr();
+  }
+  TORCH_CHECK(yp || training, "bn_fwd: eval mode needs y");
   const void* r = nullptr;
   if (res.has_value() && res->defined()) {
     check_same(x, *res, "residual");
     r = res->data_ptr();
   }
+  const float* rsc = optr<float>(res_scale, "res_scale", F32, C);
+  const float* rsh = optr<float>(res_shift, "res_shift", F32, C);
+  TORCH_CHECK(!(rsc || rsh) || (r && rsc && rsh), "bn_fwd: res_scale / res_shift need res and each other");
   check_cuda(gamma, "gamma", BF16, C);
   check_cuda(beta, "beta", BF16, C);
   float* rm = optr<float>(run_mean, "running_mean", F32, C);
@@ -47,9 +58,9 @@ void bn_fwd(const at::Tensor& x, const OptT& res, const at::Tensor& y, const at:
     check_cuda(part, "part", F32,
                (pre_nblk > 0 ? pde_bn_part_rows((int)pre_nblk) : (int64_t)pde_bn_blocks((int)M, (int)C)) * 2 * C);
   for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
-  hip_check(pde_bn_fwd(x.data_ptr(), r, y.data_ptr(), (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
+  hip_check(pde_bn_fwd(x.data_ptr(), r, yp, (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
                        (float)momentum, rm, rv, ptr<float>(part), ptr<float>(mean), ptr<float>(rstd), ptr<float>(scale),
-                       ptr<float>(shift), relu, training, (int)pre_nblk, cur_stream()),
+                       ptr<float>(shift), relu, training, (int)pre_nblk, rsc, rsh, cur_stream()),
             "bn_fwd");
 }
 
@@ -172,7 +183,8 @@ void bnpool_fwd(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& 
   for (auto* t : {&mean, &rstd, &scale, &shift}) check_cuda(*t, "bn stats", F32, C);
   hip_check(pde_bn_fwd(y.data_ptr(), nullptr, nullptr, (int)M, (int)C, gamma.data_ptr(), beta.data_ptr(), (float)eps,
                        (float)momentum, ptr<float>(run_mean), ptr<float>(run_var), ptr<float>(part), ptr<float>(mean),
-                       ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), 1, 1, (int)pre_nblk, cur_stream()),
+                       ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), 1, 1, (int)pre_nblk, nullptr, nullptr,
+                       cur_stream()),
             "bnpool_fwd (finalize)");
   hip_check(pde_bnpool_fwd(y.data_ptr(), ptr<float>(scale), ptr<float>(shift), pooled.data_ptr(), arg.data_ptr(),
                            ysel.data_ptr(), (int)y.size(0), (int)C, (int)y.size(2), (int)y.size(3), (int)pooled.size(2),
@@ -434,7 +446,10 @@ void stem_wgrad(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& par
 
 void register_resnet(pybind11::module& m) {
   m.def("bn_blocks", &bn_blocks);
-  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
+        py::arg("momentum"), py::arg("run_mean"), py::arg("run_var"), py::arg("part"), py::arg("mean"), py::arg("rstd"),
+        py::arg("scale"), py::arg("shift"), py::arg("relu"), py::arg("training"), py::arg("pre_nblk"),
+        py::arg("res_scale") = py::none(), py::arg("res_shift") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("part"), py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dx"),
         py::arg("dres"), py::arg("relu"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),

@@ -193,7 +193,8 @@ int pde_bn_blocks(int M, int C);
 int pde_bn_part_rows(int pre_nblk);
 hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
                       float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
-                      float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk, hipStream_t st);
+                      float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk,
+                      const float* res_scale, const float* res_shift, hipStream_t st);
 hipError_t pde_bn_bwd(const void* dy, const void* y, const void* x, int M, int C, const void* gamma, const float* mean,
                       const float* rstd, const float* scale, const float* shift, float* part, float* coef,
                       void* dgamma, void* dbeta, void* dx, void* dres, int relu, int pre_nblk, hipStream_t st);

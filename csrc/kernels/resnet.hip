@@ -66,34 +66,48 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint4* __restrict__ X, i
 }
 
 // Sum the [nblk][2C] partials of the 64 channels [64*blockIdx.x, +64): 1024 threads = 64 channel
-// lanes x 16 waves striding over the partial rows, LDS fold.  Each lane keeps 8 row loads in flight
-// (these folds are latency-bound: with 2 in flight, 512 rows cost 16 dependent round trips, ~7 us).
+// lanes x 16 waves striding over the partial rows, LDS fold.  Each lane keeps 8 rows (16 loads) in
+// flight (these folds are latency-bound: with 2 in flight, 512 rows cost 16 dependent round trips, ~7 us).
 __device__ __forceinline__ void fold_partials(const float* __restrict__ part, int nblk, int C, int c, float& s,
                                               float& q) {
   __shared__ float sh[16][2][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cc = min(c, C - 1);
-  float sa[4] = {0.f, 0.f, 0.f, 0.f}, qa[4] = {0.f, 0.f, 0.f, 0.f};
-  int b = w;
-  for (; b + 48 < nblk; b += 64) {
-    float sv[4], qv[4];
+  // 8 rows (16 loads) in flight per lane: 512 partial rows are 4 dependent round trips, not 8
+  float sa[8], qa[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 8; ++u) sa[u] = qa[u] = 0.f;
+  int b = w;
+  for (; b + 112 < nblk; b += 128) {
+    float sv[8], qv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
       sv[u] = part[(size_t)(b + 16 * u) * 2 * C + cc];
       qv[u] = part[(size_t)(b + 16 * u) * 2 * C + C + cc];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       sa[u] += sv[u];
       qa[u] += qv[u];
     }
   }
-  for (; b < nblk; b += 16) {
-    sa[0] += part[(size_t)b * 2 * C + cc];
-    qa[0] += part[(size_t)b * 2 * C + C + cc];
+  {
+    // remainder (< 128 rows): up to 8 rows per wave, all loads issued before any is summed
+    float sv[8], qv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = b + 16 * u;
+      sv[u] = r < nblk ? part[(size_t)r * 2 * C + cc] : 0.f;
+      qv[u] = r < nblk ? part[(size_t)r * 2 * C + C + cc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      sa[u] += sv[u];
+      qa[u] += qv[u];
+    }
   }
-  sh[w][0][lane] = (sa[0] + sa[1]) + (sa[2] + sa[3]);
-  sh[w][1][lane] = (qa[0] + qa[1]) + (qa[2] + qa[3]);
+  sh[w][0][lane] = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
+  sh[w][1][lane] = ((qa[0] + qa[1]) + (qa[2] + qa[3])) + ((qa[4] + qa[5]) + (qa[6] + qa[7]));
   __syncthreads();
   s = 0.f;
   q = 0.f;
@@ -108,22 +122,32 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
 
 // out[y][c] = sum of partial rows [y*rows_per, (y+1)*rows_per) of part[nblk][W]: folds the many
 // per-tile partials of a conv epilogue (thousands of rows) before the per-channel finalize
-// (8 rows in flight per thread).
+// (16 rows in flight per thread).
 __global__ __launch_bounds__(256) void k_fold_rows(const float* __restrict__ part, int nblk, int W, int rows_per,
                                                    float* __restrict__ out) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= W) return;
   const int r0 = blockIdx.y * rows_per, r1 = min(nblk, r0 + rows_per);
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float a[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) a[u] = 0.f;
   int r = r0;
-  for (; r + 7 < r1; r += 8) {
-    float v[8];
+  for (; r + 15 < r1; r += 16) {       // 16 rows in flight: 56 rows (B = 256 layer1) in 4 round trips
+    float v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + u) * W + c];
+    for (int u = 0; u < 16; ++u) v[u] = part[(size_t)(r + u) * W + c];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += v[u];
+    for (int u = 0; u < 16; ++u) a[u] += v[u];
   }
-  for (; r < r1; ++r) a[0] += part[(size_t)r * W + c];
+  {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = r + u < r1 ? part[(size_t)(r + u) * W + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a[u] += v[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] += a[u + 8];
   out[(size_t)blockIdx.y * W + c] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
@@ -154,16 +178,31 @@ __global__ __launch_bounds__(1024) void k_bn_finalize(const float* __restrict__ 
 
 // y = x*scale + shift (+ res), optional relu.  The grid stride is a multiple of C/8, so each
 // thread's channel chunk is fixed: its 8 scale / shift values are loaded once.
+// rscale / rshift (optional): the residual is itself a BatchNorm input (a ResNet downsample branch,
+// bn_d(conv_d(x))), applied here as res*rscale + rshift -- the branch's normalised tensor is never
+// written and read back (one rounding instead of two)
 __global__ __launch_bounds__(256) void k_bn_apply(const uint4* __restrict__ X, const uint4* __restrict__ R,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  const float* __restrict__ rscale, const float* __restrict__ rshift,
                                                   uint4* __restrict__ Y, int64_t n8, int CP, int relu) {
   const int64_t i0 = blockIdx.x * 256ll + threadIdx.x;
   const int c0 = (int)(i0 & (CP - 1)) * 8;
-  float sc[8], sf[8];
+  float sc[8], sf[8], rc[8], rf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     sc[e] = scale[c0 + e];
     sf[e] = shift[c0 + e];
+    rc[e] = 1.f;
+    rf[e] = 0.f;
+  }
+  // one uniform branch around the vector loads (a per-element pointer-or-constant select became 16
+  // scalar loads behind branches: a prologue of dependent round trips that doubled the pass time)
+  if (rscale) {
+    const float4* a = reinterpret_cast<const float4*>(rscale + c0);
+    const float4* b = reinterpret_cast<const float4*>(rshift + c0);
+    const float4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+    rc[0] = a0.x; rc[1] = a0.y; rc[2] = a0.z; rc[3] = a0.w; rc[4] = a1.x; rc[5] = a1.y; rc[6] = a1.z; rc[7] = a1.w;
+    rf[0] = b0.x; rf[1] = b0.y; rf[2] = b0.z; rf[3] = b0.w; rf[4] = b1.x; rf[5] = b1.y; rf[6] = b1.z; rf[7] = b1.w;
   }
   for (int64_t i = i0; i < n8; i += (int64_t)gridDim.x * 256) {
     float v[8], r[8];
@@ -171,7 +210,7 @@ __global__ __launch_bounds__(256) void k_bn_apply(const uint4* __restrict__ X, c
     if (R) unpack8(R[i], r);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float o = v[e] * sc[e] + sf[e] + (R ? r[e] : 0.f);
+      float o = v[e] * sc[e] + sf[e] + (R ? r[e] * rc[e] + rf[e] : 0.f);
       v[e] = relu ? fmaxf(o, 0.f) : o;
     }
     Y[i] = pack8(v);
@@ -653,10 +692,12 @@ int pde_bn_blocks(int M, int C) {
 constexpr int kFoldThreshold = 256, kFoldRows = 64;
 int pde_bn_part_rows(int pre_nblk) { return pre_nblk > kFoldThreshold ? pre_nblk + kFoldRows : pre_nblk; }
 
+// res_scale / res_shift (optional, with res): the residual is normalised on the fly (k_bn_apply)
 hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, const void* gamma, const void* beta,
                       float eps, float momentum, float* run_mean, float* run_var, float* part, float* mean,
                       float* rstd, float* scale, float* shift, int relu, int training, int pre_nblk,
-                      hipStream_t st) {
+                      const float* res_scale, const float* res_shift, hipStream_t st) {
+  if ((res_scale || res_shift) && (!res || !res_scale || !res_shift)) return hipErrorInvalidValue;
   if (C % 8 != 0 || 256 % (C / 8) != 0) return hipErrorInvalidValue;
   const int CP = C / 8, RP = 256 / CP;
   if (training) {
@@ -684,7 +725,7 @@ hipError_t pde_bn_fwd(const void* x, const void* res, void* y, int M, int C, con
   const int64_t n8 = (int64_t)M * CP;
   if (y)   // y == nullptr: statistics / finalize only (the apply is fused into a consumer, e.g. k_bnpool_fwd)
     hipLaunchKernelGGL(k_bn_apply, dim3(grid_cap(n8, 4096)), dim3(256), 0, st, (const uint4*)x, (const uint4*)res,
-                       scale, shift, (uint4*)y, n8, CP, relu);
+                       scale, shift, res_scale, res_shift, (uint4*)y, n8, CP, relu);
   return hipGetLastError();
 }
 

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dY, c
 }
 
 // Sum per-block partials: out[k] = sum_b part[b][k], k < 2C; writes dgamma | dbeta as bf16 (or
-// accumulates into them when accumulate != 0).  Block = 64 columns x 16 row-groups (16 waves, 4
+// accumulates into them when accumulate != 0).  Block = 64 columns x 16 row-groups (16 waves, 8
 // independent loads each in flight: the pass is latency-bound, it has only 2C/64 blocks).
 __global__ __launch_bounds__(1024) void k_ln_reduce(const float* __restrict__ part, int nblk, int C2,
                                                     bf16_t* __restrict__ dG, bf16_t* __restrict__ dB, int C,
@@ -203,16 +203,25 @@ __global__ __launch_bounds__(1024) void k_ln_reduce(const float* __restrict__ pa
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
   const int kc = min(k, C2 - 1);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = 0.f;
   int b = w;
-  for (; b + 48 < nblk; b += 64) {
-    s0 += part[(size_t)b * C2 + kc];
-    s1 += part[(size_t)(b + 16) * C2 + kc];
-    s2 += part[(size_t)(b + 32) * C2 + kc];
-    s3 += part[(size_t)(b + 48) * C2 + kc];
+  for (; b + 112 < nblk; b += 128) {    // 8 rows in flight: 512 partial rows in 4 round trips
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + 16 * u) * C2 + kc];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
   }
-  for (; b < nblk; b += 16) s0 += part[(size_t)b * C2 + kc];
-  sh[w][lane] = (s0 + s1) + (s2 + s3);
+  {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = b + 16 * u < nblk ? part[(size_t)(b + 16 * u) * C2 + kc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
+  }
+  sh[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (w == 0 && k < C2) {
     float t = 0.f;

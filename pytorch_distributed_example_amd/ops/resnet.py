@@ -180,12 +180,17 @@ def _conv_fwd(x, w, stride, pad):
     return y, part, nblk
 
 
-def _bn_fwd(x, part, nblk, gamma, beta, rm, rv, momentum, eps, res, relu):
+def _bn_fwd(x, part, nblk, gamma, beta, rm, rv, momentum, eps, res, relu, apply=True, res_affine=None):
+    """Training BN(+res)(+ReLU) from the producing conv's statistics partials.  ``apply=False``: batch
+    statistics / running stats / scale / shift only (y is None).  ``res_affine = (scale, shift)``: ``res``
+    is a BN input normalised inside this apply pass (the downsample branch is never materialised)."""
     C = x.shape[1]
     dev = x.device
-    y = torch.empty_like(x)
+    y = torch.empty_like(x) if apply else None
     mean, rstd, scale, shift = (torch.empty(C, device=dev, dtype=torch.float32) for _ in range(4))
-    kernels().bn_fwd(x, res, y, gamma, beta, eps, momentum, rm, rv, part, mean, rstd, scale, shift, relu, True, nblk)
+    rsc, rsh = res_affine if res_affine is not None else (None, None)
+    kernels().bn_fwd(x, res, y, gamma, beta, eps, momentum, rm, rv, part, mean, rstd, scale, shift, relu, True, nblk,
+                     rsc, rsh)
     return y, mean, rstd, scale, shift
 
 
@@ -306,20 +311,22 @@ class BasicBlockFn(torch.autograd.Function):
         y2, p2, n2 = _conv_fwd(a1, w2, 1, 1)
         if wd is not None:
             yd, pd, nd = _conv_fwd(x, wd, stride, 0)
-            idt, md, sd, _, _ = _bn_fwd(yd, pd, nd, gd, bd, rmd, rvd, momentum, eps, None, False)
+            # downsample BN: statistics only; bn2's apply pass normalises yd on the fly (the branch
+            # output is never written; its backward, without ReLU, needs only yd)
+            _, md, sd, scd, shd = _bn_fwd(yd, pd, nd, gd, bd, rmd, rvd, momentum, eps, None, False, apply=False)
+            out, m2, s2, _, _ = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, yd, True, res_affine=(scd, shd))
         else:
             yd = md = sd = None
-            idt = x                                      # identity shortcut
-        out, m2, s2, _, _ = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, idt, True)
+            out, m2, s2, _, _ = _bn_fwd(y2, p2, n2, g2, b2, rm2, rv2, momentum, eps, x, True)   # identity shortcut
         ctx.save_for_backward(x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd,
-                              idt if wd is not None else None, m1, s1, m2, s2, md, sd, sc1, sh1)
+                              m1, s1, m2, s2, md, sd, sc1, sh1)
         ctx.stride = stride
         ctx.wts = (_take_wt(w1), _take_wt(w2), _take_wt(wd))   # batched dgrad transposes (or None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd, idt, m1, s1, m2, s2, md,
+        (x, w1, g1, b1, w2, g2, b2, wd, gd, bd, y1, a1, y2, out, yd, m1, s1, m2, s2, md,
          sd, sc1, sh1) = ctx.saved_tensors
         dout = _cl(dout)
         wt1, wt2, wtd = ctx.wts
@@ -333,7 +340,7 @@ class BasicBlockFn(torch.autograd.Function):
         dy1, dg1, db1, _ = _bn_bwd(da1, None, y1, g1, b1, m1, s1, True, False, sc1, sh1, pre=pre1)
         dwd = dgd = dbd = None
         if wd is not None:
-            dyd, dgd, dbd, _ = _bn_bwd(dres, idt, yd, gd, bd, md, sd, False, False)
+            dyd, dgd, dbd, _ = _bn_bwd(dres, None, yd, gd, bd, md, sd, False, False)
             if ctx.stride == 2 and tuple(wd.shape[2:]) == (1, 1):
                 # the downsample's input gradient rides along conv1's dgrad as extra K stages of its
                 # even-pixel phase: no second dgrad pass, no residual read
