@@ -833,8 +833,9 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
 
   const int wm = w, lr = l & 31, lh = l >> 5;            // 8 x 1 waves of 32 x 64
   const bool bnb = a.bnb.X != nullptr;
-  BnbAcc za;
+  BnbAcc za;                                           // accumulates over all of the block's tiles
   if (bnb) za.init(a.bnb, (t & 7) * 8);                 // a thread's chunk is the same in every tile
+  float st_acc = 0.f;                                  // fprop statistics, thread t < 128: (t >> 6, t & 63)
   issue_halo(blockIdx.x, 0);
   int it = 0;
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x, ++it) {
@@ -908,7 +909,6 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
       }
     }
     __syncthreads();
-    if (bnb) za.reset();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {                      // 256 rows x 8 chunks of 16 B
       const int c = t + kT64 * u, row = c >> 3, cc = c & 7;
@@ -927,15 +927,19 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
         if (bnb) za.add(v, pre[u]);
       }
     }
-    // BN-backward fold through sst (unused without fprop stats: [8 waves][2][64] floats)
-    if (bnb) za.flush<8, 8, 64>(sst, a.bnb, (size_t)tile, 64, 0);
     if (a.stats && t < 128) {
-      const int which = t >> 6, n = t & 63;
       float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sum += sst[(k * 2 + which) * 64 + n];
-      a.stats[((size_t)tile * 2 + which) * 64 + n] = sum;
+      for (int k = 0; k < 8; ++k) sum += sst[(k * 2 + (t >> 6)) * 64 + (t & 63)];
+      st_acc += sum;
     }
+  }
+  // one partial row per BLOCK (its tiles summed in a fixed order): <= #CUs rows, so the BN finalize
+  // reads them directly (no k_fold_rows pass over one row per tile, thousands at B = 256)
+  if (a.stats && t < 128) a.stats[((size_t)blockIdx.x * 2 + (t >> 6)) * 64 + (t & 63)] = st_acc;
+  if (bnb) {
+    __syncthreads();                                   // every wave is done with the last tile's LDS
+    za.flush<8, 8, 64>(reinterpret_cast<float*>(smem + WB), a.bnb, (size_t)blockIdx.x, 64, 0);
   }
 }
 
@@ -1142,6 +1146,32 @@ int hconv_geom(int Bn, int H, int W, int C, int NC, int R, int S, int stride, in
   return BM;
 }
 
+// k_hconv64 (persistent, C = NC = 64) runs this geometry: returns its grid (one block per CU, at most
+// one per row tile), else 0.  Its statistics / BN-backward partials are one row per block.
+int hconv64_grid(int Bn, int H, int W, int CA, int NC) {
+  static const bool persistent = [] {
+    const char* e = getenv("PDE_CONV_HALO_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  int TH = 0, rtiles = 0;
+  const int BM = hconv_geom(Bn, H, W, CA, NC, 3, 3, 1, 1, TH, rtiles);
+  if (!(BM == 256 && CA == 64 && NC == 64 && (TH + 2) * (W + 2) <= 8 * 44 && persistent)) return 0;   // 44 used
+  int ncu = 256, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || ncu < 1)
+    ncu = 256;
+  return min(Bn * rtiles, ncu);
+}
+
+// partial rows (statistics or BN-backward) a halo-path launch writes: one per block of k_hconv64, one
+// per row tile of k_hconv
+int hconv_part_rows(int Bn, int H, int W, int CA, int NC) {
+  const int g = hconv64_grid(Bn, H, W, CA, NC);
+  if (g) return g;
+  int TH = 0, rtiles = 0;
+  return hconv_geom(Bn, H, W, CA, NC, 3, 3, 1, 1, TH, rtiles) ? Bn * rtiles : 0;
+}
+
 hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, float* stats, int Bn, int H, int W,
                         int CA, int NC, const int* taps, hipStream_t st, const BnbArgs* bnb = nullptr) {
   HconvArgs a{};
@@ -1159,17 +1189,9 @@ hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, f
   a.Bn = Bn; a.H = H; a.W = W; a.CA = CA; a.NC = NC;
   a.TH = TH; a.rtiles = rtiles;
   for (int k = 0; k < 9; ++k) a.tap[k] = taps[k];
-  static const bool persistent = [] {
-    const char* e = getenv("PDE_CONV_HALO_PERSIST");
-    return !(e && e[0] == '0');
-  }();
-  if (BM == 256 && CA == 64 && NC == 64 && (TH + 2) * (W + 2) <= 8 * 44 && persistent) {   // k_hconv64: 44 used
+  if (const int g64 = hconv64_grid(Bn, H, W, CA, NC)) {
     a.ntiles = 1;
-    int ncu = 256, dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                  hipSuccess || ncu < 1)
-      ncu = 256;
-    hipLaunchKernelGGL(k_hconv64, dim3(min(Bn * rtiles, ncu)), dim3(kT64), 0, st, a);
+    hipLaunchKernelGGL(k_hconv64, dim3(g64), dim3(kT64), 0, st, a);
   } else if (BM == 256) {
     a.ntiles = NC / 64;
     hipLaunchKernelGGL((k_hconv<256, 64>), dim3(Bn * rtiles * a.ntiles), dim3(kThreads), 0, st, a);
@@ -1260,7 +1282,7 @@ int pde_conv_fprop_mtiles(int M, int N) { return N % 128 == 0 ? (M + 127) / 128 
 // rows of BN-statistics partials an fprop writes: one per M tile of whichever kernel runs it
 int pde_conv_stats_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad, int OH, int OW) {
   int TH = 0, rtiles = 0;
-  if (hconv_geom(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles)) return Bn * rtiles;
+  if (hconv_geom(Bn, H, W, C, N, R, S, stride, pad, TH, rtiles)) return hconv_part_rows(Bn, H, W, C, N);
   return pde_conv_fprop_mtiles(Bn * OH * OW, N);
 }
 
@@ -1322,7 +1344,7 @@ int pde_conv_wtdesc_bytes() { return (int)sizeof(WtDesc); }
 int pde_conv_dgrad_bnb_rows(int Bn, int H, int W, int C, int N, int R, int S, int stride, int pad) {
   if (stride != 1) return 0;
   int TH = 0, rtiles = 0;
-  if (hconv_geom(Bn, H, W, N, C, R, S, stride, pad, TH, rtiles)) return Bn * rtiles;
+  if (hconv_geom(Bn, H, W, N, C, R, S, stride, pad, TH, rtiles)) return hconv_part_rows(Bn, H, W, N, C);
   return pde_conv_fprop_mtiles(Bn * H * W, C);
 }
 

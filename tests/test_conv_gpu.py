@@ -78,10 +78,11 @@ def test_conv_exact_integer_data():
 
 
 @pytest.mark.parametrize("N", [64, 128])
-@pytest.mark.parametrize("B,H,W", [(3, 10, 9), (2, 12, 20), (2, 9, 56)])
+@pytest.mark.parametrize("B,H,W", [(3, 10, 9), (2, 12, 20), (2, 9, 56), (24, 56, 56)])
 def test_conv_fprop_bn_stats(N, B, H, W):
     """BN statistics partials from the conv epilogue (implicit GEMM for narrow images, the halo-tiled
-    kernel for W >= 14): one row per M tile of whichever kernel ran, folding to the batch sums."""
+    kernel for W >= 14): one row per M tile of whichever kernel ran (one per block of the persistent
+    k_hconv64, which at B=24 walks 336 row tiles on <= 256 blocks), folding to the batch sums."""
     torch.manual_seed(11)
     K = kernels()
     C = 64
@@ -164,7 +165,8 @@ def test_conv_dgrad_residual_accumulate(B, C, H, W, N, k, s, p):
 
 @pytest.mark.parametrize("B,C,H,W,N,k", [
     (4, 64, 56, 56, 64, 3),     # k_hconv64 (layer1)
-    (24, 64, 56, 56, 64, 3),    # k_hconv64, 336 partial rows: the finalize's pre-fold
+    (24, 64, 56, 56, 64, 3),    # k_hconv64 over 336 row tiles: one partial row per persistent block
+    (40, 128, 28, 28, 128, 3),  # k_hconv<128, 128>, 280 partial rows: the finalize's pre-fold
     (2, 128, 28, 28, 128, 3),   # k_hconv<128, 128> (layer2)
     (3, 64, 17, 23, 128, 3),    # k_hconv<256, 64>, ragged row tiles
     (2, 512, 7, 7, 512, 3),     # k_igemm<128, 128> (layer4)
