@@ -24,6 +24,13 @@ rank 0 prints one JSON line.  A failure still prints one JSON line (``value`` nu
 exits non-zero, and so does a communication-health failure (peer barrier time-out, RCCL error):
 a poisoned peer path skips its barriers and would otherwise report an inflated number.
 
+At N>1 every rank first times the comm-free single-GPU step on its own GPU (all ranks at once,
+before the communicator exists): the same-job W=1 anchor.  The line then carries
+``w1_anchor_images_per_s`` (mean over ranks), ``scaling_eff_same_job`` = (value / N) / anchor, and
+``per_rank``: every rank's device (index, UUID), RCCL communicator size and device, and peer-path
+status, all-gathered; a repeated device or an RCCL communicator whose size is not N (the reference's
+every-rank-on-GPU-0 bug, /root/reference/mnist/main.py:181-182) fails the run with an error line.
+
 At W=1 the line also carries ``w1_rccl_comm``: the same step measured a second time with an RCCL
 communicator initialised and the full W>1 communication path running (config 2 of BASELINE.json:
 "DDP world_size=1 ... RCCL init + HIP kernels"); the headline ``value`` stays the comm-free step.
@@ -134,7 +141,114 @@ def _comm_info(dist, comm, eng):
     return info
 
 
-def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world: bool):
+def _device_id(local_rank: int) -> str:
+    """A node-unique identity of this rank's GPU (UUID, else PCI bus id, else the index)."""
+    if os.environ.get("PDE_BENCH_STUB") == "1":        # CPU control-flow rehearsal (tests)
+        return os.environ.get("PDE_BENCH_STUB_DEV", f"stub-gpu-{local_rank}")
+    import torch
+
+    props = torch.cuda.get_device_properties(local_rank)
+    for attr in ("uuid", "pci_bus_id"):
+        v = getattr(props, attr, None)
+        if v not in (None, "", 0):
+            return f"{attr}:{v}"
+    return f"index:{local_rank}"
+
+
+def _rank_row(job: _Job, comm) -> dict:
+    info = _comm_info(None, comm, None) if comm is not None else {}
+    return {"rank": job.rank, "local_rank": job.local_rank, "host": socket.gethostname(),
+            "device": job.local_rank, "device_id": _device_id(job.local_rank),
+            "rccl_world": info.get("rccl_world"), "rccl_device": info.get("rccl_device"),
+            "peer_ok": info.get("peer_ok"), "peer_reason": info.get("peer_reason", "")[:200]}
+
+
+def _gather_rows(row: dict, world: int) -> list:
+    """All-gather one JSON-able dict per rank over the host control path (fixed-size byte image)."""
+    import torch
+
+    from pytorch_distributed_example_amd import dist
+
+    if world == 1 or not dist.is_initialized():
+        return [row]
+    width = 1024
+    b = json.dumps(row).encode()[:width]
+    t = torch.zeros(world, width, dtype=torch.int32)        # one row per rank, summed = concatenated
+    t[job_rank(row)][: len(b)] = torch.tensor(list(b), dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [json.loads(bytes(r[r > 0].tolist()).decode()) for r in t]
+
+
+def job_rank(row: dict) -> int:
+    return int(row["rank"])
+
+
+def validate_ranks(rows: list, world: int, shared_gpu: bool = False) -> str:
+    """'' if every rank ran on its own GPU with an N-rank communicator, else what is wrong
+    (``shared_gpu``: the one-GPU rehearsal, where every rank is on cuda:0 by design)."""
+    if len(rows) != world or sorted(r["rank"] for r in rows) != list(range(world)):
+        return f"expected {world} rank rows, got ranks {sorted(r.get('rank') for r in rows)}"
+    seen = {}
+    for r in rows if not shared_gpu else []:
+        key = (r["host"], r["device_id"])
+        if key in seen:
+            return (f"ranks {seen[key]} and {r['rank']} share one GPU ({r['device_id']} on {r['host']}): "
+                    f"every rank must own a device")
+        seen[key] = r["rank"]
+    for r in rows:
+        if r.get("rccl_world") is not None and r["rccl_world"] != world:
+            return f"rank {r['rank']}: RCCL communicator has {r['rccl_world']} ranks, not {world}"
+        if r.get("rccl_device") is not None and r["rccl_device"] != r["device"]:
+            return f"rank {r['rank']}: RCCL communicator on device {r['rccl_device']}, rank on {r['device']}"
+    ok = {bool(r.get("peer_ok")) for r in rows}
+    if len(ok) > 1:
+        return "the xGMI peer path is enabled on some ranks only (the set-up vote must be collective)"
+    return ""
+
+
+class _StubEngine:
+    """PDE_BENCH_STUB=1 (CPU tests only): the engine surface ``bench.py`` drives, with a sleep per
+    step instead of GPU kernels, so the N>1 control flow (self-launch, anchor, gather, validation,
+    the JSON line) runs on a machine without a GPU.  Its numbers are not measurements."""
+
+    def __init__(self, comm):
+        self.comm, self.comm_on, self.mode, self.samples = comm, comm is not None, "stub", 0
+
+    def replay(self, B=None, steps=1):
+        time.sleep(50e-6 * steps)
+        if self.comm is not None:
+            import torch
+
+            from pytorch_distributed_example_amd import dist
+            dist.all_reduce(torch.zeros(1))
+
+    def step(self, B=None):
+        self.replay(B, 1)
+
+    def prime_graphs(self, *a, **k):
+        pass
+
+    def reset_meters(self):
+        pass
+
+    def read_meters(self, reset=True):
+        return 0.0, 0, 0
+
+
+def _init_group(job: _Job):
+    """The job's process group (RCCL; gloo for the shared-GPU rehearsal and the CPU stub)."""
+    from pytorch_distributed_example_amd import dist
+    from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
+
+    if dist.is_initialized():
+        return
+    init = "env://" if "MASTER_PORT" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
+    backend = "gloo" if job.args.shared_gpu or os.environ.get("PDE_BENCH_STUB") == "1" else "nccl"
+    with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
+        dist.init_process_group(backend, init_method=init, rank=job.rank, world_size=job.world)
+
+
+def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world: bool, max_over_ranks: bool = True):
     """Builds the engine, times ``steps`` steps, returns (elapsed_s, eng, comm, extra)."""
     import torch
 
@@ -145,15 +259,17 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
     args, world, rank = job.args, job.world, job.rank
-    dev = torch.device("cuda", job.local_rank)
     comm = None
+    if os.environ.get("PDE_BENCH_STUB") == "1":
+        if comm_world:
+            _init_group(job)
+        eng = _StubEngine(True if comm_world and world > 1 else None)
+        return _timed_window(job, eng, None, {}, lambda n, S=1: eng.replay(steps=n), steps, warmup,
+                             max_over_ranks=max_over_ranks)
+    dev = torch.device("cuda", job.local_rank)
     with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
         if comm_world:
-            if not dist.is_initialized():
-                init = ("env://" if "MASTER_PORT" in os.environ
-                        else f"tcp://127.0.0.1:{_free_port()}")
-                dist.init_process_group("gloo" if args.shared_gpu else "nccl", init_method=init, rank=rank,
-                                        world_size=world)
+            _init_group(job)
             comm = dist.engine_comm(allow_host_only=args.shared_gpu)
         net = build_net(seed=args.seed, device=dev)
         if comm is not None:
@@ -198,7 +314,7 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
         eng.prime_graphs(tuple(sorted({S, Sw, 1})), replays=max(1, args.prime_replays))
     _clock_warm(args, eng, run, S)
     try:
-        return _timed_window(job, eng, comm, extra, run, steps, warmup, Sw)
+        return _timed_window(job, eng, comm, extra, run, steps, warmup, Sw, max_over_ranks=max_over_ranks)
     finally:
         if gc_off:
             gc.enable()
@@ -240,21 +356,29 @@ def _device_barrier(comm, dist):
     torch.cuda.synchronize()
 
 
-def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1):
+def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1, max_over_ranks=True):
+    """W warm-up steps, then exactly K timed steps bracketed by barrier + device synchronize on both
+    sides.  ``max_over_ranks``: the elapsed time is the MAX over ranks (the job's step time); off for
+    the per-rank W=1 anchor, whose ranks still start together (host barrier) but time alone."""
     import torch
 
     from pytorch_distributed_example_amd import dist
 
+    stub = os.environ.get("PDE_BENCH_STUB") == "1"
+    sync = (lambda: None) if stub else torch.cuda.synchronize
     world = job.world
+    grouped = dist.is_initialized() and world > 1
     run(warmup, Sw)
     # meters cover the timed steps only: zeroed on the stream (no .item() round trips: every idle
     # microsecond before the window lets the GPU clock down, profiles/r3_window/)
     eng.reset_meters()
-    torch.cuda.synchronize()
+    sync()
     if comm is not None:
         _device_barrier(comm, dist)
-    torch.cuda.synchronize()
-    trace = os.environ.get("PDE_BENCH_TRACE") == "1"
+    elif grouped:
+        dist.barrier()
+    sync()
+    trace = os.environ.get("PDE_BENCH_TRACE") == "1" and not stub
     if trace:       # diagnostics only: GPU-clocked window and host launch time, to stderr
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -263,15 +387,19 @@ def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1):
     t_launch = time.perf_counter() - t0
     if trace:
         ev1.record()
-    torch.cuda.synchronize()
+    sync()
+    t_end = time.perf_counter()
     if comm is not None:
         _device_barrier(comm, dist)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        sync()
+        t_end = time.perf_counter()
+    elif grouped and max_over_ranks:
+        dist.barrier()
+    elapsed = (time.perf_counter() if max_over_ranks else t_end) - t0
     if trace:
         print(json.dumps({"trace_host_us": round(elapsed * 1e6, 1), "trace_launch_us": round(t_launch * 1e6, 1),
                           "trace_gpu_us": round(ev0.elapsed_time(ev1) * 1e3, 1)}), file=sys.stderr)
-    if comm is not None and world > 1:
+    if grouped and max_over_ranks:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -282,15 +410,44 @@ def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1):
     return elapsed, eng, comm, extra
 
 
+def _w1_anchor(job: _Job):
+    """N>1: every rank times the comm-free single-GPU step on its own GPU, all at once (host barrier
+    before the window), before the communicator exists.  Returns the per-rank images/s list."""
+    import torch
+
+    from pytorch_distributed_example_amd import dist
+
+    args = job.args
+    e, eng, _, _ = _run_lenet(job, False, args.steps, args.warmup, comm_world=False, max_over_ranks=False)
+    v = torch.zeros(job.world, dtype=torch.float64)
+    v[job.rank] = args.steps * args.batch_size / e
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    del eng
+    gc.collect()
+    if os.environ.get("PDE_BENCH_STUB") != "1":
+        torch.cuda.synchronize()
+    return [round(x, 1) for x in v.tolist()]
+
+
 def lenet_main(job: _Job):
     import torch
 
     from pytorch_distributed_example_amd import dist
 
     args, world, rank = job.args, job.world, job.rank
-    torch.cuda.set_device(job.local_rank)
+    stub = os.environ.get("PDE_BENCH_STUB") == "1"
+    if not stub:
+        torch.cuda.set_device(job.local_rank)
     comm_world = world > 1 or args.force_comm
+    anchors = None
+    if world > 1:
+        _init_group(job)                  # the group first: the anchor's ranks start together
+        anchors = _w1_anchor(job)
     elapsed, eng, comm, extra = _run_lenet(job, args.force_comm, args.steps, args.warmup, comm_world)
+    rows = _gather_rows(_rank_row(job, comm), world)
+    bad = validate_ranks(rows, world, args.shared_gpu) if world > 1 else ""
+    if bad:
+        raise RuntimeError(f"rank placement check failed: {bad}")
     loss_sum, correct, _ = eng.read_meters()
     n_img = args.steps * args.batch_size * world
     ips = n_img / elapsed
@@ -325,7 +482,15 @@ def lenet_main(job: _Job):
         "speedup_vs_stock_torch_per_gpu": round(ips / world / STOCK_TORCH_W1, 2),
         "train_loss_mean_timed_rank0": round(loss_sum / max(1, args.steps * args.batch_size), 5),
         "train_acc_timed_rank0": round(correct / max(1, args.steps * args.batch_size), 5),
+        "per_rank": rows,
     }
+    if anchors:
+        a1 = sum(anchors) / len(anchors)
+        out["w1_anchor_images_per_s"] = round(a1, 1)
+        out["w1_anchor_per_rank"] = anchors
+        out["scaling_eff_same_job"] = round(ips / world / a1, 4)
+    if stub:
+        out["data"] = "STUB (PDE_BENCH_STUB=1: CPU control-flow test, sleep per step, not a measurement)"
     want_fig = args.comm_figure == "on" or (args.comm_figure == "auto" and world == 1 and not args.force_comm)
     if want_fig and world == 1:
         # config 2 (BASELINE.json): the same step with RCCL initialised and the comm path running

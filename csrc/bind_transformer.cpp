@@ -151,6 +151,7 @@ void scale_bf16(const at::Tensor& x, const at::Tensor& s) {
   check_cuda(x, "x", BF16);
   check_cuda(s, "s", F32, 1);
   TORCH_CHECK(x.numel() % 8 == 0, "scale_bf16: numel % 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "scale_bf16: x must be 16-byte aligned (uint4 accesses)");
   hip_check(pde_scale_bf16(x.data_ptr(), ptr<float>(s), x.numel(), cur_stream()), "scale_bf16");
 }
 

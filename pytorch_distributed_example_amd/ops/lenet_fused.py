@@ -35,20 +35,18 @@ class LeNetWorkspace:
         self.Wp = torch.zeros(2 * 72 * 256, **f32)       # v2 conv2 weight image (padding stays zero)
 
 
-_SCRATCH = {}
-
-
-def _bwd2_scratch(device, B):
+def _bwd2_scratch(ws: "LeNetWorkspace"):
     """Reduction scratch of the v2 conv backward ("ext" mode): 16 conv2 slabs, per-image conv1
-    partials, and the fold-mode buffers the kernel signature carries (unused here)."""
-    key = (str(device), B)
-    sc = _SCRATCH.get(key)
+    partials, and the fold-mode buffers the kernel signature carries (unused here).  Owned by the
+    forward's workspace (``ctx.ws``), like ``Wp``: two backwards in flight at once (two models,
+    side streams, graph capture on different streams) never share a slab."""
+    sc = getattr(ws, "bwd2_scratch", None)
     if sc is None:
-        f32 = dict(device=device, dtype=torch.float32)
-        sc = {"slab": torch.zeros(16 * 25088, **f32), "c1img": torch.zeros(B * 520, **f32),
-              "c1rep": torch.zeros(16 * 576, device=device, dtype=torch.int64),
-              "c1part": torch.zeros(16 * 576, **f32), "tick": torch.zeros(32, device=device, dtype=torch.int32)}
-        _SCRATCH[key] = sc
+        f32 = dict(device=ws.P1.device, dtype=torch.float32)
+        sc = {"slab": torch.zeros(16 * 25088, **f32), "c1img": torch.zeros(ws.B * 520, **f32),
+              "c1rep": torch.zeros(16 * 576, device=ws.P1.device, dtype=torch.int64),
+              "c1part": torch.zeros(16 * 576, **f32), "tick": torch.zeros(32, device=ws.P1.device, dtype=torch.int32)}
+        ws.bwd2_scratch = sc
     return sc
 
 
@@ -104,7 +102,7 @@ class LeNetFunction(torch.autograd.Function):
         K.lenet_fc_bwd(ws.P2, ws.H1, ws.dZ1, ws.dZ2, w1f.detach().contiguous(), B, ws.dP2m, gw1f, gb1f, gw2f, gb2f,
                        None, None, None, None)
         if B <= 128:
-            sc = _bwd2_scratch(dev, B)
+            sc = _bwd2_scratch(ws)
             c1w, c1b, c2w, c2b = 0, 500, 520, 25520           # flat offsets of the views above
             K.lenet_conv_bwd2(xf, ws.P1, ws.A1, ws.dP2m, ws.A2, w2c.detach().contiguous(), B, sc["slab"], sc["c1rep"],
                               sc["c1part"], sc["tick"], grads, c1w, c1b, c2w, c2b, defer=2, c1img=sc["c1img"])

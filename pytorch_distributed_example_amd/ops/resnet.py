@@ -533,12 +533,15 @@ class HeadFn(torch.autograd.Function):
         kernels().avgpool_fwd(x, pooled)
         ctx.xshape = x.shape
         ctx.bias = b
+        ctx.wparam = w
         ctx.pad = (-O) % 8
         if ctx.pad:
             wp = torch.zeros(O + ctx.pad, C, device=w.device, dtype=w.dtype)
             wp[:O].copy_(w)
-            bp = torch.zeros(O + ctx.pad, device=b.device, dtype=b.dtype)
-            bp[:O].copy_(b)
+            bp = None
+            if b is not None:
+                bp = torch.zeros(O + ctx.pad, device=b.device, dtype=b.dtype)
+                bp[:O].copy_(b)
             ctx.save_for_backward(pooled, wp)
             return G.fprop(pooled, wp, bp)[:, :O].contiguous()
         ctx.save_for_backward(pooled, w)
@@ -549,16 +552,25 @@ class HeadFn(torch.autograd.Function):
         from . import gemm as G
         pooled, w = ctx.saved_tensors
         dl = dlogits.contiguous()
+        want_db = ctx.bias is not None
         if ctx.pad:
             O = dl.shape[1]
             dlp = torch.zeros(dl.shape[0], O + ctx.pad, device=dl.device, dtype=dl.dtype)
             dlp[:, :O].copy_(dl)
             dpooled = G.dgrad(dlp, w)
-            dwp, dbp = G.wgrad(dlp, pooled, want_db=True)
-            dw, db = dwp[:O].contiguous(), dbp[:O].contiguous()
+            dwp, dbp = G.wgrad(dlp, pooled, want_db=want_db)
+            # the padded rows are sliced off; the real rows go straight into the flat gradient slots
+            # (when the parameters are flat-bound) so DDP's hook finds them in place, no copy per step
+            dw = flat_grad_slot(ctx.wparam)
+            dw = dw.copy_(dwp[:O]) if dw is not None else dwp[:O].contiguous()
+            db = None
+            if want_db:
+                db = flat_grad_slot(ctx.bias)
+                db = db.copy_(dbp[:O]) if db is not None else dbp[:O].contiguous()
         else:
             dpooled = G.dgrad(dl, w)
-            dw, db = G.wgrad(dl, pooled, dw=flat_grad_slot(w), db=flat_grad_slot(ctx.bias), want_db=True)
+            dw, db = G.wgrad(dl, pooled, dw=flat_grad_slot(w),
+                             db=flat_grad_slot(ctx.bias) if want_db else None, want_db=want_db)
         dx = torch.empty(ctx.xshape, device=dl.device, dtype=dl.dtype, memory_format=torch.channels_last)
         kernels().avgpool_bwd(dpooled, dx)
         return dx, dw, db

@@ -71,6 +71,10 @@ from ..utils import profiling as prof
 from .flat import FlatLayout, reverse_order_buckets
 
 
+# buffer dtypes whose values widen to fp32 without loss (the peer-route buffer broadcast)
+_WIDE_EXACT = (torch.float32, torch.bfloat16, torch.float16)
+
+
 class _Bucket:
     def __init__(self, index: int, names: List[str], start: int, end: int):
         self.index = index
@@ -219,30 +223,42 @@ class DistributedDataParallel(nn.Module):
         """Rank-0 buffers to every rank with collectives that stay on the GPU (hipGraph-capturable):
         RCCL broadcast when the group has it; otherwise (host-only control group, ranks sharing a GPU)
         the peer all-reduce of a flat fp32 image that only the source rank fills -- x + 0 + ... + 0 is
-        exactly x.  Integer buffers (BatchNorm's num_batches_tracked) ride along as fp32 (exact below
-        2^24).  Without either, the host-staged broadcast (not capturable)."""
+        exactly x.  The image is exact for every dtype: fp32 / bf16 / fp16 buffers widen to fp32
+        losslessly; any other dtype (int64 counters such as BatchNorm's num_batches_tracked, fp64,
+        bool) travels as its raw bytes, one byte per fp32 lane (0..255, exact).  The image is reduced
+        in pieces of at most the peer buffer's capacity.  Without either route, the host-staged
+        broadcast (not capturable)."""
         g = self.process_group
-        src = g.ranks[0]
         if getattr(g, "rccl", None) is not None or self._peer is None or bufs[0].device.type != "cuda":
-            dist.broadcast_coalesced(bufs, src, group=g)
+            dist.broadcast_coalesced(bufs, g.ranks[0], group=g)
             return
-        if self._bcast is None or self._bcast.numel() != sum(b.numel() for b in bufs):
-            self._bcast = torch.empty(max(8, sum(b.numel() for b in bufs)), device=self.device, dtype=torch.float32)
+        lanes = [b.numel() if b.dtype in _WIDE_EXACT else b.numel() * b.element_size() for b in bufs]
+        total = max(8, sum(lanes))
+        if self._bcast is None or self._bcast.numel() != total:
+            self._bcast = torch.empty(total, device=self.device, dtype=torch.float32)
         flat = self._bcast
-        o = 0
         if g.rank() == 0:
-            for b in bufs:
-                flat[o:o + b.numel()].copy_(b.reshape(-1))
-                o += b.numel()
+            o = 0
+            for b, n in zip(bufs, lanes):
+                src = b.reshape(-1) if b.dtype in _WIDE_EXACT else b.contiguous().reshape(-1).view(torch.uint8)
+                flat[o:o + n].copy_(src)
+                o += n
             flat[o:].zero_()
         else:
             flat.zero_()
-        self._peer.native.all_reduce_f32(flat.data_ptr(), flat.data_ptr(), flat.numel(), 1.0, 0,
-                                         torch.cuda.current_stream(self.device).cuda_stream)
+        piece = max(8, (self._peer.capacity_bytes // 4) // 8 * 8)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for off in range(0, total, piece):
+            cnt = min(piece, total - off)
+            self._peer.native.all_reduce_f32(flat.data_ptr() + 4 * off, flat.data_ptr() + 4 * off, cnt, 1.0, 0,
+                                             stream)
         o = 0
-        for b in bufs:
-            b.copy_(flat[o:o + b.numel()].view_as(b))
-            o += b.numel()
+        for b, n in zip(bufs, lanes):
+            if b.dtype in _WIDE_EXACT:
+                b.copy_(flat[o:o + n].view_as(b))
+            else:
+                b.copy_(flat[o:o + n].to(torch.uint8).view(b.dtype).view_as(b))
+            o += n
 
     @contextlib.contextmanager
     def no_sync(self):

@@ -332,6 +332,33 @@ def case_ddp_peer_bf16(cap_mb="32"):
     dist.destroy_process_group()
 
 
+def case_ddp_peer_buffers():
+    """DDP's per-forward buffer broadcast on the peer route (host-only control group, ranks sharing
+    one GPU): an fp32 buffer larger than the peer capacity (chunked image), a bf16 buffer, an int64
+    counter above 2^24 and an fp64 buffer must all arrive bit-exact from rank 0 (advisor r4)."""
+    from pytorch_distributed_example_amd.parallel import DistributedDataParallel
+
+    dev = _shared_gpu_init()
+    torch.manual_seed(0)
+    net = torch.nn.Linear(64, 64).to(dev)
+    g = torch.Generator().manual_seed(7 + R)
+    net.register_buffer("big", torch.randn(40_003, generator=g).to(dev))
+    net.register_buffer("half", torch.randn(333, generator=g).to(dev, torch.bfloat16))
+    net.register_buffer("count", torch.tensor([(1 << 40) + 12_345 + R], dtype=torch.int64, device=dev))
+    net.register_buffer("dbl", (torch.randn(17, generator=g, dtype=torch.float64) * 1e-300).to(dev))
+    net.register_buffer("flag", torch.tensor([R % 2 == 0, True, R % 2 == 1], device=dev))
+    ddp = DistributedDataParallel(net, reduce_route="peer", peer_capacity_mb=0.0625, init_sync=False)
+    assert ddp._peer is not None and ddp._peer.capacity_bytes < 40_003 * 4, ddp.peer_reason
+    ddp(torch.randn(4, 64, device=dev)).sum().backward()
+    torch.cuda.synchronize()
+    sig = {n: b.detach().cpu().contiguous().view(torch.uint8).tolist() if b.dtype != torch.bool else b.tolist()
+           for n, b in net.named_buffers()}
+    import hashlib
+    emit({"rank": R, "sig": {n: hashlib.sha1(json.dumps(v).encode()).hexdigest() for n, v in sig.items()},
+          "count": int(net.count.item()), "peer_error": ddp._peer.error()})
+    dist.destroy_process_group()
+
+
 def case_ddp_peer_skew(sleep_s="6", steps="4"):
     """rank 1 sleeps ``sleep_s`` before one backward.  Past the peer barrier
     timeout (PDE_PEER_TIMEOUT_MS, set by the test) the timed-out call must write NaN and DDP must

@@ -174,3 +174,66 @@ def test_bench_refuses_world_size_mismatch():
     assert p.returncode == 2
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["value"] is None and "WORLD_SIZE=1" in out["error"] and out["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, "1"), (4, "2")])
+def test_bench_forced_peer_failure_on_one_rank_is_collective(world, fail_rank):
+    """Verdict r4 item 1: a peer-setup failure injected on ONE rank of W leaves EVERY rank on
+    RCCL-only routes and schedules (the set-up vote is collective), reported with a reason."""
+    rc, res, logs = run_ranks("bench_peer_fail", world, extra_env={"PDE_PEER_FORCE_FAIL": fail_rank})
+    assert rc == 0, logs
+    assert all(r and r["ok"] for r in res), logs
+    assert "forced" in res[int(fail_rank)]["reason"]
+    assert all(r["reason"] for r in res)
+
+
+def _bench_stub(world, extra_env=None):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PDE_BENCH_STUB="1", **(extra_env or {}))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "20",
+                        "--warmup", "5", "--no-spin-wait"], capture_output=True, text=True, env=env, timeout=180)
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, (p.stdout, p.stderr[-2000:])
+    return p.returncode, json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_multi_rank_line_carries_anchor_and_rank_devices(world):
+    """Verdict r4 item 1c: ``bench.py --gpus N`` (self-launched, CPU stub engine) emits ONE line with
+    the same-job W=1 anchor, ``scaling_eff_same_job`` and every rank's device row."""
+    rc, d = _bench_stub(world)
+    assert rc == 0, d
+    assert d["n_gpus"] == world and d["value"] > 0
+    assert [r["rank"] for r in d["per_rank"]] == list(range(world))
+    assert len({r["device_id"] for r in d["per_rank"]}) == world
+    assert len(d["w1_anchor_per_rank"]) == world and d["w1_anchor_images_per_s"] > 0
+    assert abs(d["scaling_eff_same_job"] - d["value"] / world / d["w1_anchor_images_per_s"]) < 1e-3
+    assert d["data"].startswith("STUB")
+
+
+def test_bench_multi_rank_repeated_device_fails():
+    """Every rank reporting the same GPU (the reference's all-on-GPU-0 bug, mnist/main.py:181-182)
+    makes the run fail with an error line instead of a number."""
+    rc, d = _bench_stub(2, {"PDE_BENCH_STUB_DEV": "gpu-0"})
+    assert rc != 0 and d["value"] is None
+    assert "share one GPU" in d["error"]
+
+
+def test_bench_validate_ranks_rules():
+    import bench
+    row = lambda r, **k: dict({"rank": r, "host": "h", "device": r, "device_id": f"u{r}", "rccl_world": 4,
+                               "rccl_device": r, "peer_ok": True}, **k)
+    good = [row(r) for r in range(4)]
+    assert bench.validate_ranks(good, 4) == ""
+    assert "share one GPU" in bench.validate_ranks([row(0), row(1, device_id="u0"), row(2), row(3)], 4)
+    assert bench.validate_ranks([row(0), row(1, device_id="u0"), row(2), row(3)], 4, shared_gpu=True) == ""
+    assert "3 ranks, not 4" in bench.validate_ranks([row(0), row(1), row(2, rccl_world=3), row(3)], 4)
+    assert "on device 0" in bench.validate_ranks([row(0), row(1, rccl_device=0), row(2), row(3)], 4)
+    assert "some ranks only" in bench.validate_ranks([row(0), row(1, peer_ok=False), row(2), row(3)], 4)
+    assert "expected 4" in bench.validate_ranks(good[:3], 4)

@@ -133,3 +133,13 @@ def test_ddp_graph_replay_rccl_routes(model, route):
     r = res[0]
     assert r["route"] == route
     assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])
+
+
+def test_ddp_peer_buffer_broadcast_exact_and_chunked():
+    """Advisor r4: the peer-route buffer broadcast chunks an image larger than the peer capacity and
+    carries int64 / fp64 / bool buffers as raw bytes (exact), bf16 widened to fp32 (exact)."""
+    rc, res, logs = run_ranks("ddp_peer_buffers", 2)
+    assert rc == 0, "\n".join(logs)
+    assert res[0]["sig"] == res[1]["sig"], "buffers differ across ranks"
+    assert res[0]["count"] == res[1]["count"] == (1 << 40) + 12_345
+    assert res[0]["peer_error"] == 0 and res[1]["peer_error"] == 0

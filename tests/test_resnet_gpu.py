@@ -194,6 +194,23 @@ def test_resnet_head_matches_torch(O):
     assert rel_err(b.grad, br.grad) < 3e-2
 
 
+@pytest.mark.parametrize("O", [10, 1000])
+def test_resnet_head_no_bias(O):
+    """Advisor r4: the head without a bias (padded and unpadded class counts) runs and matches fp32."""
+    from pytorch_distributed_example_amd.ops.resnet import resnet_head
+    torch.manual_seed(10)
+    x = torch.randn(16, 512, 7, 7).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (0.05 * torch.randn(O, 512)).to(dev, torch.bfloat16).requires_grad_()
+    y = resnet_head(x, w, None)
+    dy = torch.randn(16, O).to(dev, torch.bfloat16)
+    y.backward(dy)
+    xr, wr = x.float(), w.detach().float().requires_grad_()
+    yr = F.linear(F.adaptive_avg_pool2d(xr, 1).flatten(1), wr)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 3e-2
+
+
 @pytest.mark.parametrize("stride,cin,cout", [(1, 64, 64), (2, 64, 128), (1, 64, 128)])
 def test_basic_block_matches_cpu(stride, cin, cout):
     """One BasicBlock (with downsample when strided or widening) at a well-conditioned batch, through
