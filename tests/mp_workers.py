@@ -573,6 +573,51 @@ def case_peer_engine(steps="6", mode="eager", overlap="1", autotune="0"):
     dist.destroy_process_group()
 
 
+def case_engine_w2_equiv(steps="8"):
+    """Verdict r4 item 6: the fused engine at W ranks (B=64 each, sharing one GPU, peer all-reduce)
+    trains exactly like ONE rank at B=64*W on the concatenated shards: same per-step global loss and
+    the same parameters, up to fp32 reassociation; every W-rank replica bit-identical."""
+    from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
+    from pytorch_distributed_example_amd.engine import LeNetTrainStep
+    from pytorch_distributed_example_amd.models import build_net
+
+    n_steps, b = int(steps), 64
+    dev = _shared_gpu_init()
+    ds = synthetic_mnist(2048, seed=0, device=dev)
+    shards = [DistributedSampler(ds, num_replicas=W, rank=r, shuffle=True, seed=0).indices_tensor()
+              for r in range(W)]
+
+    def train(eng, idx, per_step_b):
+        eng.bind_dataset(ds.images, ds.labels)
+        eng.set_epoch_indices(idx)
+        out = []
+        for _ in range(n_steps):
+            eng.step()
+            loss, _, _ = eng.read_meters()
+            out.append(loss)
+        return out
+
+    net = build_net(seed=3, device=dev)
+    comm = dist.engine_comm(allow_host_only=True)
+    eng = LeNetTrainStep(net, batch_size=b, comm=comm, force_comm=True)
+    mine = train(eng, shards[R], b)
+    torch.cuda.synchronize()
+    assert comm.health() == "", comm.health()
+    tot = torch.tensor(mine, dtype=torch.float64)
+    dist.all_reduce(tot)                                   # global loss sum per step
+    w_bits = [int(p.detach().contiguous().view(torch.int32).to(torch.int64).sum().item()) for p in net.parameters()]
+    w_params = [p.detach().double().sum().item() for p in net.parameters()]
+    res = {"rank": R, "bits": w_bits, "w_loss": (tot / (b * W)).tolist(), "w_params": w_params}
+    if R == 0:
+        cat = torch.cat([torch.cat([shards[r][k * b:(k + 1) * b] for r in range(W)]) for k in range(n_steps)])
+        ref_net = build_net(seed=3, device=dev)
+        ref = LeNetTrainStep(ref_net, batch_size=b * W)
+        res["one_loss"] = [x / (b * W) for x in train(ref, cat, b * W)]
+        res["one_params"] = [p.detach().double().sum().item() for p in ref_net.parameters()]
+    emit(res)
+    dist.destroy_process_group()
+
+
 def case_ddp_model(model="gpt2", steps="3"):
     """DDP of the GPT-2 / ResNet-18 configs (tiny shapes) with W ranks sharing cuda:0 over gloo:
     replicas start from different seeds and must be bit-identical after training steps (broadcast at
