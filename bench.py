@@ -122,7 +122,8 @@ def _comm_info(dist, comm, eng):
     """What the communication path actually ran on (proof that RCCL saw N ranks)."""
     if comm is None:
         return {}
-    info = {"rccl_world": None, "rccl_device": None, "peer_ok": comm.peer is not None}
+    info = {"rccl_world": None, "rccl_device": None, "peer_ok": comm.peer is not None,
+            "peer_inplace": bool(getattr(comm, "peer_inplace", False))}
     rc = comm.group.rccl
     if rc is not None:
         try:

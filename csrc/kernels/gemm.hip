@@ -1415,6 +1415,543 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
   }
 }
 
+// ============================================================================ persistent 8-phase (cfg 19)
+// k_gemm8p's main loop in a persistent block (one per CU) that walks the tiles slot, slot + P, ...
+// (slot = XCD-contiguous remap of blockIdx, so at any time the P blocks work on P consecutive tiles of
+// the grouped order, as the one-shot grid's rounds do).  Per tile, after the K loop:
+//   acc -> LDS tile (bias / scale, bf16) -> barrier -> this thread's 16 chunks of 16 B into registers
+//   (GELU backward: its gelu' chunks loaded now) -> barrier -> the NEXT tile's six prologue slots of
+//   LDS-DMA -> this tile's GELU math + NSTORE buffer stores (masked lanes store to an out-of-range
+//   offset: a compile-time store count per wave) -> the next tile's K loop.
+// vmcnt counts in issue order, so the stores sit between the prologue slots and the loop's first
+// issues: the four phases of the first K-tile wait with NSTORE more in flight (the stores drain under
+// them), from the fifth on the count is k_gemm8p's.  What this buys over the one-shot grid on the
+// short-K GPT-2 fprops (K = 768: 12 K-tiles per tile): the block launch, the first K-tile's load
+// latency and the epilogue's store drain of every tile overlap the neighbouring tiles' MFMAs.
+// TA = 0 (K-contiguous A), no split-K, no bias gradient; K % 64 == 0 when TB = 0.
+template <bool TB, int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
+  constexpr bool TA = false;
+  constexpr int WM = 2, WN = 4, TM = 8, TN = 4, NT = 512;
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256
+  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 KB per K-tile
+  constexpr int RS = BN * 2 + 16;
+  constexpr int TILE_BYTES = BM * RS;
+  constexpr int SMEM = TILE_BYTES > 2 * STAGE ? TILE_BYTES : 2 * STAGE;
+  constexpr int VMW = TB ? 6 : 8;
+  constexpr int CPR = BN / 8, CH = BM * CPR / NT;                              // 16 chunks per thread
+  constexpr int NSTORE = CH * (EPI == kGelu ? 2 : 1);
+  static_assert(EPI == kBf16 || EPI == kGelu || EPI == kGeluBwd, "bf16 epilogues only");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ntile = a.mtiles * a.ntiles;
+  const int P = gridDim.x;
+  int id = xcd_remap(blockIdx.x, P);
+  if (id >= ntile) return;
+  const int KT = (a.K + 63) >> 6;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  const rsrc_t cr = make_rsrc(a.C, a.c_bytes);
+  const rsrc_t c2r = make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
+  const rsrc_t xr = make_rsrc(EPI == kGeluBwd ? (const void*)a.aux : a.C, EPI == kGeluBwd ? a.c_bytes : 0);
+  const uint32_t astep = 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const int lrow = glds_row(l);
+
+  auto coords = [&](int tid, int& m0, int& n0) {
+    constexpr int G = 8;
+    const int grp = tid / (G * a.ntiles), r2 = tid - grp * (G * a.ntiles);
+    const int gsz = min(G, a.mtiles - grp * G);
+    m0 = (grp * G + r2 % gsz) * BM;
+    n0 = (r2 / gsz) * BN;
+  };
+  // region r's two wave-instructions (u = 0, 1): LDS destination (tile-independent) and global offset
+  int gldso[4][2];
+  uint32_t goff[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool isA = r < 2;
+      const bool tr = isA ? TA : TB;
+      int g;
+      if (tr) g = (isA ? 2 * u + r : 2 * (r - 2) + u) * 8 + w;
+      else if (isA) g = u * 16 + 8 * r + w;
+      else {
+        const int x = 8 * u + w;
+        g = (x >> 2) * 8 + (x & 3) + 4 * (r - 2);
+      }
+      gldso[r][u] = (isA ? 0 : ABYTES) + g * 1024;
+    }
+  auto setup = [&](int m0, int n0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool isA = r < 2;
+        const bool tr = isA ? TA : TB;
+        const int g = (gldso[r][u] - (isA ? 0 : ABYTES)) >> 10;
+        const int ch = glds_chunk(l, g & 1);
+        const int lim = isA ? a.M : a.N, ld = isA ? a.lda : a.ldb, o0 = isA ? m0 : n0;
+        if (tr) {
+          const int k = 8 * (g & 7) + lrow, c = o0 + 64 * (g >> 3) + 8 * ch;
+          goff[r][u] = c < lim ? (uint32_t)(((size_t)k * ld + c) * 2) : kOOB;
+        } else {
+          const int row = o0 + 8 * g + lrow;
+          goff[r][u] = row < lim ? (uint32_t)(((size_t)row * ld + 8 * ch) * 2) : kOOB;
+        }
+      }
+  };
+  auto issue = [&](int r, int kt) {
+    if (kt >= KT) return;
+    const char* base = smem + (kt & 1) * STAGE;
+    const uint32_t ko = (uint32_t)kt * (r < 2 ? astep : bstep);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) glds16(r < 2 ? ar : br, base + gldso[r][u], goff[r][u] + ko);
+  };
+  auto prologue = [&]() {   // the six slots before phase 0: K-tile 0's four regions, K-tile 1's A0 and B0
+    issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0); issue(0, 1); issue(2, 1);
+  };
+
+  // ---- fragment lane bases (tile-independent) ----
+  const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+  const uint32_t abase = lds0 + (uint32_t)toff(wm * WTM + prow, l >> 4);
+  const uint32_t bbase = lds0 + (uint32_t)toff(wn * WTN + prow, l >> 4) + ABYTES;
+  uint2 tbb[TB ? 2 : 1];
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tbb[j] = add2(tr16_lane_off(wn * WTN + 16 * j), lds0 + ABYTES);
+  }
+  const int mrow = prow;
+  const int pcol = TB ? 4 * (l >> 4) : (int)((0x4c80u >> (4 * (l >> 4))) & 0xfu);   // {0, 8, 12, 4}[l >> 4]
+  const bool has_bias = (EPI == kBf16 || EPI == kGelu) && a.bias != nullptr;
+  const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+
+  int m0, n0;
+  coords(id, m0, n0);
+  setup(m0, n0);
+  if (KT > 0) prologue();
+  bool pend = false;                                  // the previous tile's NSTORE stores are in flight
+  for (;;) {
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[4][2], fb[TN][2];
+    if (KT > 0) {
+      if (KT > 1) {
+        if (pend) wait_vm<VMW + NSTORE>();
+        else wait_vm<VMW>();
+      } else {
+        wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+
+      auto phase = [&](auto BUF_, auto PH_, int kt, bool p0) {
+        constexpr int BUF = decltype(BUF_)::value, PH = decltype(PH_)::value;
+        constexpr uint32_t BO = BUF * STAGE;
+        auto rdA = [&](auto I_, int s2) -> bf16x8 {
+          constexpr int i = decltype(I_)::value;
+          return s2 ? rd128<2048 * i + 512>(abase + BO) : rd128<2048 * i>(abase + BO);
+        };
+        auto rdB = [&](auto J_, int s2) -> bf16x8 {
+          constexpr int j = decltype(J_)::value;
+          constexpr int TO = (j >> 1) * 512;
+          if constexpr (TB) return s2 ? trpair<4096 + TO>(add2(tbb[j & 1], BO)) : trpair<TO>(add2(tbb[j & 1], BO));
+          else return s2 ? rd128<2048 * j + 512>(bbase + BO) : rd128<2048 * j>(bbase + BO);
+        };
+        if constexpr (PH == 1 || PH == 3) {
+          static_for<0, 4>([&](auto I_) {
+            constexpr int i = decltype(I_)::value + (PH == 3 ? 4 : 0);
+            fa[i & 3][0] = rdA(std::integral_constant<int, i>{}, 0);
+            fa[i & 3][1] = rdA(std::integral_constant<int, i>{}, 1);
+          });
+        }
+        if constexpr (PH == 1 || PH == 2) {
+          static_for<0, 2>([&](auto J_) {
+            constexpr int j = decltype(J_)::value + (PH == 2 ? 2 : 0);
+            fb[j][0] = rdB(std::integral_constant<int, j>{}, 0);
+            fb[j][1] = rdB(std::integral_constant<int, j>{}, 1);
+          });
+        }
+        if constexpr (PH == 1) issue(3, kt + 1);
+        else if constexpr (PH == 2) issue(1, kt + 1);
+        else if constexpr (PH == 3) issue(0, kt + 2);
+        else issue(2, kt + 2);
+        if (kt + 2 < KT) {
+          if (p0) wait_vm<VMW + NSTORE>();      // the previous tile's stores are still older than this slot
+          else wait_vm<VMW>();
+        } else {
+          wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        lgkm_fence();
+        __builtin_amdgcn_s_setprio(1);
+        constexpr int I0 = (PH <= 2) ? 0 : 4, J0 = (PH == 1 || PH == 4) ? 0 : 2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              acc[I0 + i][J0 + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[J0 + j][s2], fa[i][s2], acc[I0 + i][J0 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+      };
+      if (wm == 1) __builtin_amdgcn_s_barrier();
+      for (int kt = 0; kt < KT; kt += 2) {
+        const bool p0 = pend && kt == 0;
+        phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, kt, p0);
+        phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{}, kt, p0);
+        phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{}, kt, p0);
+        phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{}, kt, p0);
+        if (kt + 1 < KT) {
+          phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, kt + 1, false);
+          phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, kt + 1, false);
+          phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{}, kt + 1, false);
+          phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{}, kt + 1, false);
+        }
+      }
+      if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the two rows
+    }
+    wait_vm<0>();                                  // (nothing in flight by now; keeps hipcc's counts simple)
+    __syncthreads();
+    // ---- accumulators -> bf16 LDS tile (bias and scale before the single rounding) ----
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nl = wn * WTN + 16 * j + pcol;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (has_bias && n0 + nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + n0 + nl), bv);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = wm * WTM + 16 * i + mrow;
+        const float v[4] = {(acc[i][j][0] + bv[0]) * sc, (acc[i][j][1] + bv[1]) * sc, (acc[i][j][2] + bv[2]) * sc,
+                            (acc[i][j][3] + bv[3]) * sc};
+        *reinterpret_cast<uint2*>(smem + ml * RS + nl * 2) = pack4(v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int tv = t;
+    asm volatile("" : "+v"(tv));
+    auto chunk_off = [&](int c, int tm0, int tn0) -> uint32_t {
+      const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
+      const int m = tm0 + row, n = tn0 + 8 * cc;
+      return (m < a.M && n < a.N) ? (uint32_t)(((size_t)m * a.ldc + n) * 2) : kOOB;
+    };
+    uint4 cv[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int q = tv + c * NT, row = q / CPR, cc = q - row * CPR;
+      cv[c] = *reinterpret_cast<const uint4*>(smem + row * RS + cc * 16);
+    }
+    uint4 gv[EPI == kGeluBwd ? CH : 1];
+    if constexpr (EPI == kGeluBwd) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) gv[c] = bload16(xr, chunk_off(c, m0, n0));   // before the next tile's DMA
+    }
+    const int tm0 = m0, tn0 = n0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                  // the LDS tile is free: the next tile's slots may land
+    const int nid = id + P;
+    if (nid < ntile) {
+      coords(nid, m0, n0);
+      setup(m0, n0);
+      if (KT > 0) prologue();
+    }
+    // ---- this tile's epilogue math and stores (NSTORE buffer stores per thread, exactly) ----
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
+      const uint32_t co = chunk_off(c, tm0, tn0);
+      if constexpr (EPI == kBf16) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
+      } else if constexpr (EPI == kGelu) {
+        uint32_t ya[4], da[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pde_f2 d;
+          const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+          ya[e] = pack_bf2(y.x, y.y);
+          da[e] = pack_bf2(d.x, d.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
+      } else {
+        const uint32_t gw[4] = {gv[c].x, gv[c].y, gv[c].z, gv[c].w};
+        uint32_t r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+          r[e] = pack_bf2(pr.x, pr.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);             // keep the next tile's accumulator zeroing below the stores
+    if (nid >= ntile) break;
+    id = nid;
+    pend = true;
+  }
+}
+
+// ============================================================================ continuous 8-phase (cfg 20)
+// k_gemm8p's main loop as ONE K-tile stream per persistent block: the tiles of the block (slot, slot + P,
+// ... with slot the XCD-contiguous remap of blockIdx) are concatenated along K, so the LDS-DMA of the next
+// tile's first two K-tiles is issued in the current tile's last phases exactly as any other look-ahead
+// slot -- no pipeline drain or refill and no barrier at a tile boundary.  The epilogue never touches LDS
+// (the stage buffers stay in use): each lane holds four consecutive columns of every 16x16 accumulator,
+// so two horizontally adjacent blocks are merged across the lane pair that holds the other half of each
+// 8-column group (one 64-lane shuffle per 8 bytes) and every lane stores one 16-byte chunk per block pair
+// (bias, scale and GELU applied in registers).  vmcnt counts in issue order: those NS stores sit behind
+// the four look-ahead slots in flight, so the first K-tile of the next tile waits with NS more
+// outstanding and the stores drain under its MFMAs.
+// TA = 0, no split-K / bias gradient, epilogues bf16 and bias + GELU; K % 128 == 0 (an even K-tile count
+// keeps every tile starting on LDS buffer 0).
+template <bool TB, int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
+  constexpr bool TA = false;
+  constexpr int WM = 2, WN = 4, TM = 8, TN = 4;
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256
+  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 KB per K-tile
+  constexpr int VMW = TB ? 6 : 8;
+  constexpr int NS = TM * (TN / 2) * (EPI == kGelu ? 2 : 1);                   // 16-byte stores per lane per tile
+  static_assert(EPI == kBf16 || EPI == kGelu, "bf16 / bias + GELU epilogues");
+  static_assert(VMW + NS <= 63, "vmcnt is a 6-bit count");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ntile = a.mtiles * a.ntiles;
+  const int P = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, P);
+  if (slot >= ntile) return;
+  const int nmy = (ntile - slot + P - 1) / P;
+  const int KT = a.K >> 6;                       // even, >= 2 (host)
+  const int total = nmy * KT;
+  const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
+  const rsrc_t cr = make_rsrc(a.C, a.c_bytes);
+  const rsrc_t c2r = make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
+  const uint32_t astep = 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
+  const int lrow = glds_row(l);
+
+  auto coords = [&](int j, int& m0, int& n0) {
+    constexpr int G = 8;
+    const int tid = slot + j * P;
+    const int grp = tid / (G * a.ntiles), r2 = tid - grp * (G * a.ntiles);
+    const int gsz = min(G, a.mtiles - grp * G);
+    m0 = (grp * G + r2 % gsz) * BM;
+    n0 = (r2 / gsz) * BN;
+  };
+  int gldso[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool isA = r < 2;
+      const bool tr = isA ? TA : TB;
+      int g;
+      if (tr) g = (isA ? 2 * u + r : 2 * (r - 2) + u) * 8 + w;
+      else if (isA) g = u * 16 + 8 * r + w;
+      else {
+        const int x = 8 * u + w;
+        g = (x >> 2) * 8 + (x & 3) + 4 * (r - 2);
+      }
+      gldso[r][u] = (isA ? 0 : ABYTES) + g * 1024;
+    }
+  // per-lane part of every region's global offset (tile-independent) and the lane's row / column inside
+  // the tile for the bounds mask; a tile adds its wave-uniform base (m0 * lda or n0, in bytes)
+  uint32_t lo_[4][2];
+  int lim_[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool isA = r < 2;
+      const bool tr = isA ? TA : TB;
+      const int g = (gldso[r][u] - (isA ? 0 : ABYTES)) >> 10;
+      const int ch = glds_chunk(l, g & 1);
+      const int ld = isA ? a.lda : a.ldb;
+      if (tr) {
+        const int k = 8 * (g & 7) + lrow, c = 64 * (g >> 3) + 8 * ch;
+        lo_[r][u] = (uint32_t)(((size_t)k * ld + c) * 2);
+        lim_[r][u] = c;
+      } else {
+        const int row = 8 * g + lrow;
+        lo_[r][u] = (uint32_t)(((size_t)row * ld + 8 * ch) * 2);
+        lim_[r][u] = row;
+      }
+    }
+  // region r of K-tile ktt of this block's tile jt (into buffer ktt & 1)
+  auto issue = [&](int r, int jt, int ktt) {
+    if (jt >= nmy) return;
+    int m0, n0;
+    coords(jt, m0, n0);
+    const bool isA = r < 2;
+    const bool tr = isA ? TA : TB;
+    const int o0 = isA ? m0 : n0, lim = isA ? a.M : a.N;
+    const uint32_t tb = tr ? (uint32_t)o0 * 2u : (uint32_t)o0 * (uint32_t)(isA ? a.lda : a.ldb) * 2u;
+    const char* base = smem + (ktt & 1) * STAGE;
+    const uint32_t ko = (uint32_t)ktt * (isA ? astep : bstep);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      glds16(isA ? ar : br, base + gldso[r][u], o0 + lim_[r][u] < lim ? lo_[r][u] + tb + ko : kOOB);
+  };
+
+  const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+  const uint32_t abase = lds0 + (uint32_t)toff(wm * WTM + prow, l >> 4);
+  const uint32_t bbase = lds0 + (uint32_t)toff(wn * WTN + prow, l >> 4) + ABYTES;
+  uint2 tbb[TB ? 2 : 1];
+  if constexpr (TB) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tbb[j] = add2(tr16_lane_off(wn * WTN + 16 * j), lds0 + ABYTES);
+  }
+  const int mrow = prow;
+  const int pcol = TB ? 4 * (l >> 4) : (int)((0x4c80u >> (4 * (l >> 4))) & 0xfu);   // {0, 8, 12, 4}[l >> 4]
+  const bool lower = (pcol & 4) == 0;            // this lane holds the low half of its 8-column group
+  constexpr int XM = TB ? 16 : 48;               // lane mask of the partner holding the other half
+  const bool has_bias = a.bias != nullptr;
+  const float sc = (EPI == kBf16 && a.scale != nullptr) ? *a.scale : 1.f;
+
+  issue(0, 0, 0); issue(2, 0, 0); issue(3, 0, 0); issue(1, 0, 0); issue(0, 0, 1); issue(2, 0, 1);
+  wait_vm<VMW>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();     // the two wave rows run one barrier apart (k_gemm8p)
+
+  bf16x8 fa[4][2], fb[TN][2];
+  bool pend = false;
+  for (int j = 0; j < nmy; ++j) {
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int gj = j * KT;
+    auto phase = [&](auto BUF_, auto PH_, int c, bool p0) {
+      constexpr int BUF = decltype(BUF_)::value, PH = decltype(PH_)::value;
+      constexpr uint32_t BO = BUF * STAGE;
+      auto rdA = [&](auto I_, int s2) -> bf16x8 {
+        constexpr int i = decltype(I_)::value;
+        return s2 ? rd128<2048 * i + 512>(abase + BO) : rd128<2048 * i>(abase + BO);
+      };
+      auto rdB = [&](auto J_, int s2) -> bf16x8 {
+        constexpr int jj = decltype(J_)::value;
+        constexpr int TO = (jj >> 1) * 512;
+        if constexpr (TB) return s2 ? trpair<4096 + TO>(add2(tbb[jj & 1], BO)) : trpair<TO>(add2(tbb[jj & 1], BO));
+        else return s2 ? rd128<2048 * jj + 512>(bbase + BO) : rd128<2048 * jj>(bbase + BO);
+      };
+      if constexpr (PH == 1 || PH == 3) {
+        static_for<0, 4>([&](auto I_) {
+          constexpr int i = decltype(I_)::value + (PH == 3 ? 4 : 0);
+          fa[i & 3][0] = rdA(std::integral_constant<int, i>{}, 0);
+          fa[i & 3][1] = rdA(std::integral_constant<int, i>{}, 1);
+        });
+      }
+      if constexpr (PH == 1 || PH == 2) {
+        static_for<0, 2>([&](auto J_) {
+          constexpr int jj = decltype(J_)::value + (PH == 2 ? 2 : 0);
+          fb[jj][0] = rdB(std::integral_constant<int, jj>{}, 0);
+          fb[jj][1] = rdB(std::integral_constant<int, jj>{}, 1);
+        });
+      }
+      // the look-ahead slot of this phase: K-tile c + 1 (phases 1, 2) or c + 2 (3, 4) of the stream
+      const int cn = c + (PH <= 2 ? 1 : 2);
+      const int jt = cn < KT ? j : j + 1, kn = cn < KT ? cn : cn - KT;
+      if constexpr (PH == 1) issue(3, jt, kn);
+      else if constexpr (PH == 2) issue(1, jt, kn);
+      else if constexpr (PH == 3) issue(0, jt, kn);
+      else issue(2, jt, kn);
+      if (gj + c + 2 < total) {
+        if (p0) wait_vm<VMW + NS>();            // the previous tile's stores are older than this slot
+        else wait_vm<VMW>();
+      } else {
+        wait_vm<0>();                           // end of the stream: fewer slots in flight, drain
+      }
+      __builtin_amdgcn_s_barrier();
+      lgkm_fence();
+      __builtin_amdgcn_s_setprio(1);
+      constexpr int I0 = (PH <= 2) ? 0 : 4, J0 = (PH == 1 || PH == 4) ? 0 : 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            acc[I0 + i][J0 + jj] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[J0 + jj][s2], fa[i][s2], acc[I0 + i][J0 + jj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    };
+    for (int kt = 0; kt < KT; kt += 2) {
+      const bool p0 = pend && kt == 0;
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, kt, p0);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{}, kt, p0);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{}, kt, p0);
+      phase(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{}, kt, p0);
+      phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, kt + 1, false);
+      phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, kt + 1, false);
+      phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{}, kt + 1, false);
+      phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{}, kt + 1, false);
+    }
+    // ---- register epilogue: merge block pairs across the lane pair, one 16-byte store per pair ----
+    int m0, n0;
+    coords(j, m0, n0);
+    const int row0 = m0 + wm * WTM + mrow, col0 = n0 + wn * WTN + (pcol & 8);
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp) {
+      float bv0[4] = {0.f, 0.f, 0.f, 0.f}, bv1[4] = {0.f, 0.f, 0.f, 0.f};
+      const int nb = n0 + wn * WTN + 32 * jp + pcol;
+      if (has_bias && nb < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + nb), bv0);
+      if (has_bias && nb + 16 < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + nb + 16), bv1);
+      const int col = col0 + 16 * (2 * jp + (lower ? 0 : 1));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = row0 + 16 * i;
+        float v0[4], v1[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = (acc[i][2 * jp][e] + bv0[e]) * sc;
+          v1[e] = (acc[i][2 * jp + 1][e] + bv1[e]) * sc;
+        }
+        const uint32_t off = (row < a.M && col < a.N) ? (uint32_t)(((size_t)row * a.ldc + col) * 2) : kOOB;
+        auto emit = [&](const uint2 u0, const uint2 u1, rsrc_t rs) {
+          // lower lane: block 2jp (own low half + partner's high half); upper: block 2jp+1
+          const uint2 send = lower ? u1 : u0;
+          const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, XM, 64), (uint32_t)__shfl_xor((int)send.y, XM, 64));
+          const v4u out = lower ? v4u{u0.x, u0.y, recv.x, recv.y} : v4u{recv.x, recv.y, u1.x, u1.y};
+          __builtin_amdgcn_raw_buffer_store_b128(out, rs, off, 0, 0);
+        };
+        if constexpr (EPI == kBf16) {
+          emit(pack4(v0), pack4(v1), cr);
+        } else {
+          uint32_t y0[2], d0[2], y1[2], d1[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            pde_f2 d;
+            pde_f2 y = gelu2_d(pde_f2{v0[2 * e], v0[2 * e + 1]}, d);
+            y0[e] = pack_bf2(y.x, y.y);
+            d0[e] = pack_bf2(d.x, d.y);
+            y = gelu2_d(pde_f2{v1[2 * e], v1[2 * e + 1]}, d);
+            y1[e] = pack_bf2(y.x, y.y);
+            d1[e] = pack_bf2(d.x, d.y);
+          }
+          emit(make_uint2(y0[0], y0[1]), make_uint2(y1[0], y1[1]), cr);
+          emit(make_uint2(d0[0], d0[1]), make_uint2(d1[0], d1[1]), c2r);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);           // keep the next tile's accumulator zeroing below the stores
+    pend = true;
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();     // re-align the two rows before the block retires
+}
+
 // dW (bf16 [M][N] contiguous) = sum of the fp32 slabs [S][M][N]; blocks past the dW range fold the
 // bias-gradient partials [S][M] into db (bf16) the same way
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int S, int64_t mn,
@@ -1477,7 +2014,13 @@ template <> struct Cfg<17> { static constexpr int V = 4, TM = 4, TN = 8, WM = 4,
 //   18: the 8-phase loop (k_gemm8p) at 256x256, every operand layout and epilogue; a K-contiguous operand
 //       needs K % 64 == 0 (a call with a K tail runs 17)
 template <> struct Cfg<18> { static constexpr int V = 5, TM = 8, TN = 4, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 19;
+//   19: the 8-phase loop in a persistent block per CU (k_gemm8pp), fprop / dgrad (TA = 0), bf16 epilogues;
+//       other calls with this id (wgrad, split-K, K tail with TB = 0, > 2 GB of C) run 18
+template <> struct Cfg<19> { static constexpr int V = 6, TM = 8, TN = 4, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
+//   20: the 8-phase loop as one continuous K-tile stream per persistent block (k_gemm8pc), register
+//       epilogue; fprop (bias) and plain dgrad with K % 128 == 0; other calls run 19
+template <> struct Cfg<20> { static constexpr int V = 7, TM = 8, TN = 4, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 21;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -1499,7 +2042,26 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 5) {
+  if constexpr (C::V == 7) {
+    // (the bias + GELU form still spills a few registers inside the K loop: runs 19)
+    constexpr bool ok = !TA && !CS && EPI == kBf16;
+    if constexpr (ok) {
+      if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
+        hipLaunchKernelGGL((k_gemm8pc<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 6) {
+    constexpr bool ok = !TA && !CS && EPI != kSlab;
+    if constexpr (ok) {
+      if (splits == 1 && a.c_bytes < kOOB && (TB || a.K % 64 == 0)) {
+        hipLaunchKernelGGL((k_gemm8pp<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 5) {
     if ((TA && TB) || a.K % 64 == 0) {
       hipLaunchKernelGGL((k_gemm8p<TA, TB, EPI, CS>), dim3(grid), dim3(512), 0, st, a);
       return hipGetLastError();
@@ -1549,7 +2111,9 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 15: return launch_cfg<15, TA, TB, EPI, CS>(a, splits, st);
     case 16: return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
     case 17: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
+    case 18: return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
+    case 19: return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<20, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -1563,7 +2127,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                                     {256, 256}, {256, 192}, {256, 256}, {256, 256}};
+                                     {256, 256}, {256, 192}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];

@@ -23,6 +23,7 @@
 #include "pde_adam.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace {
@@ -177,7 +178,7 @@ __device__ __forceinline__ void wait_epoch(const long long* epoch, long long t, 
   __syncthreads();
 }
 
-template <bool PROF>
+template <bool PROF, bool NTP>
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, long long n4,
                                               float lr, float b1, float b2, float eps, float wd, int decoupled,
@@ -237,8 +238,15 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
     const FoldLane fl = fold_lane(fd, g, fb);
     if (fl.e >= 0) {
       adam_elem(pa, ma, va, fl.g * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
-      p[fl.e] = pa; m[fl.e] = ma; v[fl.e] = va;
-      g[fl.e] = fl.g;                                  // p.grad holds the true (folded) gradient
+      if constexpr (NTP) {     // NTP: nothing of this launch is left dirty in the XCD L2s (see below)
+        __builtin_nontemporal_store(pa, p + fl.e);
+        __builtin_nontemporal_store(ma, m + fl.e);
+        __builtin_nontemporal_store(va, v + fl.e);
+        __builtin_nontemporal_store(fl.g, g + fl.e);   // p.grad holds the true (folded) gradient
+      } else {
+        p[fl.e] = pa; m[fl.e] = ma; v[fl.e] = va;
+        g[fl.e] = fl.g;                                // p.grad holds the true (folded) gradient
+      }
       pack_store(pk, fl.e, pa);
     }
     continue;
@@ -252,10 +260,13 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
       adam_elem(pa[j], ma[j], va[j], ga[j] * grad_scale, lr, wd, decoupled, omb1, omb2, b2, step_size, bc2s, eps);
       pack_store(pk, 4 * i + j, pa[j]);
     }
-    p4[i] = pp;
     // the moments are read again only by the next step's Adam: streamed out (non-temporal) rather than
-    // left dirty in the XCD L2s for the end-of-kernel write-back that the next kernel waits behind
+    // left dirty in the XCD L2s for the end-of-kernel write-back that the next kernel waits behind.
+    // NTP: the parameters too -- their next readers (the next step's forward kernels) run on other
+    // XCDs' L2s anyway, so a dirty line here only lengthens this kernel's end-of-kernel write-back
     typedef float nt_f4 __attribute__((ext_vector_type(4)));
+    if constexpr (NTP) __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&pp), reinterpret_cast<nt_f4*>(p4 + i));
+    else p4[i] = pp;
     __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&mm), reinterpret_cast<nt_f4*>(m4 + i));
     __builtin_nontemporal_store(*reinterpret_cast<nt_f4*>(&vv), reinterpret_cast<nt_f4*>(v4 + i));
   }
@@ -379,14 +390,22 @@ hipError_t pde_adam_flat(float* p, float* g, float* m, float* v, long long n, fl
       return hipErrorInvalidValue;
   const int nfb = fold_blocks(fdh.f[0]) + fold_blocks(fdh.f[1]);
   unsigned long long* prof = pde_lenet_prof_slot(5);
-  if (prof)
-    hipLaunchKernelGGL(k_adam<true>, dim3(grid_for(n4c) + ar.nvb + nfb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
-                       wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
-                       Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, prof);
-  else
-    hipLaunchKernelGGL(k_adam<false>, dim3(grid_for(n4c) + ar.nvb + nfb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, b2, eps,
-                       wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},
-                       Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride}, Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}}, ar, nullptr);
+  static const bool ntp = [] {
+    const char* e = getenv("PDE_ADAM_NT_P");
+    return e != nullptr && e[0] == '1';   // default off: neutral in a same-box A/B (profiles/r5_lenet/)
+  }();
+#define PDE_ADAM_LAUNCH(P, N)                                                                                   \
+  hipLaunchKernelGGL((k_adam<P, N>), dim3(grid_for(n4c) + ar.nvb + nfb), dim3(256), 0, st, p, g, m, v, n4, lr, b1, \
+                     b2, eps, wd, decoupled, grad_scale, step, arrive, bump, Pack{pack_off, pack_dst, pack_mode},    \
+                     Fold{{Fold1{fold_off, fold_len, fold_nrep, fold_stride},                                      \
+                           Fold1{fold2_off, fold2_len, fold2_nrep, fold2_stride}}},                                \
+                     ar, P ? prof : nullptr)
+  if (prof) {
+    if (ntp) PDE_ADAM_LAUNCH(true, true); else PDE_ADAM_LAUNCH(true, false);
+  } else {
+    if (ntp) PDE_ADAM_LAUNCH(false, true); else PDE_ADAM_LAUNCH(false, false);
+  }
+#undef PDE_ADAM_LAUNCH
   return hipGetLastError();
 }
 

@@ -224,6 +224,23 @@ PYBIND11_MODULE(_runtime, m) {
       .def("device_args", [](PeerAllReduce& p) { return py::bytes(p.device_args()); })
       .def("device_probe_f32", &PeerAllReduce::device_probe_f32, py::arg("inp"), py::arg("out"), py::arg("count"),
            py::arg("scale"), py::arg("two"), py::arg("stream"))
+      .def("register_buffer",
+           [](PeerAllReduce& p, uintptr_t ptr, int64_t bytes) {
+             int id = -1;
+             std::string h = p.register_buffer(ptr, bytes, &id);
+             return py::make_tuple(id, py::bytes(h));
+           })
+      .def("open_registered",
+           [](PeerAllReduce& p, int id, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             py::gil_scoped_release nogil;
+             p.open_registered(id, v);
+           })
+      .def("all_reduce_registered_f32", &PeerAllReduce::all_reduce_registered_f32, py::arg("id"), py::arg("off"),
+           py::arg("count"), py::arg("scale"), py::arg("algo"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("registered_bytes", &PeerAllReduce::registered_bytes)
       .def("debug_skip_stage", &PeerAllReduce::debug_skip_stage)
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
       .def("error_async", &PeerAllReduce::error_async)

@@ -23,6 +23,22 @@
 // Spins are bounded by a wall-clock timeout (s_memrealtime): a dead peer latches an error word
 // instead of hanging the GPU.
 //
+// In-place form over REGISTERED buffers (the engines' persistent flat gradient buffers): every rank
+// IPC-maps its peers' buffer once (register_buffer / open_registered), and a call reads the peers'
+// gradients where the backward left them -- no stage copy, no fence:
+//
+//   one-shot:  barrier A | v = sum_p buf_p[i] (system-coherent loads) | barrier B | buf_self[i] = v
+//   two-shot:  barrier A | buf_self[my chunk] = sum_p buf_p[my chunk] (write-through stores) | barrier B
+//              | buf_self[chunk q] = buf_q[chunk q] for every q | barrier C
+//
+// Barrier A needs no release: the gradients were written by earlier kernels, whose end-of-kernel
+// release already made them visible in memory; the peers' reads are system-scope loads (no stale L1 /
+// L2 line), and the only bytes published inside the call (the two-shot partial sums) are written
+// through with system-scope stores and drained (vmcnt(0)) before the flag store.  B keeps every rank
+// from overwriting its buffer while a peer may still read it; C (two-shot) the same for the gathered
+// chunks.  One-shot sums are held in registers across B: at most 256 blocks x 512 lanes x 16 B = 2 MB
+// per call.
+//
 // Calls on one PeerAllReduce must be ordered on a single stream (the engine's comm stream) and be
 // issued by every rank in the same order with the same sizes (collective semantics); launches are
 // hipGraph-capturable (the call number lives in device memory).
@@ -71,6 +87,15 @@ class PeerAllReduce {
   void set_timeout_ms(int64_t ms) { timeout_ticks_ = ms * 100000; }   // s_memrealtime runs at 100 MHz
   void set_one_shot_max_bytes(int64_t b) { one_shot_max_ = b; }
   void set_max_blocks(int b) { max_blocks_ = b < 1 ? 1 : (b > kPeerMaxBlocks ? kPeerMaxBlocks : b); }
+  // In-place registered form.  register_buffer returns the bytes (IPC handle of the allocation's base |
+  // int64 offset of `ptr` in it) peers pass to open_registered; returns the registration id through
+  // `id` (the same on every rank when every rank registers in the same order).
+  std::string register_buffer(uintptr_t ptr, int64_t bytes, int* id);
+  void open_registered(int id, const std::vector<std::string>& handles);
+  // buf[off, off + count) of registration `id` = scale * sum over ranks, in place.  algo: 1 one-shot
+  // (count <= 2 MB of fp32), 2 two-shot, 0 auto.
+  void all_reduce_registered_f32(int id, int64_t off, int64_t count, float scale, int algo, uintptr_t stream);
+  int64_t registered_bytes(int id) const;
   void close();
 
  private:
@@ -86,6 +111,16 @@ class PeerAllReduce {
   uint32_t* err_dev_ = nullptr;             // its device address
   uint8_t* peers_[kPeerMaxRanks] = {};
   uint8_t* peer_flags_[kPeerMaxRanks] = {};
+  uint8_t* ipflags_ = nullptr;                  // own in-place flag region (uncached): [3][blocks][ranks] u32
+  uint8_t* peer_ipflags_[kPeerMaxRanks] = {};
+  uint32_t* ipctrl_ = nullptr;                  // in-place calls: [0] call counter, [1] done counter
+  struct Reg {
+    uint8_t* base[kPeerMaxRanks] = {};          // every rank's registered buffer, mapped here ([rank] = own)
+    uint8_t* mapped[kPeerMaxRanks] = {};        // what hipIpcOpenMemHandle returned (closed in close())
+    int64_t bytes = 0;
+    bool open = false;
+  };
+  std::vector<Reg> regs_;
   bool opened_ = false;
   int64_t timeout_ticks_ = 10LL * 100000000;   // 10 s
   int64_t one_shot_max_ = 256 * 1024;

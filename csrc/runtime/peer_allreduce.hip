@@ -289,6 +289,159 @@ __global__ void __launch_bounds__(kThreads) peer_dev_probe_kernel(PeerDev d, con
   peer_ar_f32_vblock(d, in, out, count, scale, blockIdx.x, gridDim.x, two != 0, lds2);
 }
 
+
+// ============================================================================ in-place (registered)
+// See peer_allreduce.h.  Block b of every rank owns the same vectors; barriers are per block index.
+struct IpArgs {
+  uint8_t* data[kPeerMaxRanks];    // every rank's buffer at this call's first element (mapped here)
+  uint8_t* flags[kPeerMaxRanks];   // every rank's in-place flag region
+  uint32_t* ctrl;                  // [0] calls, [1] blocks done
+  uint32_t* errc;                  // the staged protocol's ctrl: [2] = time-out count (shared latch)
+  uint32_t* err_host;
+  int64_t n4, tail, chunk4, bytes;
+  int64_t timeout;
+  float scale;
+  int rank;
+};
+constexpr int kAuxSys = 1 | 16;    // sc0 sc1: system-scope (coherent across GPUs) load / write-through store
+
+__device__ __forceinline__ uint32_t* ip_flag(uint8_t* region, int phase, int block, int src) {
+  return reinterpret_cast<uint32_t*>(region) + (phase * kPeerMaxBlocks + block) * kPeerMaxRanks + src;
+}
+__device__ __forceinline__ vec_t ld_sys(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, kAuxSys));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ip_rsrc(const uint8_t* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Flag barrier of block b across ranks, NO fences: every wave drains its memory operations (loads
+// consumed, write-through stores acknowledged), then lane t < W stores the call number into rank t's
+// slot for this rank and waits for rank t's store into ours (relaxed system-scope accesses to
+// uncached memory).  A time-out poisons the call (NaN results) and latches the error words.
+template <int W>
+__device__ __forceinline__ void ip_barrier(const IpArgs& a, int phase, uint32_t target, bool failed, uint32_t* bad) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < W) {
+    __hip_atomic_store(ip_flag(a.flags[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = ip_flag(a.flags[a.rank], phase, blockIdx.x, t);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int spins = 0;
+    while (!failed && __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == 256) {
+        spins = 0;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
+          __hip_atomic_fetch_add(a.errc + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          *bad = 1u;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int W, bool TWO>
+__global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
+  __shared__ uint32_t s_call, s_bad;
+  if (threadIdx.x == 0) {
+    s_call = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_bad = __hip_atomic_load(a.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t target = s_call + 1u;
+  const bool failed = s_bad != 0;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  __amdgpu_buffer_rsrc_t rs[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) rs[p] = ip_rsrc(a.data[p], a.bytes);
+  float* own = reinterpret_cast<float*>(a.data[a.rank]);
+  const int64_t tail_off = a.n4 * 4;
+  const bool tail_lane = blockIdx.x == 0 && threadIdx.x < a.tail;
+  float tail_sum = 0.f;
+
+  ip_barrier<W>(a, 0, target, failed, &s_bad);          // A: every rank's buffer holds its input
+  if (tail_lane) {                                      // trailing elements: read now, written after B
+#pragma unroll
+    for (int p = 0; p < W; ++p)
+      tail_sum += __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rs[p], (int)((tail_off + threadIdx.x) * 4), 0, kAuxSys));
+  }
+  if (!TWO) {
+    const bool have = t0 < a.n4;                        // host guarantees gridDim * kThreads >= n4
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    vec_t v[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) v[p] = ld_sys(rs[p], have ? t0 : 0);
+#pragma unroll
+    for (int p = 0; p < W; ++p) F32Op::add(acc, v[p]);  // fixed rank order: bit-identical on every rank
+    ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every rank has read every buffer
+    const bool bad = s_bad != 0;
+    if (have) reinterpret_cast<vec_t*>(own)[t0] = bad ? F32Op::nan_vec() : F32Op::pack(acc, a.scale);
+    if (tail_lane) own[tail_off + threadIdx.x] = bad ? __builtin_nanf("") : tail_sum * a.scale;
+  } else {
+    // reduce-scatter: my chunk from every rank, written through into my own buffer
+    const int64_t lo = (int64_t)a.rank * a.chunk4;
+    const int64_t len = lo + a.chunk4 <= a.n4 ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
+    const __amdgpu_buffer_rsrc_t ro = rs[a.rank];
+    for (int64_t i = t0; i < len; i += stride) {
+      vec_t v[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) v[p] = ld_sys(rs[p], lo + i);
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < W; ++p) F32Op::add(acc, v[p]);
+      const vec_t r = s_bad ? F32Op::nan_vec() : F32Op::pack(acc, a.scale);
+      __builtin_amdgcn_raw_buffer_store_b128(r, ro, (int)((lo + i) * 16), 0, kAuxSys);
+    }
+    ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every chunk reduced, every input read
+    const bool bad = s_bad != 0;
+    if (tail_lane) own[tail_off + threadIdx.x] = bad ? __builtin_nanf("") : tail_sum * a.scale;
+    // all-gather: chunk q from its owner q (W-1 loads in flight per lane)
+    const int64_t last = a.n4 - 1;
+    for (int64_t i = t0; i < a.chunk4; i += stride) {
+      vec_t v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const int64_t g = (int64_t)q * a.chunk4 + i;
+        v[q] = (q == a.rank) ? vec_t{0u, 0u, 0u, 0u} : ld_sys(rs[q], g < last ? g : last);
+      }
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const int64_t g = (int64_t)q * a.chunk4 + i;
+        if (q != a.rank && g <= last) reinterpret_cast<vec_t*>(own)[g] = bad ? F32Op::nan_vec() : v[q];
+      }
+    }
+    ip_barrier<W>(a, 2, target, failed, &s_bad);        // C: every rank has gathered from every owner
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(a.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(a.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <bool TWO>
+void ip_launch(int world, const IpArgs& a, int nb, hipStream_t s) {
+  switch (world) {
+#define PDE_IP_CASE(W) \
+    case W: hipLaunchKernelGGL((peer_inplace_kernel<W, TWO>), dim3(nb), dim3(kThreads), 0, s, a); break;
+    PDE_IP_CASE(1) PDE_IP_CASE(2) PDE_IP_CASE(3) PDE_IP_CASE(4) PDE_IP_CASE(5) PDE_IP_CASE(6) PDE_IP_CASE(7)
+    PDE_IP_CASE(8)
+#undef PDE_IP_CASE
+    default: throw std::invalid_argument("peer all-reduce supports 1..8 ranks");
+  }
+}
+
+
 template <int W, typename Op>
 void launch_w(const Args& a, bool two, int nb, hipStream_t s) {
   if (two)
@@ -343,9 +496,18 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_b
   void* ed = nullptr;
   hip_check(hipHostGetDevicePointer(&ed, eh, 0), "hipHostGetDevicePointer(err)");
   err_dev_ = static_cast<uint32_t*>(ed);
+  void* ipf = nullptr;
+  hip_check(hipExtMallocWithFlags(&ipf, kFlagBytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipflags)");
+  ipflags_ = static_cast<uint8_t*>(ipf);
+  hip_check(hipMemset(ipflags_, 0, kFlagBytes), "hipMemset");
+  void* ipc = nullptr;
+  hip_check(hipExtMallocWithFlags(&ipc, 256, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipctrl)");
+  ipctrl_ = static_cast<uint32_t*>(ipc);
+  hip_check(hipMemset(ipctrl_, 0, 256), "hipMemset");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_[rank_] = region_;
   peer_flags_[rank_] = flags_;
+  peer_ipflags_[rank_] = ipflags_;
 }
 
 PeerAllReduce::~PeerAllReduce() {
@@ -363,9 +525,18 @@ void PeerAllReduce::close() {
     if (p == rank_) continue;
     if (peers_[p] != nullptr) (void)hipIpcCloseMemHandle(peers_[p]);
     if (peer_flags_[p] != nullptr) (void)hipIpcCloseMemHandle(peer_flags_[p]);
+    if (peer_ipflags_[p] != nullptr) (void)hipIpcCloseMemHandle(peer_ipflags_[p]);
+    for (auto& r : regs_)
+      if (r.mapped[p] != nullptr) (void)hipIpcCloseMemHandle(r.mapped[p]);
   }
+  regs_.clear();
   for (auto& q : peers_) q = nullptr;
   for (auto& q : peer_flags_) q = nullptr;
+  for (auto& q : peer_ipflags_) q = nullptr;
+  (void)hipFree(ipflags_);
+  (void)hipFree(ipctrl_);
+  ipflags_ = nullptr;
+  ipctrl_ = nullptr;
   (void)hipFree(region_);
   (void)hipFree(flags_);
   (void)hipFree(ctrl_);
@@ -379,9 +550,10 @@ void PeerAllReduce::close() {
 }
 
 std::string PeerAllReduce::handle() const {
-  hipIpcMemHandle_t h[2];
+  hipIpcMemHandle_t h[3];
   hip_check(hipIpcGetMemHandle(&h[0], flags_), "hipIpcGetMemHandle(flags)");
   hip_check(hipIpcGetMemHandle(&h[1], region_), "hipIpcGetMemHandle(data)");
+  hip_check(hipIpcGetMemHandle(&h[2], ipflags_), "hipIpcGetMemHandle(in-place flags)");
   return std::string(reinterpret_cast<const char*>(h), sizeof(h));
 }
 
@@ -390,15 +562,18 @@ void PeerAllReduce::open(const std::vector<std::string>& handles) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
-    if (handles[p].size() != 2 * kHandle) throw std::invalid_argument("bad IPC handle size");
-    hipIpcMemHandle_t h[2];
+    if (handles[p].size() != 3 * kHandle) throw std::invalid_argument("bad IPC handle size");
+    hipIpcMemHandle_t h[3];
     std::memcpy(h, handles[p].data(), sizeof(h));
     void* fp = nullptr;
     void* dp = nullptr;
+    void* ip = nullptr;
     hip_check(hipIpcOpenMemHandle(&fp, h[0], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(flags)");
     peer_flags_[p] = static_cast<uint8_t*>(fp);
     hip_check(hipIpcOpenMemHandle(&dp, h[1], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(data)");
     peers_[p] = static_cast<uint8_t*>(dp);
+    hip_check(hipIpcOpenMemHandle(&ip, h[2], hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(in-place flags)");
+    peer_ipflags_[p] = static_cast<uint8_t*>(ip);
   }
   opened_ = true;
 }
@@ -495,6 +670,94 @@ void PeerAllReduce::device_probe_f32(uintptr_t in, uintptr_t out, int64_t count,
   hipLaunchKernelGGL(peer_dev_probe_kernel, dim3((int)nb), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), d,
                      reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), count, scale, two);
   hip_check(hipGetLastError(), "peer device-path probe launch");
+}
+
+std::string PeerAllReduce::register_buffer(uintptr_t ptr, int64_t bytes, int* id) {
+  if (ptr & 15) throw std::invalid_argument("registered buffers must be 16-byte aligned");
+  if (bytes <= 0 || bytes > 0x7fffffffLL) throw std::invalid_argument("registered buffer size must be in (0, 2 GB)");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  void* base = nullptr;
+  size_t size = 0;
+  hip_check(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(ptr)), "hipMemGetAddressRange");
+  const int64_t off = (int64_t)(ptr - reinterpret_cast<uintptr_t>(base));
+  if (off < 0 || off + bytes > (int64_t)size) throw std::invalid_argument("buffer outside its allocation");
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle(registered)");   // the allocation's base: offset 0
+  Reg r;
+  r.base[rank_] = reinterpret_cast<uint8_t*>(ptr);
+  r.bytes = bytes;
+  regs_.push_back(r);
+  *id = (int)regs_.size() - 1;
+  std::string out(reinterpret_cast<const char*>(&h), sizeof(h));
+  out.append(reinterpret_cast<const char*>(&off), sizeof(off));
+  out.append(reinterpret_cast<const char*>(&bytes), sizeof(bytes));
+  return out;
+}
+
+void PeerAllReduce::open_registered(int id, const std::vector<std::string>& handles) {
+  if (id < 0 || id >= (int)regs_.size()) throw std::invalid_argument("unknown registration");
+  if ((int)handles.size() != world_) throw std::invalid_argument("need one registration handle per rank");
+  if (!opened_) throw std::runtime_error("open() the peer regions before registered buffers");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  Reg& r = regs_[id];
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    const std::string& s = handles[p];
+    if (s.size() != kHandle + 16) throw std::invalid_argument("bad registration handle size");
+    hipIpcMemHandle_t h;
+    int64_t off = 0, bytes = 0;
+    std::memcpy(&h, s.data(), kHandle);
+    std::memcpy(&off, s.data() + kHandle, 8);
+    std::memcpy(&bytes, s.data() + kHandle + 8, 8);
+    if (bytes != r.bytes) throw std::invalid_argument("registered buffers differ in size across ranks");
+    if (off & 15) throw std::invalid_argument("a peer's registered buffer is not 16-byte aligned");
+    void* m = nullptr;
+    hip_check(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(registered)");
+    r.mapped[p] = static_cast<uint8_t*>(m);
+    r.base[p] = static_cast<uint8_t*>(m) + off;
+  }
+  r.open = true;
+}
+
+int64_t PeerAllReduce::registered_bytes(int id) const {
+  if (id < 0 || id >= (int)regs_.size()) throw std::invalid_argument("unknown registration");
+  return regs_[id].bytes;
+}
+
+void PeerAllReduce::all_reduce_registered_f32(int id, int64_t off, int64_t count, float scale, int algo,
+                                              uintptr_t stream) {
+  if (id < 0 || id >= (int)regs_.size() || !regs_[id].open) throw std::runtime_error("registration not open");
+  const Reg& r = regs_[id];
+  if (count <= 0) return;
+  if (off < 0 || (off + count) * 4 > r.bytes) throw std::invalid_argument("range outside the registered buffer");
+  if (off & 3) throw std::invalid_argument("in-place range must start 16-byte aligned");
+  IpArgs a{};
+  for (int p = 0; p < world_; ++p) {
+    a.data[p] = r.base[p] + off * 4;
+    a.flags[p] = peer_ipflags_[p];
+  }
+  a.ctrl = ipctrl_;
+  a.errc = ctrl_;
+  a.err_host = err_dev_;
+  a.n4 = count / 4;
+  a.tail = count - a.n4 * 4;
+  a.bytes = count * 4;
+  a.timeout = timeout_ticks_;
+  a.scale = scale;
+  a.rank = rank_;
+  constexpr int64_t kOneShotMaxVec = (int64_t)kPeerMaxBlocks * kThreads;   // sums held in registers across B
+  bool two = algo == 2 || (algo == 0 && world_ > 2 && count * 4 > one_shot_max_);
+  if (!two && a.n4 > kOneShotMaxVec) {
+    if (algo == 1) throw std::invalid_argument("in-place one-shot holds at most 2 MB per call");
+    two = true;
+  }
+  a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
+  int64_t nb = ((two ? a.chunk4 : a.n4) + kThreads - 1) / kThreads;
+  nb = nb < 1 ? 1 : (nb > kPeerMaxBlocks ? kPeerMaxBlocks : nb);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (two) ip_launch<true>(world_, a, (int)nb, s);
+  else ip_launch<false>(world_, a, (int)nb, s);
+  hip_check(hipGetLastError(), "peer in-place all-reduce launch");
 }
 
 int64_t PeerAllReduce::error() {

@@ -806,6 +806,7 @@ class EngineComm:
         self.rank = group.rank()
         self.peer = None
         self.peer_reason = ""
+        self.peer_inplace = False
         self.routes = {}
         self.timings = {}
 
@@ -813,12 +814,17 @@ class EngineComm:
         self.group.rccl.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPES[t.dtype], _op_code(op),
                                    torch.cuda.current_stream(t.device).cuda_stream)
 
-    def enable_peer(self, sizes, device, dtype=torch.float32, capacity_bytes: Optional[int] = None, tune=True):
-        """Collective.  Returns the chosen route per size ({numel: 'rccl'|'peer1'|'peer2'})."""
+    def enable_peer(self, sizes, device, dtype=torch.float32, capacity_bytes: Optional[int] = None, tune=True,
+                    inplace: Optional[torch.Tensor] = None, bufs: Optional[dict] = None):
+        """Collective.  Returns the chosen route per size ({numel: 'rccl'|'peer1'|'peer2'}).
+        ``inplace``: a persistent fp32 buffer (the engine's flat gradients) to register, so the peer
+        routes of any range of it run in place (no stage copy; ``PDE_PEER_INPLACE=0`` disables);
+        ``bufs``: {numel: tensor} -- the tensors the routes will run on, timed instead of scratch ones."""
         from .peer import PeerAllReduce, tune_routes
         sizes = sorted({int(n) for n in sizes})
         esize = torch.tensor([], dtype=dtype).element_size()
         cap = capacity_bytes or max(sizes) * esize
+        self.peer_inplace = False
         if os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0":
             self.peer = PeerAllReduce(self.group, torch.device(device), cap)
             if not self.peer.ok:
@@ -826,9 +832,13 @@ class EngineComm:
                 self.peer = None
         else:
             self.peer_reason = "disabled by PDE_PEER_ALLREDUCE=0"
+        if self.peer is not None and inplace is not None and os.environ.get("PDE_PEER_INPLACE", "1") != "0":
+            self.peer_inplace = self.peer.register(inplace)
+            if not self.peer_inplace:
+                self.peer_reason = self.peer.reg_reason
         rccl_fn = self._rccl if self.group.rccl is not None else None
         if tune:
-            self.routes, self.timings = tune_routes(self.group, self.peer, rccl_fn, sizes, device, dtype)
+            self.routes, self.timings = tune_routes(self.group, self.peer, rccl_fn, sizes, device, dtype, bufs=bufs)
         else:
             self.routes = {n: ("peer2" if self.peer is not None else "rccl") for n in sizes}
         return self.routes

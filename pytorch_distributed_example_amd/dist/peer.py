@@ -17,6 +17,12 @@ path on every rank and the caller keeps using RCCL.
 every rank must then agree on RCCL only).  ``PDE_PEER_DEBUG_STALE=<rank>`` makes that rank skip
 staging one self-test call (a stale stage buffer): the self-test must then disable the path.
 
+``register(tensor)`` (collective) IPC-maps a persistent fp32 buffer of every rank (the engines' flat
+gradient buffer): an all-reduce of any range of it then runs IN PLACE -- the peers' gradients are read
+where the backward left them, with no stage copy and no L2 write-back / invalidate fences (only flag
+barriers; ``peer_allreduce.h``).  Registration runs its own self-test of both algorithms on the
+buffer (its contents are clobbered, then zeroed) and is voted on like the set-up.
+
 ``tune_routes`` times RCCL against the one-/two-shot peer kernels at the sizes an engine will use
 (max over ranks, so every rank takes the same decision) and returns the fastest per size.
 """
@@ -61,6 +67,8 @@ class PeerAllReduce:
         self.native = None
         self.ok = False
         self.reason = ""
+        self.reg_reason = ""
+        self._regs = []          # (data_ptr, numel, registration id, tensor kept alive)
         _SEQ[0] += 1
         key = f"{group.prefix}/peer_ar/{_SEQ[0]}"
         err = ""
@@ -112,18 +120,106 @@ class PeerAllReduce:
                 pass
             self.native = None
 
+    def register(self, t: torch.Tensor, self_test: bool = True) -> bool:
+        """Collective: map every rank's ``t`` (contiguous fp32, the same size on every rank) so that
+        ``all_reduce_`` of any 16-byte-aligned range of it runs in place.  False (on every rank) if any
+        rank failed; the staged path stays available either way."""
+        if not self.ok:
+            return False
+        _SEQ[0] += 1
+        key = f"{self.group.prefix}/peer_reg/{_SEQ[0]}"
+        err, rid = "", -1
+        try:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
+                raise ValueError("registered buffers are contiguous fp32 tensors on the rank's device")
+            rid, h = self.native.register_buffer(t.data_ptr(), t.numel() * 4)
+            self.group.store.set(f"{key}/h{self.rank}", h)
+        except Exception as e:   # noqa: BLE001
+            err = f"register: {e}"
+            self.group.store.set(f"{key}/h{self.rank}", b"")
+        hs = [self.group.store.get(f"{key}/h{r}") for r in range(self.world)]
+        if not err:
+            try:
+                if any(len(h) == 0 for h in hs):
+                    raise RuntimeError("a peer failed to register its buffer")
+                self.native.open_registered(rid, hs)
+            except Exception as e:   # noqa: BLE001
+                err = f"open registered: {e}"
+        ok = _host_allreduce_min(self.group, 0 if err else 1)
+        if ok and self_test:
+            try:
+                self._self_test_registered(t, rid)
+            except Exception as e:   # noqa: BLE001
+                err = f"registered self-test: {e}"
+            ok = _host_allreduce_min(self.group, 0 if err else 1)
+        if not ok:
+            print(f"[rank {self.rank}] in-place peer all-reduce disabled: {err or 'disabled by a peer rank'}",
+                  file=sys.stderr, flush=True)
+            self.reg_reason = err or "disabled by a peer rank"
+            return False
+        self._regs.append((t.data_ptr(), t.numel(), rid, t))
+        return True
+
+    def registered_range(self, t: torch.Tensor):
+        """(registration id, element offset) if ``t`` is a 16-byte aligned fp32 range of a registered
+        buffer, else None."""
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            return None
+        p = t.data_ptr()
+        for base, n, rid, _ in self._regs:
+            if base <= p and p + t.numel() * 4 <= base + n * 4 and (p - base) % 16 == 0:
+                return rid, (p - base) // 4
+        return None
+
+    def _self_test_registered(self, buf: torch.Tensor, rid: int):
+        W, r = self.world, self.rank
+        n_all = buf.numel()
+        call = [0]
+
+        def data(n, rank, c):
+            i = torch.arange(n, device=self.device, dtype=torch.int64)
+            return (((i * 7 + c * 13 + rank * 5) % 17) - 8).to(torch.float32)
+
+        s = torch.cuda.current_stream(self.device)
+        for n in sorted({1, 5, 4099, min(n_all, 70001), n_all - (n_all % 4)}):
+            if n <= 0 or n > n_all:
+                continue
+            for algo in (1, 2):
+                if algo == 1 and n > 256 * 512 * 4:
+                    continue
+                for off in (0, 4 * ((n_all - n) // 8)):      # two offsets inside the buffer
+                    c = call[0]
+                    call[0] += 1
+                    buf[off:off + n].copy_(data(n, r, c))
+                    self.native.all_reduce_registered_f32(rid, off, n, 1.0, algo, s.cuda_stream)
+                    torch.cuda.synchronize(self.device)
+                    if self.error():
+                        raise RuntimeError(f"barrier time-out (algo {algo}, n={n}, off={off})")
+                    want = sum(data(n, q, c) for q in range(W))
+                    if not torch.equal(buf[off:off + n], want):
+                        bad = int((buf[off:off + n] != want).sum())
+                        raise RuntimeError(f"algo {algo} n={n} off={off} call {c}: {bad} wrong elements")
+        buf.zero_()
+
     @property
     def capacity_bytes(self) -> int:
         return self.native.capacity_bytes if self.native is not None else 0
 
     def supports(self, t: torch.Tensor) -> bool:
+        if self.ok and self.registered_range(t) is not None:
+            return True
         return (self.ok and t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
                 and t.numel() * t.element_size() <= self.capacity_bytes and t.data_ptr() % 16 == 0)
 
     def all_reduce_(self, t: torch.Tensor, algo: str = "auto", scale: float = 1.0, stream=None):
-        """In-place SUM (times ``scale``) on ``stream`` (default: the current stream)."""
+        """In-place SUM (times ``scale``) on ``stream`` (default: the current stream): straight on the
+        peers' buffers when ``t`` lies in a registered buffer, else through the staged regions."""
         s = stream if stream is not None else torch.cuda.current_stream(t.device)
         a = _ALGO.get(algo, 0)
+        reg = self.registered_range(t)
+        if reg is not None and not (a == 1 and t.numel() > 256 * 512 * 4):
+            self.native.all_reduce_registered_f32(reg[0], reg[1], t.numel(), float(scale), a, s.cuda_stream)
+            return
         fn = self.native.all_reduce_f32 if t.dtype == torch.float32 else self.native.all_reduce_bf16
         fn(t.data_ptr(), t.data_ptr(), t.numel(), float(scale), a, s.cuda_stream)
 
@@ -204,7 +300,7 @@ def _time_calls(fn, iters: int, device) -> float:
 
 
 def tune_routes(group, peer: Optional[PeerAllReduce], rccl_fn, sizes: Iterable[int], device,
-                dtype=torch.float32, iters: int = 30):
+                dtype=torch.float32, iters: int = 30, bufs: Optional[dict] = None):
     """Fastest all-reduce route per element count: ({numel: 'rccl' | 'peer1' | 'peer2'},
     {numel: {candidate: us per call (max over ranks)}}).
 
@@ -220,7 +316,8 @@ def tune_routes(group, peer: Optional[PeerAllReduce], rccl_fn, sizes: Iterable[i
             cands.append(RCCL)
         buf = None
         if peer is not None and peer.ok:
-            buf = torch.zeros(n, device=device, dtype=dtype)
+            # the tensor the route will run on (a registered buffer times the in-place kernel)
+            buf = bufs[n] if bufs and n in bufs else torch.zeros(n, device=device, dtype=dtype)
             if peer.supports(buf):
                 cands += [ONE_SHOT, TWO_SHOT]
         if forced in cands:
@@ -232,6 +329,8 @@ def tune_routes(group, peer: Optional[PeerAllReduce], rccl_fn, sizes: Iterable[i
             out[n] = cands[0]
             continue
         times = []
+        if buf is None:
+            buf = bufs[n] if bufs and n in bufs else torch.zeros(n, device=device, dtype=dtype)
         for c in cands:
             fn = (lambda: rccl_fn(buf)) if c == RCCL else (lambda c=c: peer.all_reduce_(buf, c))
             fn()

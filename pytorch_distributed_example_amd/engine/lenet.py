@@ -179,8 +179,11 @@ class LeNetTrainStep:
         self.bucket_ranges = [tuple(r) for r in self.layout.bucket_ranges]
         assert self.bucket_ranges[0][0] == 0 and self.bucket_ranges[1][0] >= self.bucket_ranges[0][1]
         if self.comm_on and hasattr(comm, "enable_peer") and not comm.routes:
-            # small buckets: time the xGMI peer all-reduce against RCCL at exactly these sizes
-            comm.enable_peer([b.numel() for b in self.bucket_grads] + [self.grads.numel()], dev)
+            # small buckets: time the xGMI peer all-reduce against RCCL at exactly these sizes, on the
+            # flat gradient buffer itself, registered so the peer routes read it in place
+            bufs = {b.numel(): b for b in self.bucket_grads}
+            bufs[self.grads.numel()] = self.grads
+            comm.enable_peer(list(bufs), dev, inplace=self.grads, bufs=bufs)
         self.X = self.Y = self.idx = None
         self.nbatches = 0
         self.graphs = {}

@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(19))
+CFGS = list(range(21))
 
 
 def rel_err(a, b):
@@ -25,11 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 19
+    assert K.gemm_num_cfgs() == 21
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
                                                      (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
-                                                     (256, 256), (256, 192), (256, 256), (256, 256)]
+                                                     (256, 256), (256, 192), (256, 256), (256, 256), (256, 256), (256, 256)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -128,7 +128,7 @@ def test_k_tail(cfg):
         assert rel_err(db, dy3.float().sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [14, 15, 16, 17])
+@pytest.mark.parametrize("cfg", [14, 15, 16, 17, 19, 20])
 @pytest.mark.parametrize("M,N,K", [(8200, 1544, 192), (4100, 3080, 1000)])
 def test_persistent_multi_tile(cfg, M, N, K):
     """Persistent configs with more tiles than CUs (each block walks several tiles, a tile's stores in
@@ -193,3 +193,43 @@ def test_gemm8p_wgrad(T, N, K, splits):
     assert rel_err(db, dy.float().sum(0)) < 1e-2
     dw17, db17 = G.wgrad(dy, x, want_db=True, cfg=17, splits=splits)
     assert torch.equal(dw, dw17) and torch.equal(db, db17)
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (9000, 3072, 768), (4100, 776, 1536), (300, 200, 64),
+                                   (20000, 2056, 128)])
+def test_gemm8pp_persistent_bit_identical(M, N, K):
+    """cfg 19, the 8-phase loop in a persistent block per CU (the next tile's prologue DMA issued before
+    this tile's stores, the first K-tile's waits counting those stores in flight): bit-identical to
+    cfg 18 over many tiles per block, ragged edges, one- and two-K-tile shapes; fprop (bias, GELU) and
+    dgrad (plain, GELU backward)."""
+    x, w, b = _bf(M, K, seed=50), _bf(N, K, scale=0.03, seed=51), _bf(N, seed=52)
+    y = G.fprop(x, w, b, cfg=19)
+    assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
+    assert torch.equal(y, G.fprop(x, w, b, cfg=18))
+    a19, d19 = G.fprop(x, w, b, gelu=True, cfg=19)
+    a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
+    assert torch.equal(a19, a18) and torch.equal(d19, d18)
+    dy, w2 = _bf(M, K, seed=53), _bf(K, N, scale=0.03, seed=54)
+    assert torch.equal(G.dgrad(dy, w2, cfg=19), G.dgrad(dy, w2, cfg=18))
+    dg = _bf(M, N, seed=55)
+    assert torch.equal(G.dgrad(dy, w2, dgelu=dg, cfg=19), G.dgrad(dy, w2, dgelu=dg, cfg=18))
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (9000, 3072, 768), (4100, 776, 1536), (20000, 2056, 128),
+                                   (300, 200, 256), (16384, 768, 3072)])
+def test_gemm8pc_continuous_bit_identical(M, N, K):
+    """cfg 20: one K-tile stream per persistent block (the next tile's first K-tiles issued as ordinary
+    look-ahead slots), register epilogue merging block pairs across lanes: bit-identical to cfg 18 for
+    fprop (with and without bias, with a scale) and dgrad, over many tiles per block and ragged edges."""
+    x, w, b = _bf(M, K, seed=60), _bf(N, K, scale=0.03, seed=61), _bf(N, seed=62)
+    y = G.fprop(x, w, b, cfg=20)
+    assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
+    assert torch.equal(y, G.fprop(x, w, b, cfg=18))
+    assert torch.equal(G.fprop(x, w, None, cfg=20), G.fprop(x, w, None, cfg=18))
+    a20, d20 = G.fprop(x, w, b, gelu=True, cfg=20)         # GELU form runs cfg 19
+    a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
+    assert torch.equal(a20, a18) and torch.equal(d20, d18)
+    dy, w2 = _bf(M, K, seed=63), _bf(K, N, scale=0.03, seed=64)
+    assert torch.equal(G.dgrad(dy, w2, cfg=20), G.dgrad(dy, w2, cfg=18))
+    s = torch.tensor([0.37], device=dev)
+    assert torch.equal(G.dgrad(dy, w2, cfg=20, scale=s), G.dgrad(dy, w2, cfg=18, scale=s))

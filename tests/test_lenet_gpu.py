@@ -348,3 +348,4 @@ def test_engine_rejects_unknown_bwd_mode(monkeypatch):
     monkeypatch.setenv("PDE_LENET_BWD_MODE", "v1")
     with pytest.raises(ValueError):
         LeNetTrainStep(build_net(seed=1, device=DEV), batch_size=128)
+

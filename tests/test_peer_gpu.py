@@ -159,3 +159,13 @@ def test_engine_w2_matches_w1_on_concatenated_shards():
     assert min(w) > 0.2, w
     for a, b in zip(res[0]["w_params"], res[0]["one_params"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(b)), (res[0]["w_params"], res[0]["one_params"])
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_peer_inplace_registered_matches_exact(world):
+    """The in-place route over a registered buffer: exact sums, nothing written outside the range,
+    bit-identical across ranks, graph-replayable."""
+    rc, res, logs = run_ranks("peer_inplace", world, "1")
+    assert rc == 0, "\n".join(logs)
+    assert all(r is not None for r in res), "\n".join(logs)
+    assert all(r["sums"] == res[0]["sums"] for r in res), "results differ across ranks"
