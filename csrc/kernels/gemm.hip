@@ -48,6 +48,7 @@ namespace {
 using namespace pde_lds;
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 enum Epi { kBf16 = 0, kGelu = 1, kGeluBwd = 2, kSlab = 3 };
 
@@ -1712,14 +1713,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
 // outstanding and the stores drain under its MFMAs.
 // TA = 0, no split-K / bias gradient, epilogues bf16 and bias + GELU; K % 128 == 0 (an even K-tile count
 // keeps every tile starting on LDS buffer 0).
-template <bool TB, int EPI>
+//
+// TN = 3 (cfg 21: a 256 x 192 tile, each wave 128 x 48): B regions B0 = n-blocks 0..1 of every wave (two
+// instructions per wave), B1 = n-block 2 (one); phases 2 and 3 run the single n-block 2 (8 MFMAs); any four
+// consecutive phases still issue one slot of each region, so the counted wait keeps 1 + 2 + 2 + 2 = 7
+// instructions in flight; the third accumulator column has no merge partner and is stored 8 bytes per lane.
+template <bool TB, int EPI, int TN = 4>
 __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
   constexpr bool TA = false;
-  constexpr int WM = 2, WN = 4, TM = 8, TN = 4;
-  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256
-  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 KB per K-tile
-  constexpr int VMW = TB ? 6 : 8;
-  constexpr int NS = TM * (TN / 2) * (EPI == kGelu ? 2 : 1);                   // 16-byte stores per lane per tile
+  constexpr int WM = 2, WN = 4, TM = 8;
+  static_assert(TN == 4 || (TN == 3 && !TB), "256 x 256, or 256 x 192 with a K-contiguous B");
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256 / 192
+  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 / 56 KB per K-tile
+  constexpr int B1N = TN == 4 ? 2 : 1;                                         // instructions of region B1
+  constexpr int VMW = TB ? 6 : (TN == 4 ? 8 : 7);
+  constexpr int NS = TM * (TN / 2 + TN % 2) * (EPI == kGelu ? 2 : 1);          // stores per lane per tile
   static_assert(EPI == kBf16 || EPI == kGelu, "bf16 / bias + GELU epilogues");
   static_assert(VMW + NS <= 63, "vmcnt is a 6-bit count");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -1758,16 +1766,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       int g;
       if (tr) g = (isA ? 2 * u + r : 2 * (r - 2) + u) * 8 + w;
       else if (isA) g = u * 16 + 8 * r + w;
-      else {
+      else if (TN == 4) {
         const int x = 8 * u + w;
         g = (x >> 2) * 8 + (x & 3) + 4 * (r - 2);
+      } else if (r == 2) {                      // 48-row wave images: n-blocks 0..1 = groups 6w'..6w'+3
+        const int x = 8 * u + w;
+        g = (x >> 2) * 6 + (x & 3);
+      } else {                                  // n-block 2 = groups 6w'+4, 6w'+5 (one instruction)
+        g = (w >> 1) * 6 + 4 + (w & 1);
       }
       gldso[r][u] = (isA ? 0 : ABYTES) + g * 1024;
     }
   // per-lane part of every region's global offset (tile-independent) and the lane's row / column inside
   // the tile for the bounds mask; a tile adds its wave-uniform base (m0 * lda or n0, in bytes)
   uint32_t lo_[4][2];
-  int lim_[4][2];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1777,21 +1789,25 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       const int g = (gldso[r][u] - (isA ? 0 : ABYTES)) >> 10;
       const int ch = glds_chunk(l, g & 1);
       const int ld = isA ? a.lda : a.ldb;
-      if (tr) {
-        const int k = 8 * (g & 7) + lrow, c = 64 * (g >> 3) + 8 * ch;
-        lo_[r][u] = (uint32_t)(((size_t)k * ld + c) * 2);
-        lim_[r][u] = c;
-      } else {
-        const int row = 8 * g + lrow;
-        lo_[r][u] = (uint32_t)(((size_t)row * ld + 8 * ch) * 2);
-        lim_[r][u] = row;
-      }
+      if (tr) lo_[r][u] = (uint32_t)(((size_t)(8 * (g & 7) + lrow) * ld + 64 * (g >> 3) + 8 * ch) * 2);
+      else lo_[r][u] = (uint32_t)(((size_t)(8 * g + lrow) * ld + 8 * ch) * 2);
     }
+  // the lane's row (K-contiguous operand) or column (transposed) inside the tile, for the bounds mask
+  auto lane_pos = [&](int r, int u) -> int {
+    const bool isA = r < 2;
+    const bool tr = isA ? TA : TB;
+    const int g = (gldso[r][u] - (isA ? 0 : ABYTES)) >> 10;
+    return tr ? 64 * (g >> 3) + 8 * glds_chunk(l, g & 1) : 8 * g + lrow;
+  };
   // region r of K-tile ktt of this block's tile jt (into buffer ktt & 1)
+  // tile origins of the even / odd tile in flight (a tile's slots are issued while it or its predecessor
+  // runs, so two are live; refreshed once per tile -- coords() costs three integer divisions)
+  int m0e = 0, n0e = 0, m0o = 0, n0o = 0;
+  coords(0, m0e, n0e);
+  if (nmy > 1) coords(1, m0o, n0o);
   auto issue = [&](int r, int jt, int ktt) {
     if (jt >= nmy) return;
-    int m0, n0;
-    coords(jt, m0, n0);
+    const int m0 = (jt & 1) ? m0o : m0e, n0 = (jt & 1) ? n0o : n0e;
     const bool isA = r < 2;
     const bool tr = isA ? TA : TB;
     const int o0 = isA ? m0 : n0, lim = isA ? a.M : a.N;
@@ -1799,8 +1815,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
     const char* base = smem + (ktt & 1) * STAGE;
     const uint32_t ko = (uint32_t)ktt * (isA ? astep : bstep);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      glds16(isA ? ar : br, base + gldso[r][u], o0 + lim_[r][u] < lim ? lo_[r][u] + tb + ko : kOOB);
+    for (int u = 0; u < (r == 3 ? B1N : 2); ++u)
+      glds16(isA ? ar : br, base + gldso[r][u], o0 + lane_pos(r, u) < lim ? lo_[r][u] + tb + ko : kOOB);
   };
 
   const int q16 = l & 15, prow = q16 < 4 ? q16 : (q16 < 12 ? q16 + 4 : q16 - 8);
@@ -1854,7 +1870,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
         });
       }
       if constexpr (PH == 1 || PH == 2) {
-        static_for<0, 2>([&](auto J_) {
+        static_for<0, (PH == 1 ? 2 : TN - 2)>([&](auto J_) {
           constexpr int jj = decltype(J_)::value + (PH == 2 ? 2 : 0);
           fb[jj][0] = rdB(std::integral_constant<int, jj>{}, 0);
           fb[jj][1] = rdB(std::integral_constant<int, jj>{}, 1);
@@ -1877,10 +1893,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       lgkm_fence();
       __builtin_amdgcn_s_setprio(1);
       constexpr int I0 = (PH <= 2) ? 0 : 4, J0 = (PH == 1 || PH == 4) ? 0 : 2;
+      constexpr int NJ = (PH == 1 || PH == 4) ? 2 : TN - 2;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
+        for (int jj = 0; jj < NJ; ++jj)
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
             acc[I0 + i][J0 + jj] =
@@ -1900,8 +1917,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       phase(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{}, kt + 1, false);
     }
     // ---- register epilogue: merge block pairs across the lane pair, one 16-byte store per pair ----
-    int m0, n0;
-    coords(j, m0, n0);
+    const int m0 = (j & 1) ? m0o : m0e, n0 = (j & 1) ? n0o : n0e;
+    // every slot of tile j has been issued: its origin makes room for tile j + 2's (read by the stores
+    // below through m0 / n0, copied above)
+    if (j + 2 < nmy) {
+      if (j & 1) coords(j + 2, m0o, n0o);
+      else coords(j + 2, m0e, n0e);
+    }
     const int row0 = m0 + wm * WTM + mrow, col0 = n0 + wn * WTN + (pcol & 8);
 #pragma unroll
     for (int jp = 0; jp < TN / 2; ++jp) {
@@ -1930,19 +1952,52 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
         if constexpr (EPI == kBf16) {
           emit(pack4(v0), pack4(v1), cr);
         } else {
+          // GELU of the bf16-rounded pre-activation, as the LDS epilogues of cfgs 17-19 compute it
+          const uint2 p0 = pack4(v0), p1 = pack4(v1);
+          const uint32_t w0[2] = {p0.x, p0.y}, w1[2] = {p1.x, p1.y};
           uint32_t y0[2], d0[2], y1[2], d1[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             pde_f2 d;
-            pde_f2 y = gelu2_d(pde_f2{v0[2 * e], v0[2 * e + 1]}, d);
+            pde_f2 y = gelu2_d(pde_f2{bf_lo(w0[e]), bf_hi(w0[e])}, d);
             y0[e] = pack_bf2(y.x, y.y);
             d0[e] = pack_bf2(d.x, d.y);
-            y = gelu2_d(pde_f2{v1[2 * e], v1[2 * e + 1]}, d);
+            y = gelu2_d(pde_f2{bf_lo(w1[e]), bf_hi(w1[e])}, d);
             y1[e] = pack_bf2(y.x, y.y);
             d1[e] = pack_bf2(d.x, d.y);
           }
           emit(make_uint2(y0[0], y0[1]), make_uint2(y1[0], y1[1]), cr);
           emit(make_uint2(d0[0], d0[1]), make_uint2(d1[0], d1[1]), c2r);
+        }
+      }
+    }
+    if constexpr (TN % 2) {                      // the unpaired last n-block: 8 bytes per lane
+      constexpr int jl = TN - 1;
+      float bvl[4] = {0.f, 0.f, 0.f, 0.f};
+      const int nl = n0 + wn * WTN + 16 * jl + pcol;
+      if (has_bias && nl < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + nl), bvl);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = row0 + 16 * i;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (acc[i][jl][e] + bvl[e]) * sc;
+        const uint32_t off = (row < a.M && nl < a.N) ? (uint32_t)(((size_t)row * a.ldc + nl) * 2) : kOOB;
+        const uint2 pv = pack4(v);
+        if constexpr (EPI == kBf16) {
+          __builtin_amdgcn_raw_buffer_store_b64(v2u{pv.x, pv.y}, cr, off, 0, 0);
+        } else {
+          const uint32_t wv[2] = {pv.x, pv.y};
+          uint32_t y[2], d2[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            pde_f2 d;
+            const pde_f2 yy = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+            y[e] = pack_bf2(yy.x, yy.y);
+            d2[e] = pack_bf2(d.x, d.y);
+          }
+          __builtin_amdgcn_raw_buffer_store_b64(v2u{y[0], y[1]}, cr, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(v2u{d2[0], d2[1]}, c2r, off, 0, 0);
         }
       }
     }
@@ -2020,7 +2075,10 @@ template <> struct Cfg<19> { static constexpr int V = 6, TM = 8, TN = 4, WM = 2,
 //   20: the 8-phase loop as one continuous K-tile stream per persistent block (k_gemm8pc), register
 //       epilogue; fprop (bias) and plain dgrad with K % 128 == 0; other calls run 19
 template <> struct Cfg<20> { static constexpr int V = 7, TM = 8, TN = 4, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 21;
+//   21: 20 at 256 x 192 (waves of 128 x 48), fprop only (bias / bias + GELU); other calls run 17 (256 x 192
+//       would otherwise change the tile grid of a fallback): dgrad / wgrad / odd K-tile counts
+template <> struct Cfg<21> { static constexpr int V = 8, TM = 8, TN = 3, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 22;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -2042,9 +2100,17 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 7) {
-    // (the bias + GELU form still spills a few registers inside the K loop: runs 19)
-    constexpr bool ok = !TA && !CS && EPI == kBf16;
+  if constexpr (C::V == 8) {
+    constexpr bool ok = !TA && !TB && !CS && (EPI == kBf16 || EPI == kGelu);
+    if constexpr (ok) {
+      if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
+        hipLaunchKernelGGL((k_gemm8pc<false, EPI, 3>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 7) {
+    constexpr bool ok = !TA && !CS && (EPI == kBf16 || (EPI == kGelu && !TB));
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
         hipLaunchKernelGGL((k_gemm8pc<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
@@ -2113,7 +2179,8 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 17: return launch_cfg<17, TA, TB, EPI, CS>(a, splits, st);
     case 18: return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
     case 19: return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<20, TA, TB, EPI, CS>(a, splits, st);
+    case 20: return launch_cfg<20, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<21, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -2127,7 +2194,8 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
   static const int t[kNumCfg][2] = {{256, 192}, {256, 128}, {128, 128}, {256, 256}, {128, 128},
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                                     {256, 256}, {256, 192}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
+                                     {256, 256}, {256, 192}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
+                                     {256, 192}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];

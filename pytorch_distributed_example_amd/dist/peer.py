@@ -217,7 +217,9 @@ class PeerAllReduce:
         s = stream if stream is not None else torch.cuda.current_stream(t.device)
         a = _ALGO.get(algo, 0)
         reg = self.registered_range(t)
-        if reg is not None and not (a == 1 and t.numel() > 256 * 512 * 4):
+        if reg is not None:
+            if a == 1 and t.numel() > 256 * 512 * 4:     # one-shot holds <= 2 MB of sums: two-shot in place
+                a = 2
             self.native.all_reduce_registered_f32(reg[0], reg[1], t.numel(), float(scale), a, s.cuda_stream)
             return
         fn = self.native.all_reduce_f32 if t.dtype == torch.float32 else self.native.all_reduce_bf16

@@ -57,7 +57,9 @@ class LeNetTrainStep:
         self.comm = comm
         self.world = comm.world_size if comm is not None else 1
         # communication schedule (W > 1): "overlap" = fc bucket all-reduced on the comm stream beside
-        # the conv backward; "flat" = one all-reduce on the comm stream after backward; "serial" = one
+        # the conv backward (conv bucket on the comm stream too: four cross-stream edges per step);
+        # "overlap2" = the same fc overlap, the conv bucket after it on the comm stream and one join
+        # before the whole optimizer (three edges); "flat" = one all-reduce on the comm stream after backward; "serial" = one
         # all-reduce on the compute stream (no cross-stream edges: in a hipGraph each edge between
         # kernels on different streams measured 5-9 us, see autotune_schedule); "fused" = the fc
         # bucket is all-reduced by side blocks of the conv backward kernel (xGMI peer protocol), the
@@ -338,12 +340,23 @@ class LeNetTrainStep:
                 self.comm.all_reduce_(self.bucket_grads[1])
                 self._opt(0, self.params.numel(), True)
             return
-        if self.comm_on and self.mode == "overlap":
+        if self.comm_on and self.mode in ("overlap", "overlap2"):
             ev["fc"].record(cur)
             cs.wait_event(ev["fc"])
             with torch.cuda.stream(cs):
                 self.comm.all_reduce_(self.bucket_grads[0])
         conv_bwd()
+        if self.comm_on and self.mode == "overlap2":
+            # three cross-stream edges per step instead of four: both buckets are reduced on the comm
+            # stream (one communicator, one stream: collectives stay ordered), then ONE join before the
+            # whole optimizer (no separate fc-range update beside the conv bucket's reduction)
+            ev["conv"].record(cur)
+            cs.wait_event(ev["conv"])
+            with torch.cuda.stream(cs):
+                self.comm.all_reduce_(self.bucket_grads[1])
+            cur.wait_stream(cs)
+            self._opt(0, self.params.numel(), True)
+            return
         if not self.comm_on or self.mode == "none":     # "none": the comm path's compute alone (autotune probe)
             self._opt(0, self.params.numel(), True)
             return
@@ -558,6 +571,7 @@ class LeNetTrainStep:
             routes += ["peer1", "peer2"]
         n0, n1, nall = (self.bucket_grads[0].numel(), self.bucket_grads[1].numel(), self.grads.numel())
         out = [("overlap", {n0: a, n1: b}) for a in routes for b in routes]
+        out += [("overlap2", {n0: a, n1: b}) for a in routes for b in routes]
         out += [(m, {nall: a}) for m in ("flat", "serial") for a in routes]
         if getattr(self.comm, "peer", None) is not None:
             out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in routes]
@@ -679,7 +693,7 @@ class LeNetTrainStep:
         # a schedule with cross-stream edges (overlap / flat) must win by > 1 %: in a replayed hipGraph
         # every such edge adds 5-9 us of jitter-prone join latency (round 3: flat 61.9 us in the
         # autotuner, 68.3 us in the timed window; the single-stream serial schedule measured 62.0)
-        eff = [x * (1.01 if cands[i][0] in ("overlap", "flat") else 1.0) for i, x in enumerate(times)]
+        eff = [x * (1.01 if cands[i][0] in ("overlap", "overlap2", "flat") else 1.0) for i, x in enumerate(times)]
         best = min(range(len(cands)), key=lambda i: eff[i])
         self.mode, self.comm.routes = cands[best][0], dict(cands[best][1])
         self.graphs.clear()

@@ -23,7 +23,7 @@ fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 
 v_mfma_f32_16x16x32_bf16 (every operand layout: fprop, dgrad, split-K wgrad); 18 = the 8-phase
 256x256 loop (every layout); 19 = 18 in a persistent block per CU (fprop / dgrad; other calls run 18);
 20 = 18 as one continuous K-tile stream per persistent block with a register epilogue (bias fprop /
-plain dgrad, K % 128 == 0; other calls run 19).
+plain dgrad, K % 128 == 0; other calls run 19); 21 = 20 at 256x192 (fprop; other calls run 16).
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -41,10 +41,10 @@ N_CU = 256
 _TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (128, 128),
           5: (256, 256), 6: (256, 192), 7: (256, 128), 8: (128, 128), 9: (256, 192), 10: (256, 192),
           11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 192), 15: (256, 256),
-          16: (256, 192), 17: (256, 256), 18: (256, 256), 19: (256, 256), 20: (256, 256)}
+          16: (256, 192), 17: (256, 256), 18: (256, 256), 19: (256, 256), 20: (256, 256), 21: (256, 192)}
 # relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
 _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 8: 0.8, 9: 1.0, 10: 1.0, 11: 1.0,
-             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 1.0, 17: 1.0, 18: 1.0, 19: 1.0, 20: 1.0}
+             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 1.0, 17: 1.0, 18: 1.0, 19: 1.0, 20: 1.0, 21: 1.0}
 
 # GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/,
 # profiles/r3_gemm/):

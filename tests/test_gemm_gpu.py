@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(21))
+CFGS = list(range(22))
 
 
 def rel_err(a, b):
@@ -25,11 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 21
+    assert K.gemm_num_cfgs() == 22
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
                                                      (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
-                                                     (256, 256), (256, 192), (256, 256), (256, 256), (256, 256), (256, 256)]
+                                                     (256, 256), (256, 192), (256, 256), (256, 256), (256, 256), (256, 256), (256, 192)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -226,10 +226,26 @@ def test_gemm8pc_continuous_bit_identical(M, N, K):
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
     assert torch.equal(y, G.fprop(x, w, b, cfg=18))
     assert torch.equal(G.fprop(x, w, None, cfg=20), G.fprop(x, w, None, cfg=18))
-    a20, d20 = G.fprop(x, w, b, gelu=True, cfg=20)         # GELU form runs cfg 19
+    a20, d20 = G.fprop(x, w, b, gelu=True, cfg=20)
     a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
     assert torch.equal(a20, a18) and torch.equal(d20, d18)
     dy, w2 = _bf(M, K, seed=63), _bf(K, N, scale=0.03, seed=64)
     assert torch.equal(G.dgrad(dy, w2, cfg=20), G.dgrad(dy, w2, cfg=18))
     s = torch.tensor([0.37], device=dev)
     assert torch.equal(G.dgrad(dy, w2, cfg=20, scale=s), G.dgrad(dy, w2, cfg=18, scale=s))
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (16384, 2304, 768), (5000, 776, 256), (300, 200, 128)])
+def test_gemm8pc_192_bit_identical(M, N, K):
+    """cfg 21: the continuous 8-phase stream at 256 x 192 (waves of 128 x 48: one-instruction B1 region,
+    7 instructions in flight, an unpaired third n-block stored 8 bytes per lane): bit-identical to the
+    16x16x32 loop at the same tile (cfg 16) for bias and bias + GELU fprops; dgrad falls back to cfg 16."""
+    x, w, b = _bf(M, K, seed=70), _bf(N, K, scale=0.03, seed=71), _bf(N, seed=72)
+    y = G.fprop(x, w, b, cfg=21)
+    assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
+    assert torch.equal(y, G.fprop(x, w, b, cfg=16))
+    a21, d21 = G.fprop(x, w, b, gelu=True, cfg=21)
+    a16, d16 = G.fprop(x, w, b, gelu=True, cfg=16)
+    assert torch.equal(a21, a16) and torch.equal(d21, d16)
+    dy, w2 = _bf(M, K, seed=73), _bf(K, N, scale=0.03, seed=74)
+    assert torch.equal(G.dgrad(dy, w2, cfg=21), G.dgrad(dy, w2, cfg=16))

@@ -49,7 +49,7 @@ def test_engine_autotune_restores_training_state():
 
 @pytest.mark.parametrize("world,sched", [(2, s) for s in (
     "mode=fused:peer2:peer1", "mode=fused:peer1:peer2", "mode=serial:peer2:peer2",
-    "mode=fused:peer2:adam1", "mode=fused:peer1:adam2")])
+    "mode=fused:peer2:adam1", "mode=fused:peer1:adam2", "mode=overlap2:peer1:peer2", "mode=overlap2:peer2:peer1")])
 def test_engine_fused_schedules_match(world, sched):
     """The fc bucket all-reduced by side blocks of the conv backward (fused) and the serial schedule
     train exactly like the overlapped reference schedule (same parameters up to fp32 reassociation).
