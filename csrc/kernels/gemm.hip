@@ -35,6 +35,7 @@
 //
 // Blocks: XCD-aware id remap (pde_hip.h), then groups of 8 row tiles x all column tiles so the
 // blocks sharing an XCD's L2 share operand rows; split-K slices of one tile are adjacent ids.
+#include <cstdlib>
 #include <type_traits>
 
 #include "pde_act.h"
@@ -65,6 +66,7 @@ struct GemmArgs {
   int M, N, K, lda, ldb, ldc;
   int mtiles, ntiles, kper;
   int dbg;               // ablation (v1 loop, wrong results): 1 no DMA, 2 no waits/barriers, 4 no LDS reads
+  int ntc;               // cfg 19: store C (and C2) non-temporally (outputs far larger than the caches)
 };
 
 // Transposed-read lane bases delivering the STANDARD k order (element j of a lane in half h is
@@ -1139,16 +1141,21 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm16(GemmArgs a) {
 // passed behind its own wait).  Operand forms, split-K slabs and the bias-gradient MFMA (against a ones
 // fragment, m-blocks 0..3 by waves 0 / 1 in phase 1, 4..7 by waves 2 / 3 in phase 3: k-steps split over
 // the two) as k_gemm16; a K-contiguous operand needs K % 64 == 0 (no masked tail).
-template <bool TA, bool TB, int EPI, bool CS>
+// TN = 3 (cfg 22, fprop only): a 256 x 192 tile of 128 x 48 waves -- B1 is n-block 2 alone (one
+// instruction per wave), phases 2 and 3 run 8 MFMAs, and the counted wait keeps 7 instructions in flight
+// (any four consecutive phases issue one slot of each region: 1 + 2 + 2 + 2).
+template <bool TA, bool TB, int EPI, bool CS, int TN = 4>
 __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
-  constexpr int WM = 2, WN = 4, TM = 8, TN = 4, NT = 512;
-  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256
-  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 KB per K-tile
+  constexpr int WM = 2, WN = 4, TM = 8, NT = 512;
+  static_assert(TN == 4 || (TN == 3 && !TA && !TB && !CS), "256 x 192 only for the fprop layout");
+  constexpr int WTM = TM * 16, WTN = TN * 16, BM = WM * WTM, BN = WN * WTN;   // 256 x 256 / 192
+  constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;                  // 64 / 56 KB per K-tile
+  constexpr int B1N = TN == 4 ? 2 : 1;
   constexpr int RS = BN * 2 + 16;
   constexpr int TILE_BYTES = EPI == kSlab ? 0 : BM * RS;
   constexpr int EPI_BYTES = TILE_BYTES + (CS ? 2 * BM * 4 : 0);
   constexpr int SMEM = EPI_BYTES > 2 * STAGE ? EPI_BYTES : 2 * STAGE;
-  constexpr int VMW = TB ? 6 : 8;
+  constexpr int VMW = TB ? 6 : (TN == 4 ? 8 : 7);
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int t = threadIdx.x, l = t & 63;
@@ -1178,9 +1185,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
       int g;
       if (tr) g = (isA ? 2 * u + r : 2 * (r - 2) + u) * 8 + w;    // image q = (A: 2u + r | B: 2(r-2) + u)
       else if (isA) g = u * 16 + 8 * r + w;
-      else {
+      else if (TN == 4) {
         const int x = 8 * u + w;
         g = (x >> 2) * 8 + (x & 3) + 4 * (r - 2);
+      } else if (r == 2) {                      // 48-row wave images: n-blocks 0..1 = groups 6w'..6w'+3
+        const int x = 8 * u + w;
+        g = (x >> 2) * 6 + (x & 3);
+      } else {                                  // n-block 2 = groups 6w'+4, 6w'+5 (one instruction)
+        g = (w >> 1) * 6 + 4 + (w & 1);
       }
       const int ch = glds_chunk(l, g & 1);
       gldso[r][u] = (isA ? 0 : ABYTES) + g * 1024;
@@ -1201,7 +1213,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
     const char* base = smem + (kt & 1) * STAGE;
     const uint32_t ko = (uint32_t)kt * (r < 2 ? astep : bstep);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) glds16(r < 2 ? ar : br, base + gldso[r][u], goff[r][u] + ko);
+    for (int u = 0; u < (r == 3 ? B1N : 2); ++u) glds16(r < 2 ? ar : br, base + gldso[r][u], goff[r][u] + ko);
   };
 
   // ---- fragment lane bases ----
@@ -1240,12 +1252,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
     if constexpr (!TB) { issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0); issue(0, 1); issue(2, 1); }
     else { issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0); issue(0, 1); issue(2, 1); }
     // phase 0 reads K-tile 0's A0 + B0 (TB = 0) or A0 + B0 + B1 (TB = 1)
-    if (KT > 1) {
-      if constexpr (TB) wait_vm<6>();
-      else wait_vm<8>();
-    } else {
-      wait_vm<0>();
-    }
+    if (KT > 1) wait_vm<VMW>();               // every slot of phase 0's read set landed (A0, B0; TB: + B1)
+    else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
 
     auto phase = [&](auto BUF_, auto PH_, int kt) {
@@ -1271,7 +1279,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
         });
       }
       if constexpr (PH == 1 || PH == 2) {
-        static_for<0, 2>([&](auto J_) {
+        static_for<0, (PH == 1 ? 2 : TN - 2)>([&](auto J_) {
           constexpr int j = decltype(J_)::value + (PH == 2 ? 2 : 0);
           fb[j][0] = rdB(std::integral_constant<int, j>{}, 0);
           fb[j][1] = rdB(std::integral_constant<int, j>{}, 1);
@@ -1287,10 +1295,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
       lgkm_fence();
       __builtin_amdgcn_s_setprio(1);
       constexpr int I0 = (PH <= 2) ? 0 : 4, J0 = (PH == 1 || PH == 4) ? 0 : 2;
+      constexpr int NJ = (PH == 1 || PH == 4) ? 2 : TN - 2;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
             acc[I0 + i][J0 + j] =
@@ -1670,7 +1679,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
       const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
       const uint32_t co = chunk_off(c, tm0, tn0);
       if constexpr (EPI == kBf16) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
+        if (a.ntc) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
       } else if constexpr (EPI == kGelu) {
         uint32_t ya[4], da[4];
 #pragma unroll
@@ -2078,7 +2088,9 @@ template <> struct Cfg<20> { static constexpr int V = 7, TM = 8, TN = 4, WM = 2,
 //   21: 20 at 256 x 192 (waves of 128 x 48), fprop only (bias / bias + GELU); other calls run 17 (256 x 192
 //       would otherwise change the tile grid of a fallback): dgrad / wgrad / odd K-tile counts
 template <> struct Cfg<21> { static constexpr int V = 8, TM = 8, TN = 3, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
-constexpr int kNumCfg = 22;
+//   22: the one-shot 8-phase loop (18) at 256 x 192, fprop only; other calls run 16
+template <> struct Cfg<22> { static constexpr int V = 9, TM = 8, TN = 3, WM = 2, WN = 4, NST = 2, OCC = 1, SP = 2; };
+constexpr int kNumCfg = 23;
 
 int g_num_cu = 0;
 int num_cu() {
@@ -2100,7 +2112,16 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
   a.mtiles = (a.M + BM - 1) / BM;
   a.ntiles = (a.N + BN - 1) / BN;
   const int grid = splits * a.mtiles * a.ntiles;
-  if constexpr (C::V == 8) {
+  if constexpr (C::V == 9) {
+    constexpr bool ok = !TA && !TB && !CS && EPI != kSlab;
+    if constexpr (ok) {
+      if (splits == 1 && a.K % 64 == 0) {
+        hipLaunchKernelGGL((k_gemm8p<false, false, EPI, false, 3>), dim3(grid), dim3(512), 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
+  } else if constexpr (C::V == 8) {
     constexpr bool ok = !TA && !TB && !CS && (EPI == kBf16 || EPI == kGelu);
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
@@ -2180,7 +2201,8 @@ hipError_t launch_any(int cfg, GemmArgs& a, int splits, hipStream_t st) {
     case 18: return launch_cfg<18, TA, TB, EPI, CS>(a, splits, st);
     case 19: return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
     case 20: return launch_cfg<20, TA, TB, EPI, CS>(a, splits, st);
-    default: return launch_cfg<21, TA, TB, EPI, CS>(a, splits, st);
+    case 21: return launch_cfg<21, TA, TB, EPI, CS>(a, splits, st);
+    default: return launch_cfg<22, TA, TB, EPI, CS>(a, splits, st);
   }
 }
 
@@ -2195,7 +2217,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
                                      {256, 256}, {256, 192}, {256, 128}, {128, 128}, {256, 192},
                                      {256, 192}, {256, 256}, {256, 256}, {256, 128}, {256, 192},
                                      {256, 256}, {256, 192}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                     {256, 192}};
+                                     {256, 192}, {256, 192}};
   cfg = cfg < 0 || cfg >= kNumCfg ? 0 : cfg;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
@@ -2212,6 +2234,10 @@ void pde_gemm_set_dbg(int d) { g_gemm_dbg = d; }
 hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void* bias, const void* aux, float* colsum,
                     int ta, int tb, int epi, int M, int N, int K, int lda, int ldb, int ldc, int splits, int cfg,
                     const float* scale, hipStream_t st) {
+  // cfg bit 8: store C non-temporally (cfg 19; an output far larger than the caches, e.g. the LM-head
+  // logits: streamed past L2 / MALL instead of evicting the operand tiles every CU re-reads)
+  const int ntc = (cfg >> 8) & 1;
+  cfg &= 0xff;
   // a K-contiguous operand is staged in 8-element chunks: K % 8 == 0 unless both operands are transposed
   if (M <= 0 || N <= 0 || K <= 0 || (K % 8 && !(ta && tb)) || N % 8 || lda % 8 || ldb % 8 || ldc % 8 ||
       splits < 1)
@@ -2237,6 +2263,7 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   a.c_bytes = c_bytes < kOOB ? (uint32_t)c_bytes : kOOB;   // >= kOOB: cfgs 14 / 15 run the one-shot grid
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.dbg = g_gemm_dbg;
+  a.ntc = ntc;
   a.kper = (((K + 63) / 64 + splits - 1) / splits) * 64;
   splits = (K + a.kper - 1) / a.kper;
   if (!ta && !tb) {

@@ -23,7 +23,7 @@ fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 
 v_mfma_f32_16x16x32_bf16 (every operand layout: fprop, dgrad, split-K wgrad); 18 = the 8-phase
 256x256 loop (every layout); 19 = 18 in a persistent block per CU (fprop / dgrad; other calls run 18);
 20 = 18 as one continuous K-tile stream per persistent block with a register epilogue (bias fprop /
-plain dgrad, K % 128 == 0; other calls run 19); 21 = 20 at 256x192 (fprop; other calls run 16).
+plain dgrad, K % 128 == 0; other calls run 19); 21 = 20 at 256x192 (fprop; other calls run 16); 22 = 18 at 256x192 (fprop; other calls run 16).
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -41,22 +41,25 @@ N_CU = 256
 _TILES = {0: (256, 192), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (128, 128),
           5: (256, 256), 6: (256, 192), 7: (256, 128), 8: (128, 128), 9: (256, 192), 10: (256, 192),
           11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 192), 15: (256, 256),
-          16: (256, 192), 17: (256, 256), 18: (256, 256), 19: (256, 256), 20: (256, 256), 21: (256, 192)}
+          16: (256, 192), 17: (256, 256), 18: (256, 256), 19: (256, 256), 20: (256, 256), 21: (256, 192), 22: (256, 192)}
 # relative per-CU throughput of a full tile wave (bigger tiles re-read less through L2)
 _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 8: 0.8, 9: 1.0, 10: 1.0, 11: 1.0,
-             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 1.0, 17: 1.0, 18: 1.0, 19: 1.0, 20: 1.0, 21: 1.0}
+             12: 1.0, 13: 0.93, 14: 0.99, 15: 0.99, 16: 1.0, 17: 1.0, 18: 1.0, 19: 1.0, 20: 1.0, 21: 1.0, 22: 1.0}
 
 # GPT-2-small GEMMs at 16384 tokens, measured on MI355X (tools/gemm_own_bench.py, profiles/r2_gemm/,
 # profiles/r3_gemm/):
 #   fprop / dgrad: (kind, N, K) -> (cfg, 1) for M >= 4096 rows
 #   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
 _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
-    ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (9, 1), ("fprop", 3072, 768): (15, 1),
-    ("fprop", 768, 3072): (9, 1), ("fprop", 50304, 768): (15, 1),
+    # round 5 (profiles/r5_gemm/, profiles/r5_gpt2/): every GPT-2 GEMM on the framework's kernels, no
+    # library fallback -- the 8-phase loop at 256x192 (cfg 22) for the N = 768 output projections and
+    # c_attn (one tile round on 256 CUs, on par with or ahead of hipBLASLt), the persistent 8-phase loop
+    # (cfg 19) for the GELU fprop, the GELU-backward dgrad and the LM head (whose fprop stores the 1.65 GB
+    # of logits non-temporally: within 3 % of hipBLASLt, 12 % faster than plain stores)
+    ("fprop", 2304, 768): (22, 1), ("fprop", 768, 768): (22, 1), ("fprop", 3072, 768): (19, 1),
+    ("fprop", 768, 3072): (22, 1), ("fprop", 50304, 768): (19, 1),
     ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
-    # round 4: the 8-phase loop (cfg 18) where it measured fastest (profiles/r4_gemm/
-    # summary_8phase_v2_staggered.txt): the GELU-backward dgrad, the LM-head dgrad and the long-K wgrads
-    ("dgrad", 3072, 768): (18, 1), ("dgrad", 768, 50304): (18, 1),
+    ("dgrad", 3072, 768): (19, 1), ("dgrad", 768, 50304): (19, 1),
     # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/; 256x256 tiles
     # for cfg 18: 36 tiles x 7, 27 x 9)
     ("wgrad", 2304, 768): (18, 9), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (18, 7),
@@ -78,23 +81,6 @@ def _env_overrides() -> None:
 
 _env_overrides()
 
-
-def _lib_fprop_keys():
-    """Plain fprops (bias epilogue only: no GELU, nothing a library GEMM cannot do) whose (N, K) is listed
-    run through hipBLASLt (``F.linear``) instead of the own kernel.  Default: GPT-2's two output
-    projections (attn.c_proj 768x768, mlp.c_proj 768x3072), where the library measured faster in-step
-    (869.6 / 872.7 -> 878.5 / 881.4 K tok/s same box, profiles/r4_gpt2/fprop_lib_ab.txt; adding c_attn
-    2304x768 did not help further).  PDE_GEMM_FPROP_LIB="N:K,..." / "all" / "none" overrides."""
-    import os
-    spec = os.environ.get("PDE_GEMM_FPROP_LIB", "768:768,768:3072").strip()
-    if spec == "all":
-        return "all"
-    if spec in ("", "none"):
-        return set()
-    return {tuple(int(v) for v in x.split(":")) for x in spec.split(",") if x.strip()}
-
-
-_FPROP_LIB = _lib_fprop_keys()
 
 _SCRATCH: Dict[Tuple, torch.Tensor] = {}
 
@@ -143,21 +129,21 @@ def _chk(t: torch.Tensor, name: str):
 
 
 def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
-          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
-    """x2 [M, K] . w[N, K]^T (+ bias) -> y [M, N]; with ``gelu`` returns (gelu(y), gelu'(y))."""
+          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None, nt_out: bool = False):
+    """x2 [M, K] . w[N, K]^T (+ bias) -> y [M, N]; with ``gelu`` returns (gelu(y), gelu'(y)).
+    ``nt_out``: store y non-temporally (the persistent cfg 19 only; for outputs far larger than the
+    caches, e.g. the LM-head logits)."""
     _chk(x2, "x")
     _chk(w, "w")
     M, K = x2.shape
     N = w.shape[0]
-    if not gelu and out is None and cfg is None and (_FPROP_LIB == "all" or (N, K) in _FPROP_LIB):
-        return torch.nn.functional.linear(x2, w, bias)       # plain library GEMM (hipBLASLt)
     c = pick("fprop", M, N, K)[0] if cfg is None else cfg
     y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16) if out is None else out
     if gelu:
         dgelu = torch.empty_like(y)
         kernels().gemm_bf16(x2, w, y, 0, 0, EPI_GELU, M, N, K, K, K, N, 1, c, C2=dgelu, bias=bias)
         return y, dgelu
-    kernels().gemm_bf16(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c, bias=bias)
+    kernels().gemm_bf16(x2, w, y, 0, 0, EPI_BF16, M, N, K, K, K, N, 1, c | (256 if nt_out else 0), bias=bias)
     return y
 
 

@@ -298,24 +298,10 @@ class LMHeadLossFn(torch.autograd.Function):
         N = h2.shape[0]
         rows = torch.empty(N, device=h.device, dtype=torch.float32)
         tg = _c(targets.reshape(-1).long())
-        chunk = _LMHEAD_CHUNK
-        if chunk and N > chunk:
-            # token chunks: each chunk's bf16 logits (chunk x Vp x 2 B, e.g. 206 MB at 2048 tokens) are
-            # consumed by the cross-entropy right after the GEMM wrote them, while they still sit in
-            # the 256 MB Infinity Cache, instead of one 1.65 GB write followed by a read from HBM
-            logits = torch.empty(N, w.shape[0], device=h.device, dtype=torch.bfloat16)
-            cfg = G.pick("fprop", N, w.shape[0], C)[0]
-            for s0 in range(0, N, chunk):
-                s1 = min(N, s0 + chunk)
-                if _LMHEAD_LIB:
-                    torch.matmul(h2[s0:s1], w.t(), out=logits[s0:s1])
-                else:
-                    G.fprop(h2[s0:s1], w, out=logits[s0:s1], cfg=cfg)
-                kernels().xent_bf16(logits[s0:s1], tg[s0:s1], V, 1.0 / N, rows[s0:s1], True)
-        else:
-            # [N, Vp] bf16: own MFMA GEMM, or the library for this plain GEMM (PDE_LMHEAD_GEMM=lib)
-            logits = torch.matmul(h2, w.t()) if _LMHEAD_LIB else G.fprop(h2, w)
-            kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
+        # [N, Vp] bf16 logits on the own persistent GEMM; 1.65 GB at GPT-2 shapes, stored non-temporally
+        # (read back once, by the cross-entropy right after) so they do not evict the operand tiles
+        logits = G.fprop(h2, w, nt_out=True)
+        kernels().xent_bf16(logits, tg, V, 1.0 / N, rows, True)
         tot = torch.empty(1, device=h.device, dtype=torch.float32)
         kernels().sum_f32(rows, tot, 1.0 / N)               # mean loss, no separate divide
         ctx.save_for_backward(h2, w, logits)
@@ -333,34 +319,11 @@ class LMHeadLossFn(torch.autograd.Function):
         gs = g.reshape(1)
         if gs.dtype != torch.float32 or not gs.is_cuda:
             gs = gs.to(device=dlogits.device, dtype=torch.float32)
-        if _LMHEAD_LIB_D:
-            dh = torch.matmul(dlogits, w)                    # plain library GEMM, then the loss-gradient
-            kernels().scale_bf16(dh, gs)                     # scale (device scalar, vectorised, in place)
-        else:
-            dh = G.dgrad(dlogits, w, scale=gs)               # [N, C]
-        if _LMHEAD_LIB_W:
-            slot = _grad_out(w)
-            dw = torch.matmul(dlogits.t(), h2, out=slot) if slot is not None else torch.matmul(dlogits.t(), h2)
-            kernels().scale_bf16(dw, gs)
-        else:
-            dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
+        dh = G.dgrad(dlogits, w, scale=gs)                   # [N, C], loss-gradient scale in the epilogue
+        dw, _ = G.wgrad(dlogits, h2, dw=_grad_out(w), scale=gs)   # [Vp, C]
         if ctx.tied is not None:
             ctx.tied["dw"] = dw                              # the tied embedding adds its part in place
         return dh.reshape(ctx.hshape), dw, None, None
-
-
-# PDE_LMHEAD_CHUNK=<tokens>: run the LM-head GEMM + cross-entropy in token chunks (0 = one pass)
-import os as _os
-_LMHEAD_CHUNK = int(_os.environ.get("PDE_LMHEAD_CHUNK", "0"))
-# The LM head's fprop / dgrad are plain GEMMs (no epilogue to fuse: the cross-entropy needs whole rows):
-# the fprop runs through hipBLASLt, faster on MI355X (in-step, one box: 886 vs 864 K tok/s with both on
-# the library, profiles/r4_gpt2/); the dgrad on the own 8-phase GEMM with the loss-gradient scale in its
-# epilogue (1027 vs 1057 + 9.5 us, profiles/r4_gemm/).  PDE_LMHEAD_GEMM=lib puts the dgrad on the library
-# too, =own keeps both on the framework's GEMM, =lib3 also moves the wgrad.
-_LMHEAD_MODE = _os.environ.get("PDE_LMHEAD_GEMM", "mixed")
-_LMHEAD_LIB = _LMHEAD_MODE in ("lib", "lib3", "mixed")       # fprop on hipBLASLt
-_LMHEAD_LIB_D = _LMHEAD_MODE in ("lib", "lib3")               # dgrad too ("mixed": the own 8-phase dgrad)
-_LMHEAD_LIB_W = _LMHEAD_MODE == "lib3"
 
 
 def lm_head_loss(h, w, targets, V: int):

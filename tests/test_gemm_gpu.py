@@ -10,7 +10,7 @@ from pytorch_distributed_example_amd.ops import gemm as G
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
-CFGS = list(range(22))
+CFGS = list(range(23))
 
 
 def rel_err(a, b):
@@ -25,11 +25,11 @@ def _bf(*shape, scale=1.0, seed=0):
 
 def test_tiles_and_cfgs():
     K = kernels()
-    assert K.gemm_num_cfgs() == 22
+    assert K.gemm_num_cfgs() == 23
     assert [tuple(K.gemm_tile(c)) for c in CFGS] == [(256, 192), (256, 128), (128, 128), (256, 256), (128, 128),
                                                      (256, 256), (256, 192), (256, 128), (128, 128), (256, 192),
                                                      (256, 192), (256, 256), (256, 256), (256, 128), (256, 192),
-                                                     (256, 256), (256, 192), (256, 256), (256, 256), (256, 256), (256, 256), (256, 192)]
+                                                     (256, 256), (256, 192), (256, 256), (256, 256), (256, 256), (256, 256), (256, 192), (256, 192)]
     assert K.gemm_splits(16384, 8) == 8 and K.gemm_splits(192, 8) == 3
 
 
@@ -237,15 +237,25 @@ def test_gemm8pc_continuous_bit_identical(M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (16384, 2304, 768), (5000, 776, 256), (300, 200, 128)])
 def test_gemm8pc_192_bit_identical(M, N, K):
+    _check_192(M, N, K, 21)
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (16384, 2304, 768), (5000, 776, 256), (300, 200, 64)])
+def test_gemm8p_192_bit_identical(M, N, K):
+    """cfg 22: the one-shot 8-phase loop at 256 x 192 (one tile per block, LDS epilogue)."""
+    _check_192(M, N, K, 22)
+
+
+def _check_192(M, N, K, cfg):
     """cfg 21: the continuous 8-phase stream at 256 x 192 (waves of 128 x 48: one-instruction B1 region,
     7 instructions in flight, an unpaired third n-block stored 8 bytes per lane): bit-identical to the
     16x16x32 loop at the same tile (cfg 16) for bias and bias + GELU fprops; dgrad falls back to cfg 16."""
     x, w, b = _bf(M, K, seed=70), _bf(N, K, scale=0.03, seed=71), _bf(N, seed=72)
-    y = G.fprop(x, w, b, cfg=21)
+    y = G.fprop(x, w, b, cfg=cfg)
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
     assert torch.equal(y, G.fprop(x, w, b, cfg=16))
-    a21, d21 = G.fprop(x, w, b, gelu=True, cfg=21)
+    a21, d21 = G.fprop(x, w, b, gelu=True, cfg=cfg)
     a16, d16 = G.fprop(x, w, b, gelu=True, cfg=16)
     assert torch.equal(a21, a16) and torch.equal(d21, d16)
     dy, w2 = _bf(M, K, seed=73), _bf(K, N, scale=0.03, seed=74)
-    assert torch.equal(G.dgrad(dy, w2, cfg=21), G.dgrad(dy, w2, cfg=16))
+    assert torch.equal(G.dgrad(dy, w2, cfg=cfg), G.dgrad(dy, w2, cfg=16))
