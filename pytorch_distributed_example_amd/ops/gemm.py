@@ -52,13 +52,14 @@ _TILE_EFF = {0: 1.0, 1: 0.93, 2: 0.8, 3: 1.0, 4: 0.85, 5: 0.9, 6: 0.9, 7: 0.85, 
 #   wgrad:         (kind, M, N) -> (cfg, splits at 16384 tokens; scaled with the token count)
 _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
     # round 5 (profiles/r5_gemm/, profiles/r5_gpt2/): every GPT-2 GEMM on the framework's kernels, no
-    # library fallback -- the 8-phase loop at 256x192 (cfg 22) for the N = 768 output projections and
-    # c_attn (one tile round on 256 CUs, on par with or ahead of hipBLASLt), the persistent 8-phase loop
+    # library fallback -- the 8-phase loop at 256x192 (cfg 22) for the N = 768 output projections (one
+    # tile round on 256 CUs, on par with hipBLASLt), the 16x16x32 loop at 256x192 (cfg 16) for c_attn
+    # (12 column tiles: 3 exact rounds), the persistent 8-phase loop
     # (cfg 19) for the GELU fprop, the GELU-backward dgrad and the LM head (whose fprop stores the 1.65 GB
     # of logits non-temporally: within 3 % of hipBLASLt, 12 % faster than plain stores)
-    ("fprop", 2304, 768): (22, 1), ("fprop", 768, 768): (22, 1), ("fprop", 3072, 768): (19, 1),
+    ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (22, 1), ("fprop", 3072, 768): (19, 1),
     ("fprop", 768, 3072): (22, 1), ("fprop", 50304, 768): (19, 1),
-    ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (9, 1),
+    ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (19, 1),
     ("dgrad", 3072, 768): (19, 1), ("dgrad", 768, 50304): (19, 1),
     # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/; 256x256 tiles
     # for cfg 18: 36 tiles x 7, 27 x 9)
