@@ -113,7 +113,8 @@ class PeerAllReduce {
   uint8_t* peer_flags_[kPeerMaxRanks] = {};
   uint8_t* ipflags_ = nullptr;                  // own in-place flag region (uncached): [3][blocks][ranks] u32
   uint8_t* peer_ipflags_[kPeerMaxRanks] = {};
-  uint32_t* ipctrl_ = nullptr;                  // in-place calls: [0] call counter, [1] done counter
+  uint32_t* ipctrl_ = nullptr;                  // in-place calls: call counter per block index
+  int ip_vpt_ = 2;                              // one-shot vectors per thread (PDE_PEER_IP_VPT; 2 measured best)
   struct Reg {
     uint8_t* base[kPeerMaxRanks] = {};          // every rank's registered buffer, mapped here ([rank] = own)
     uint8_t* mapped[kPeerMaxRanks] = {};        // what hipIpcOpenMemHandle returned (closed in close())

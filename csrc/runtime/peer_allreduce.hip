@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -346,11 +347,16 @@ __device__ __forceinline__ void ip_barrier(const IpArgs& a, int phase, uint32_t 
   __syncthreads();
 }
 
-template <int W, bool TWO>
+// Call numbers are per block index (ctrl[b]): block b of every rank runs in the same calls (same
+// sizes on every rank), so its count agrees across ranks without a grid-wide "last block" atomic --
+// the former ctrl[1] done counter serialised every block's exit on one uncached address.  (The
+// staged protocol keeps its global counter: its stage parity must flip for ALL blocks between calls
+// whose grids differ.)  U: 16-byte vectors per thread in the one-shot form (held across barrier B).
+template <int W, bool TWO, int U>
 __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
   __shared__ uint32_t s_call, s_bad;
   if (threadIdx.x == 0) {
-    s_call = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_call = __hip_atomic_load(a.ctrl + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_bad = __hip_atomic_load(a.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
@@ -374,16 +380,28 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
           __builtin_amdgcn_raw_buffer_load_b32(rs[p], (int)((tail_off + threadIdx.x) * 4), 0, kAuxSys));
   }
   if (!TWO) {
-    const bool have = t0 < a.n4;                        // host guarantees gridDim * kThreads >= n4
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    vec_t v[W];
+    // host guarantees gridDim * kThreads * U >= n4
+    float acc[U][4];
+    vec_t v[U][W];
 #pragma unroll
-    for (int p = 0; p < W; ++p) v[p] = ld_sys(rs[p], have ? t0 : 0);
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = t0 + u * stride;
 #pragma unroll
-    for (int p = 0; p < W; ++p) F32Op::add(acc, v[p]);  // fixed rank order: bit-identical on every rank
+      for (int p = 0; p < W; ++p) v[u][p] = ld_sys(rs[p], i < a.n4 ? i : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[u][0] = acc[u][1] = acc[u][2] = acc[u][3] = 0.f;
+#pragma unroll
+      for (int p = 0; p < W; ++p) F32Op::add(acc[u], v[u][p]);  // fixed rank order: bit-identical on every rank
+    }
     ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every rank has read every buffer
     const bool bad = s_bad != 0;
-    if (have) reinterpret_cast<vec_t*>(own)[t0] = bad ? F32Op::nan_vec() : F32Op::pack(acc, a.scale);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = t0 + u * stride;
+      if (i < a.n4) reinterpret_cast<vec_t*>(own)[i] = bad ? F32Op::nan_vec() : F32Op::pack(acc[u], a.scale);
+    }
     if (tail_lane) own[tail_off + threadIdx.x] = bad ? __builtin_nanf("") : tail_sum * a.scale;
   } else {
     // reduce-scatter: my chunk from every rank, written through into my own buffer
@@ -420,20 +438,14 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
     }
     ip_barrier<W>(a, 2, target, failed, &s_bad);        // C: every rank has gathered from every owner
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(a.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-      __hip_atomic_store(a.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.ctrl, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.ctrl + blockIdx.x, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool TWO>
+template <bool TWO, int U>
 void ip_launch(int world, const IpArgs& a, int nb, hipStream_t s) {
   switch (world) {
 #define PDE_IP_CASE(W) \
-    case W: hipLaunchKernelGGL((peer_inplace_kernel<W, TWO>), dim3(nb), dim3(kThreads), 0, s, a); break;
+    case W: hipLaunchKernelGGL((peer_inplace_kernel<W, TWO, U>), dim3(nb), dim3(kThreads), 0, s, a); break;
     PDE_IP_CASE(1) PDE_IP_CASE(2) PDE_IP_CASE(3) PDE_IP_CASE(4) PDE_IP_CASE(5) PDE_IP_CASE(6) PDE_IP_CASE(7)
     PDE_IP_CASE(8)
 #undef PDE_IP_CASE
@@ -501,9 +513,10 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_b
   ipflags_ = static_cast<uint8_t*>(ipf);
   hip_check(hipMemset(ipflags_, 0, kFlagBytes), "hipMemset");
   void* ipc = nullptr;
-  hip_check(hipExtMallocWithFlags(&ipc, 256, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipctrl)");
+  hip_check(hipExtMallocWithFlags(&ipc, kPeerMaxBlocks * 4, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipctrl)");
   ipctrl_ = static_cast<uint32_t*>(ipc);
-  hip_check(hipMemset(ipctrl_, 0, 256), "hipMemset");
+  if (const char* e = std::getenv("PDE_PEER_IP_VPT")) ip_vpt_ = std::atoi(e) < 1 ? 1 : std::atoi(e);
+  hip_check(hipMemset(ipctrl_, 0, kPeerMaxBlocks * 4), "hipMemset");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_[rank_] = region_;
   peer_flags_[rank_] = flags_;
@@ -745,18 +758,30 @@ void PeerAllReduce::all_reduce_registered_f32(int id, int64_t off, int64_t count
   a.timeout = timeout_ticks_;
   a.scale = scale;
   a.rank = rank_;
-  constexpr int64_t kOneShotMaxVec = (int64_t)kPeerMaxBlocks * kThreads;   // sums held in registers across B
+  // one-shot: U vectors per thread held across barrier B; U > 1 trades flag traffic (one barrier pair
+  // per block) for a longer per-thread load chain
+  const int64_t u_max = ip_vpt_;
+  const int64_t one_shot_max_vec = (int64_t)kPeerMaxBlocks * kThreads * 4;
   bool two = algo == 2 || (algo == 0 && world_ > 2 && count * 4 > one_shot_max_);
-  if (!two && a.n4 > kOneShotMaxVec) {
-    if (algo == 1) throw std::invalid_argument("in-place one-shot holds at most 2 MB per call");
+  if (!two && a.n4 > one_shot_max_vec) {
+    if (algo == 1) throw std::invalid_argument("in-place one-shot holds at most 8 MB per call");
     two = true;
   }
   a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
-  int64_t nb = ((two ? a.chunk4 : a.n4) + kThreads - 1) / kThreads;
-  nb = nb < 1 ? 1 : (nb > kPeerMaxBlocks ? kPeerMaxBlocks : nb);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (two) ip_launch<true>(world_, a, (int)nb, s);
-  else ip_launch<false>(world_, a, (int)nb, s);
+  if (two) {
+    int64_t nb = (a.chunk4 + kThreads - 1) / kThreads;
+    nb = nb < 1 ? 1 : (nb > kPeerMaxBlocks ? kPeerMaxBlocks : nb);
+    ip_launch<true, 1>(world_, a, (int)nb, s);
+  } else {
+    int64_t u = 1;
+    while (u < 4 && (u < u_max || a.n4 > (int64_t)kPeerMaxBlocks * kThreads * u)) u *= 2;
+    int64_t nb = (a.n4 + kThreads * u - 1) / (kThreads * u);
+    nb = nb < 1 ? 1 : nb;
+    if (u == 1) ip_launch<false, 1>(world_, a, (int)nb, s);
+    else if (u == 2) ip_launch<false, 2>(world_, a, (int)nb, s);
+    else ip_launch<false, 4>(world_, a, (int)nb, s);
+  }
   hip_check(hipGetLastError(), "peer in-place all-reduce launch");
 }
 
