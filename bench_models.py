@@ -80,6 +80,7 @@ def _tune(ddp, step, world, args, restore=None) -> dict:
     else:
         out["bucket_mb"] = float(args.bucket_mb)
     out["grad_reduce_route"] = ddp.reduce_route
+    out["peer_inplace"] = bool(getattr(ddp, "peer_inplace", False))
     out["grad_reduce_dtype"] = str(ddp.reduce_dtype or "param dtype").replace("torch.", "")
     out["grad_allreduce_bytes_per_step"] = ddp.wire_bytes_per_step()
     out["n_buckets"] = len(ddp.buckets)

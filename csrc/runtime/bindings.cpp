@@ -240,6 +240,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("all_reduce_registered_f32", &PeerAllReduce::all_reduce_registered_f32, py::arg("id"), py::arg("off"),
            py::arg("count"), py::arg("scale"), py::arg("algo"), py::arg("stream"),
            py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_registered", &PeerAllReduce::all_reduce_registered, py::arg("id"), py::arg("off"),
+           py::arg("count"), py::arg("esz"), py::arg("scale"), py::arg("algo"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
       .def("registered_bytes", &PeerAllReduce::registered_bytes)
       .def("debug_skip_stage", &PeerAllReduce::debug_skip_stage)
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())

@@ -92,8 +92,10 @@ class PeerAllReduce {
   // `id` (the same on every rank when every rank registers in the same order).
   std::string register_buffer(uintptr_t ptr, int64_t bytes, int* id);
   void open_registered(int id, const std::vector<std::string>& handles);
-  // buf[off, off + count) of registration `id` = scale * sum over ranks, in place.  algo: 1 one-shot
-  // (count <= 2 MB of fp32), 2 two-shot, 0 auto.
+  // buf[off, off + count) of registration `id` = scale * sum over ranks, in place (elements of esz
+  // bytes: 4 fp32, 2 bf16 with fp32 accumulation and one rounding).  algo: 1 one-shot (<= 8 MB),
+  // 2 two-shot, 0 auto.
+  void all_reduce_registered(int id, int64_t off, int64_t count, int esz, float scale, int algo, uintptr_t stream);
   void all_reduce_registered_f32(int id, int64_t off, int64_t count, float scale, int algo, uintptr_t stream);
   int64_t registered_bytes(int id) const;
   void close();
@@ -111,9 +113,9 @@ class PeerAllReduce {
   uint32_t* err_dev_ = nullptr;             // its device address
   uint8_t* peers_[kPeerMaxRanks] = {};
   uint8_t* peer_flags_[kPeerMaxRanks] = {};
-  uint8_t* ipflags_ = nullptr;                  // own in-place flag region (uncached): [3][blocks][ranks] u32
+  uint8_t* ipflags_ = nullptr;                  // own in-place flag region (uncached): [3][blocks][ranks] u32;
+                                                // phase 0 slots count the calls (see peer_inplace_kernel)
   uint8_t* peer_ipflags_[kPeerMaxRanks] = {};
-  uint32_t* ipctrl_ = nullptr;                  // in-place calls: call counter per block index
   int ip_vpt_ = 2;                              // one-shot vectors per thread (PDE_PEER_IP_VPT; 2 measured best)
   struct Reg {
     uint8_t* base[kPeerMaxRanks] = {};          // every rank's registered buffer, mapped here ([rank] = own)

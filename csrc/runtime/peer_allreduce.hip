@@ -296,7 +296,6 @@ __global__ void __launch_bounds__(kThreads) peer_dev_probe_kernel(PeerDev d, con
 struct IpArgs {
   uint8_t* data[kPeerMaxRanks];    // every rank's buffer at this call's first element (mapped here)
   uint8_t* flags[kPeerMaxRanks];   // every rank's in-place flag region
-  uint32_t* ctrl;                  // [0] calls, [1] blocks done
   uint32_t* errc;                  // the staged protocol's ctrl: [2] = time-out count (shared latch)
   uint32_t* err_host;
   int64_t n4, tail, chunk4, bytes;
@@ -320,14 +319,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ip_rsrc(const uint8_t* p, int6
 // consumed, write-through stores acknowledged), then lane t < W stores the call number into rank t's
 // slot for this rank and waits for rank t's store into ours (relaxed system-scope accesses to
 // uncached memory).  A time-out poisons the call (NaN results) and latches the error words.
-template <int W>
+// SKIP_OWN: this rank's own slot is known to hold `target` already (barrier A's signal is an atomic
+// add whose return value this block waited for) -- no poll of it.
+template <int W, bool SIGNAL = true, bool SKIP_OWN = false>
 __device__ __forceinline__ void ip_barrier(const IpArgs& a, int phase, uint32_t target, bool failed, uint32_t* bad) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (SIGNAL) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   const int t = threadIdx.x;
-  if (t < W) {
-    __hip_atomic_store(ip_flag(a.flags[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < W && !(SKIP_OWN && t == a.rank)) {
+    if constexpr (SIGNAL)
+      __hip_atomic_store(ip_flag(a.flags[t], phase, blockIdx.x, a.rank), target, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = ip_flag(a.flags[a.rank], phase, blockIdx.x, t);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int spins = 0;
@@ -347,19 +351,28 @@ __device__ __forceinline__ void ip_barrier(const IpArgs& a, int phase, uint32_t 
   __syncthreads();
 }
 
-// Call numbers are per block index (ctrl[b]): block b of every rank runs in the same calls (same
-// sizes on every rank), so its count agrees across ranks without a grid-wide "last block" atomic --
-// the former ctrl[1] done counter serialised every block's exit on one uncached address.  (The
+// Call numbers are per block index: block b of every rank runs in the same calls (same sizes on every
+// rank), so its count agrees across ranks with no grid-wide "last block" atomic (the former done
+// counter serialised every block's exit on one uncached address).  The count lives in barrier A's
+// own flag slots: at the start lane t < W adds 1 to this rank's slot in rank t's region -- the arrival
+// signal -- and the add on this rank's OWN region returns the calls so far, so no separate counter
+// load precedes the signal (one memory round trip less per call; the remote adds are posted).  (The
 // staged protocol keeps its global counter: its stage parity must flip for ALL blocks between calls
 // whose grids differ.)  U: 16-byte vectors per thread in the one-shot form (held across barrier B).
-template <int W, bool TWO, int U>
+template <int W, bool TWO, int U, typename Op>
 __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
   __shared__ uint32_t s_call, s_bad;
-  if (threadIdx.x == 0) {
-    s_call = __hip_atomic_load(a.ctrl + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_bad = __hip_atomic_load(a.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    const int t = threadIdx.x;
+    if (t < W) {
+      uint32_t* slot = ip_flag(a.flags[t], 0, blockIdx.x, a.rank);
+      if (t == a.rank) s_call = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else (void)__hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (t == 64) s_bad = __hip_atomic_load(a.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  constexpr int ESZ = 16 / Op::kPerVec;                  // element bytes (4: fp32, 2: bf16)
   const uint32_t target = s_call + 1u;
   const bool failed = s_bad != 0;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
@@ -367,21 +380,25 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
   __amdgpu_buffer_rsrc_t rs[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) rs[p] = ip_rsrc(a.data[p], a.bytes);
-  float* own = reinterpret_cast<float*>(a.data[a.rank]);
-  const int64_t tail_off = a.n4 * 4;
+  uint8_t* own = a.data[a.rank];
+  const int64_t tail_off = a.n4 * Op::kPerVec;           // first trailing element
   const bool tail_lane = blockIdx.x == 0 && threadIdx.x < a.tail;
   float tail_sum = 0.f;
 
-  ip_barrier<W>(a, 0, target, failed, &s_bad);          // A: every rank's buffer holds its input
+  ip_barrier<W, false, true>(a, 0, target, failed, &s_bad);   // A: every rank's buffer holds its input
   if (tail_lane) {                                      // trailing elements: read now, written after B
+    const int tb = (int)((tail_off + threadIdx.x) * ESZ);
 #pragma unroll
-    for (int p = 0; p < W; ++p)
-      tail_sum += __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(rs[p], (int)((tail_off + threadIdx.x) * 4), 0, kAuxSys));
+    for (int p = 0; p < W; ++p) {
+      if constexpr (ESZ == 4)
+        tail_sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs[p], tb, 0, kAuxSys));
+      else
+        tail_sum += __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs[p], tb, 0, kAuxSys) << 16);
+    }
   }
   if (!TWO) {
     // host guarantees gridDim * kThreads * U >= n4
-    float acc[U][4];
+    float acc[U][Op::kAcc];
     vec_t v[U][W];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -391,66 +408,94 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc[u][0] = acc[u][1] = acc[u][2] = acc[u][3] = 0.f;
+      Op::zero(acc[u]);
 #pragma unroll
-      for (int p = 0; p < W; ++p) F32Op::add(acc[u], v[u][p]);  // fixed rank order: bit-identical on every rank
+      for (int p = 0; p < W; ++p) Op::add(acc[u], v[u][p]);  // fixed rank order: bit-identical on every rank
     }
     ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every rank has read every buffer
     const bool bad = s_bad != 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = t0 + u * stride;
-      if (i < a.n4) reinterpret_cast<vec_t*>(own)[i] = bad ? F32Op::nan_vec() : F32Op::pack(acc[u], a.scale);
+      if (i < a.n4) reinterpret_cast<vec_t*>(own)[i] = bad ? Op::nan_vec() : Op::pack(acc[u], a.scale);
     }
-    if (tail_lane) own[tail_off + threadIdx.x] = bad ? __builtin_nanf("") : tail_sum * a.scale;
+    if (tail_lane) Op::tail_store(own, tail_off + threadIdx.x, bad ? __builtin_nanf("") : tail_sum * a.scale);
   } else {
     // reduce-scatter: my chunk from every rank, written through into my own buffer
     const int64_t lo = (int64_t)a.rank * a.chunk4;
     const int64_t len = lo + a.chunk4 <= a.n4 ? a.chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
     const __amdgpu_buffer_rsrc_t ro = rs[a.rank];
-    for (int64_t i = t0; i < len; i += stride) {
-      vec_t v[W];
+    // R vectors per thread per iteration: R * W uncached loads in flight (one per iteration was
+    // latency-bound: ~0.75 TB/s on a 248 MB GPT-2 gradient at W = 1)
+    constexpr int R = W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    for (int64_t i0 = t0; i0 < len; i0 += R * stride) {
+      vec_t v[R][W];
 #pragma unroll
-      for (int p = 0; p < W; ++p) v[p] = ld_sys(rs[p], lo + i);
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < R; ++r) {
+        const int64_t i = i0 + r * stride;
 #pragma unroll
-      for (int p = 0; p < W; ++p) F32Op::add(acc, v[p]);
-      const vec_t r = s_bad ? F32Op::nan_vec() : F32Op::pack(acc, a.scale);
-      __builtin_amdgcn_raw_buffer_store_b128(r, ro, (int)((lo + i) * 16), 0, kAuxSys);
+        for (int p = 0; p < W; ++p) v[r][p] = ld_sys(rs[p], lo + (i < len ? i : i0));
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int64_t i = i0 + r * stride;
+        float acc[Op::kAcc];
+        Op::zero(acc);
+#pragma unroll
+        for (int p = 0; p < W; ++p) Op::add(acc, v[r][p]);
+        const vec_t o = s_bad ? Op::nan_vec() : Op::pack(acc, a.scale);
+        if (i < len) __builtin_amdgcn_raw_buffer_store_b128(o, ro, (int)((lo + i) * 16), 0, kAuxSys);
+      }
     }
     ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every chunk reduced, every input read
     const bool bad = s_bad != 0;
-    if (tail_lane) own[tail_off + threadIdx.x] = bad ? __builtin_nanf("") : tail_sum * a.scale;
+    if (tail_lane) Op::tail_store(own, tail_off + threadIdx.x, bad ? __builtin_nanf("") : tail_sum * a.scale);
     // all-gather: chunk q from its owner q (W-1 loads in flight per lane)
     const int64_t last = a.n4 - 1;
-    for (int64_t i = t0; i < a.chunk4; i += stride) {
-      vec_t v[W];
+    constexpr int RG = W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    for (int64_t i0 = t0; i0 < a.chunk4; i0 += RG * stride) {
+      vec_t v[RG][W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) {
-        const int64_t g = (int64_t)q * a.chunk4 + i;
-        v[q] = (q == a.rank) ? vec_t{0u, 0u, 0u, 0u} : ld_sys(rs[q], g < last ? g : last);
+      for (int r = 0; r < RG; ++r) {
+        const int64_t i = i0 + r * stride;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const int64_t g = (int64_t)q * a.chunk4 + i;
+          v[r][q] = (q == a.rank) ? vec_t{0u, 0u, 0u, 0u} : ld_sys(rs[q], g < last ? g : last);
+        }
       }
 #pragma unroll
-      for (int q = 0; q < W; ++q) {
-        const int64_t g = (int64_t)q * a.chunk4 + i;
-        if (q != a.rank && g <= last) reinterpret_cast<vec_t*>(own)[g] = bad ? F32Op::nan_vec() : v[q];
+      for (int r = 0; r < RG; ++r) {
+        const int64_t i = i0 + r * stride;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const int64_t g = (int64_t)q * a.chunk4 + i;
+          if (q != a.rank && i < a.chunk4 && g <= last) reinterpret_cast<vec_t*>(own)[g] = bad ? Op::nan_vec() : v[r][q];
+        }
       }
     }
     ip_barrier<W>(a, 2, target, failed, &s_bad);        // C: every rank has gathered from every owner
   }
-  if (threadIdx.x == 0) __hip_atomic_store(a.ctrl + blockIdx.x, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool TWO, int U>
+template <bool TWO, int U, typename Op>
 void ip_launch(int world, const IpArgs& a, int nb, hipStream_t s) {
   switch (world) {
 #define PDE_IP_CASE(W) \
-    case W: hipLaunchKernelGGL((peer_inplace_kernel<W, TWO, U>), dim3(nb), dim3(kThreads), 0, s, a); break;
+    case W: hipLaunchKernelGGL((peer_inplace_kernel<W, TWO, U, Op>), dim3(nb), dim3(kThreads), 0, s, a); break;
     PDE_IP_CASE(1) PDE_IP_CASE(2) PDE_IP_CASE(3) PDE_IP_CASE(4) PDE_IP_CASE(5) PDE_IP_CASE(6) PDE_IP_CASE(7)
     PDE_IP_CASE(8)
 #undef PDE_IP_CASE
     default: throw std::invalid_argument("peer all-reduce supports 1..8 ranks");
   }
+}
+
+template <typename Op>
+void ip_dispatch(int world, const IpArgs& a, bool two, int64_t u, int nb, hipStream_t s) {
+  if (two) ip_launch<true, 1, Op>(world, a, nb, s);
+  else if (u == 1) ip_launch<false, 1, Op>(world, a, nb, s);
+  else if (u == 2) ip_launch<false, 2, Op>(world, a, nb, s);
+  else ip_launch<false, 4, Op>(world, a, nb, s);
 }
 
 
@@ -512,11 +557,7 @@ PeerAllReduce::PeerAllReduce(int rank, int world, int device, int64_t capacity_b
   hip_check(hipExtMallocWithFlags(&ipf, kFlagBytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipflags)");
   ipflags_ = static_cast<uint8_t*>(ipf);
   hip_check(hipMemset(ipflags_, 0, kFlagBytes), "hipMemset");
-  void* ipc = nullptr;
-  hip_check(hipExtMallocWithFlags(&ipc, kPeerMaxBlocks * 4, hipDeviceMallocUncached), "hipExtMallocWithFlags(ipctrl)");
-  ipctrl_ = static_cast<uint32_t*>(ipc);
   if (const char* e = std::getenv("PDE_PEER_IP_VPT")) ip_vpt_ = std::atoi(e) < 1 ? 1 : std::atoi(e);
-  hip_check(hipMemset(ipctrl_, 0, kPeerMaxBlocks * 4), "hipMemset");
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   peers_[rank_] = region_;
   peer_flags_[rank_] = flags_;
@@ -547,9 +588,7 @@ void PeerAllReduce::close() {
   for (auto& q : peer_flags_) q = nullptr;
   for (auto& q : peer_ipflags_) q = nullptr;
   (void)hipFree(ipflags_);
-  (void)hipFree(ipctrl_);
   ipflags_ = nullptr;
-  ipctrl_ = nullptr;
   (void)hipFree(region_);
   (void)hipFree(flags_);
   (void)hipFree(ctrl_);
@@ -739,22 +778,28 @@ int64_t PeerAllReduce::registered_bytes(int id) const {
 
 void PeerAllReduce::all_reduce_registered_f32(int id, int64_t off, int64_t count, float scale, int algo,
                                               uintptr_t stream) {
+  all_reduce_registered(id, off, count, 4, scale, algo, stream);
+}
+
+void PeerAllReduce::all_reduce_registered(int id, int64_t off, int64_t count, int esz, float scale, int algo,
+                                          uintptr_t stream) {
   if (id < 0 || id >= (int)regs_.size() || !regs_[id].open) throw std::runtime_error("registration not open");
+  if (esz != 4 && esz != 2) throw std::invalid_argument("in-place all-reduce: fp32 (4) or bf16 (2) elements");
   const Reg& r = regs_[id];
   if (count <= 0) return;
-  if (off < 0 || (off + count) * 4 > r.bytes) throw std::invalid_argument("range outside the registered buffer");
-  if (off & 3) throw std::invalid_argument("in-place range must start 16-byte aligned");
+  if (off < 0 || (off + count) * esz > r.bytes) throw std::invalid_argument("range outside the registered buffer");
+  if ((off * esz) & 15) throw std::invalid_argument("in-place range must start 16-byte aligned");
+  const int per = 16 / esz;
   IpArgs a{};
   for (int p = 0; p < world_; ++p) {
-    a.data[p] = r.base[p] + off * 4;
+    a.data[p] = r.base[p] + off * esz;
     a.flags[p] = peer_ipflags_[p];
   }
-  a.ctrl = ipctrl_;
   a.errc = ctrl_;
   a.err_host = err_dev_;
-  a.n4 = count / 4;
-  a.tail = count - a.n4 * 4;
-  a.bytes = count * 4;
+  a.n4 = count / per;
+  a.tail = count - a.n4 * per;
+  a.bytes = count * esz;
   a.timeout = timeout_ticks_;
   a.scale = scale;
   a.rank = rank_;
@@ -762,26 +807,27 @@ void PeerAllReduce::all_reduce_registered_f32(int id, int64_t off, int64_t count
   // per block) for a longer per-thread load chain
   const int64_t u_max = ip_vpt_;
   const int64_t one_shot_max_vec = (int64_t)kPeerMaxBlocks * kThreads * 4;
-  bool two = algo == 2 || (algo == 0 && world_ > 2 && count * 4 > one_shot_max_);
+  bool two = algo == 2 || (algo == 0 && world_ > 2 && count * esz > one_shot_max_);
   if (!two && a.n4 > one_shot_max_vec) {
     if (algo == 1) throw std::invalid_argument("in-place one-shot holds at most 8 MB per call");
     two = true;
   }
   a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int64_t u = 1, nb;
   if (two) {
-    int64_t nb = (a.chunk4 + kThreads - 1) / kThreads;
-    nb = nb < 1 ? 1 : (nb > kPeerMaxBlocks ? kPeerMaxBlocks : nb);
-    ip_launch<true, 1>(world_, a, (int)nb, s);
+    // capped like the staged path (64 blocks by default): the two-shot is link-bound well below that,
+    // and spinning blocks on every CU starve a peer's full-LDS kernels when ranks share a GPU (a
+    // ResNet-18 DDP step deadlocked that way with 256 blocks)
+    nb = (a.chunk4 + kThreads - 1) / kThreads;
+    nb = nb < 1 ? 1 : (nb > max_blocks_ ? max_blocks_ : nb);
   } else {
-    int64_t u = 1;
     while (u < 4 && (u < u_max || a.n4 > (int64_t)kPeerMaxBlocks * kThreads * u)) u *= 2;
-    int64_t nb = (a.n4 + kThreads * u - 1) / (kThreads * u);
+    nb = (a.n4 + kThreads * u - 1) / (kThreads * u);
     nb = nb < 1 ? 1 : nb;
-    if (u == 1) ip_launch<false, 1>(world_, a, (int)nb, s);
-    else if (u == 2) ip_launch<false, 2>(world_, a, (int)nb, s);
-    else ip_launch<false, 4>(world_, a, (int)nb, s);
   }
+  if (esz == 4) ip_dispatch<F32Op>(world_, a, two, u, (int)nb, s);
+  else ip_dispatch<BF16Op>(world_, a, two, u, (int)nb, s);
   hip_check(hipGetLastError(), "peer in-place all-reduce launch");
 }
 

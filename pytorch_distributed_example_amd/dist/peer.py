@@ -47,6 +47,10 @@ def _host_allreduce_min(group, value: int) -> int:
     return int(t.item())
 
 
+_REG_DTYPES = (torch.float32, torch.bfloat16)
+_ONE_SHOT_MAX_BYTES = 256 * 512 * 4 * 16        # in-place one-shot: <= 4 vectors per thread, 256 blocks
+
+
 def _host_allreduce_max_f64(group, vals) -> list:
     t = torch.tensor(list(vals), dtype=torch.float64)
     group.host.allreduce(t.data_ptr(), t.numel(), 1, 3)   # float64, MAX
@@ -121,7 +125,7 @@ class PeerAllReduce:
             self.native = None
 
     def register(self, t: torch.Tensor, self_test: bool = True) -> bool:
-        """Collective: map every rank's ``t`` (contiguous fp32, the same size on every rank) so that
+        """Collective: map every rank's ``t`` (contiguous fp32 or bf16, the same size on every rank) so that
         ``all_reduce_`` of any 16-byte-aligned range of it runs in place.  False (on every rank) if any
         rank failed; the staged path stays available either way."""
         if not self.ok:
@@ -130,9 +134,9 @@ class PeerAllReduce:
         key = f"{self.group.prefix}/peer_reg/{_SEQ[0]}"
         err, rid = "", -1
         try:
-            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
-                raise ValueError("registered buffers are contiguous fp32 tensors on the rank's device")
-            rid, h = self.native.register_buffer(t.data_ptr(), t.numel() * 4)
+            if t.dtype not in _REG_DTYPES or not t.is_contiguous() or t.device != self.device:
+                raise ValueError("registered buffers are contiguous fp32 / bf16 tensors on the rank's device")
+            rid, h = self.native.register_buffer(t.data_ptr(), t.numel() * t.element_size())
             self.group.store.set(f"{key}/h{self.rank}", h)
         except Exception as e:   # noqa: BLE001
             err = f"register: {e}"
@@ -161,14 +165,14 @@ class PeerAllReduce:
         return True
 
     def registered_range(self, t: torch.Tensor):
-        """(registration id, element offset) if ``t`` is a 16-byte aligned fp32 range of a registered
-        buffer, else None."""
-        if t.dtype != torch.float32 or not t.is_contiguous():
+        """(registration id, element offset) if ``t`` is a 16-byte aligned range of a registered buffer
+        of its dtype, else None."""
+        if t.dtype not in _REG_DTYPES or not t.is_contiguous():
             return None
-        p = t.data_ptr()
-        for base, n, rid, _ in self._regs:
-            if base <= p and p + t.numel() * 4 <= base + n * 4 and (p - base) % 16 == 0:
-                return rid, (p - base) // 4
+        p, esz = t.data_ptr(), t.element_size()
+        for base, n, rid, buf in self._regs:
+            if buf.dtype == t.dtype and base <= p and p + t.numel() * esz <= base + n * esz and (p - base) % 16 == 0:
+                return rid, (p - base) // esz
         return None
 
     def _self_test_registered(self, buf: torch.Tensor, rid: int):
@@ -176,22 +180,24 @@ class PeerAllReduce:
         n_all = buf.numel()
         call = [0]
 
-        def data(n, rank, c):
+        esz, per = buf.element_size(), 16 // buf.element_size()
+
+        def data(n, rank, c):   # small integers: every sum is exact in bf16 too
             i = torch.arange(n, device=self.device, dtype=torch.int64)
-            return (((i * 7 + c * 13 + rank * 5) % 17) - 8).to(torch.float32)
+            return (((i * 7 + c * 13 + rank * 5) % 17) - 8).to(buf.dtype)
 
         s = torch.cuda.current_stream(self.device)
-        for n in sorted({1, 5, 4099, min(n_all, 70001), n_all - (n_all % 4)}):
+        for n in sorted({1, 5, 4099, min(n_all, 70001), n_all - (n_all % per)}):
             if n <= 0 or n > n_all:
                 continue
             for algo in (1, 2):
-                if algo == 1 and n > 256 * 512 * 4:
+                if algo == 1 and n * esz > _ONE_SHOT_MAX_BYTES:
                     continue
-                for off in (0, 4 * ((n_all - n) // 8)):      # two offsets inside the buffer
+                for off in (0, per * ((n_all - n) // (2 * per))):      # two offsets inside the buffer
                     c = call[0]
                     call[0] += 1
                     buf[off:off + n].copy_(data(n, r, c))
-                    self.native.all_reduce_registered_f32(rid, off, n, 1.0, algo, s.cuda_stream)
+                    self.native.all_reduce_registered(rid, off, n, esz, 1.0, algo, s.cuda_stream)
                     torch.cuda.synchronize(self.device)
                     if self.error():
                         raise RuntimeError(f"barrier time-out (algo {algo}, n={n}, off={off})")
@@ -218,9 +224,10 @@ class PeerAllReduce:
         a = _ALGO.get(algo, 0)
         reg = self.registered_range(t)
         if reg is not None:
-            if a == 1 and t.numel() > 256 * 512 * 4:     # one-shot holds <= 2 MB of sums: two-shot in place
+            if a == 1 and t.numel() * t.element_size() > _ONE_SHOT_MAX_BYTES:   # two-shot in place
                 a = 2
-            self.native.all_reduce_registered_f32(reg[0], reg[1], t.numel(), float(scale), a, s.cuda_stream)
+            self.native.all_reduce_registered(reg[0], reg[1], t.numel(), t.element_size(), float(scale), a,
+                                              s.cuda_stream)
             return
         fn = self.native.all_reduce_f32 if t.dtype == torch.float32 else self.native.all_reduce_bf16
         fn(t.data_ptr(), t.data_ptr(), t.numel(), float(scale), a, s.cuda_stream)

@@ -130,6 +130,7 @@ class DistributedDataParallel(nn.Module):
         self._stage = None
         self._bcast = None
         self._peer = None
+        self.peer_inplace = False
         self.peer_reason = ""
         want_peer = (reduce_route in ("auto", "peer") and self.comm_on and self.device.type == "cuda"
                      and gdt in (torch.bfloat16, torch.float32) and os.environ.get("PDE_PEER_ALLREDUCE", "1") != "0")
@@ -142,6 +143,10 @@ class DistributedDataParallel(nn.Module):
             pk = PeerAllReduce(self.process_group, self.device, max(cap, 1 << 16), timeout_ms=tmo)
             if pk.ok:
                 self._peer = pk
+                # the flat gradient buffer IPC-mapped on every rank: bucket all-reduces then read the
+                # peers' gradients where they are (no stage copy, no capacity chunks)
+                if os.environ.get("PDE_PEER_INPLACE", "1") != "0":
+                    self.peer_inplace = pk.register(self.flat_grads)
             else:
                 self.peer_reason = pk.reason
         if reduce_route == "auto":
@@ -321,6 +326,14 @@ class DistributedDataParallel(nn.Module):
         pk = self._peer
         self.check_health()
         esz = view.element_size()
+        reg = pk.registered_range(view) if self.peer_inplace else None
+        if reg is not None:
+            rid, off = reg
+            n, scale = view.numel(), 1.0 / self.world_size
+
+            def fn_ip(stream):
+                pk.native.all_reduce_registered(rid, off, n, esz, scale, 2, stream)
+            return dist.gpu_launch(self.process_group, [view], fn_ip, async_op=True, what="ddp peer all-reduce")
         chunk = max(8, (pk.capacity_bytes // esz) // 8 * 8)
         n = view.numel()
         fn_native = pk.native.all_reduce_bf16 if view.dtype == torch.bfloat16 else pk.native.all_reduce_f32

@@ -516,23 +516,26 @@ def case_peer_allreduce(graph="1"):
     dist.destroy_process_group()
 
 
-def case_peer_inplace(graph="1"):
+def case_peer_inplace(graph="1", dtype="f32"):
     """Verdict r4 item 1a: the in-place peer all-reduce over a REGISTERED buffer (peers read each
     other's buffer directly, no stage copy): ranges at several offsets / ragged sizes, one- and two-shot,
-    bit-identical on every rank and equal to the exact sum; then replayed from a captured hipGraph."""
+    bit-identical on every rank and equal to the exact sum; then replayed from a captured hipGraph.
+    dtype bf16: the DDP flat-gradient form (fp32 accumulation, one rounding; integer data, exact)."""
     from pytorch_distributed_example_amd.dist.peer import PeerAllReduce
 
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = _shared_gpu_init()
     g = dist.get_default_group()
     p = PeerAllReduce(g, dev, 1 << 20, timeout_ms=120000)
     assert p.ok, p.reason
-    buf = torch.zeros(600_000, device=dev)
+    buf = torch.zeros(600_000, device=dev, dtype=dt)
     assert p.register(buf), p.reg_reason
     sums = []
-    for off, n in ((0, 1), (4, 7), (0, 4096), (1000, 65_539), (8, 431_080), (0, 600_000), (599_996, 3)):
+    q = 16 // buf.element_size()          # 16-byte aligned offsets
+    for off, n in ((0, 1), (q, 7), (0, 4096), (1000, 65_539), (8, 431_080), (0, 600_000), (600_000 - q, 3)):
         for algo in ("peer1", "peer2", "auto"):
             gens = [torch.Generator().manual_seed(1000 * r + n + off) for r in range(W)]
-            xs = [torch.randint(-50, 50, (n,), generator=gg).float() for gg in gens]
+            xs = [torch.randint(-50, 50, (n,), generator=gg).to(dt) for gg in gens]
             buf.fill_(float("nan"))
             buf[off:off + n].copy_(xs[R].to(dev))
             view = buf[off:off + n]
@@ -561,7 +564,8 @@ def case_peer_inplace(graph="1"):
             gr.replay()
             torch.cuda.synchronize()
             assert torch.all(a == float(sum(r + 1 + rep for r in range(W)))), (rep, a[:3])
-            assert torch.allclose(b, torch.full_like(b, sum(2 * r + rep for r in range(W)) / W)), (rep, b[:3])
+            assert torch.allclose(b.float(), torch.full_like(b, sum(2 * r + rep for r in range(W)) / W).float(),
+                                  atol=1e-2 if dt == torch.bfloat16 else 1e-6), (rep, b[:3])
     assert p.error() == 0
     emit({"rank": R, "sums": sums})
     p.close()
@@ -833,7 +837,7 @@ def case_ddp_graph(model="gpt2", steps="3", route="auto", backend="gloo"):
     npar = len(list(net.parameters()))
     emit({"rank": R, "eager_bits": eager_bits, "graph_bits": graph_bits, "eager_losses": eager_losses,
           "graph_losses": graph_losses, "peer_error": ddp._peer.error() if ddp._peer is not None else 0,
-          "route": ddp.reduce_route,
+          "route": ddp.reduce_route, "peer_inplace": ddp.peer_inplace,
           # torch-DDP semantics: buffers are broadcast at the START of each forward, then updated from
           # the local batch, so across ranks only parameters and optimizer state must agree
           "replicated_bits": graph_bits[:npar] + graph_bits[npar + nb:]})

@@ -119,6 +119,7 @@ def test_ddp_graph_replay_matches_eager(model):
     assert rc == 0, "\n".join(logs)
     for r in res:
         assert r["peer_error"] == 0
+        assert r["peer_inplace"], "DDP's flat gradients were not registered for the in-place route"
         assert r["graph_bits"] == r["eager_bits"], (r["eager_losses"], r["graph_losses"])
     assert res[0]["replicated_bits"] == res[1]["replicated_bits"], "replicas diverged"
 
@@ -161,11 +162,11 @@ def test_engine_w2_matches_w1_on_concatenated_shards():
         assert abs(a - b) <= 1e-3 * max(1.0, abs(b)), (res[0]["w_params"], res[0]["one_params"])
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
-def test_peer_inplace_registered_matches_exact(world):
-    """The in-place route over a registered buffer: exact sums, nothing written outside the range,
-    bit-identical across ranks, graph-replayable."""
-    rc, res, logs = run_ranks("peer_inplace", world, "1")
+@pytest.mark.parametrize("world,dtype", [(1, "f32"), (2, "f32"), (4, "f32"), (2, "bf16"), (4, "bf16")])
+def test_peer_inplace_registered_matches_exact(world, dtype):
+    """The in-place route over a registered buffer (fp32, and bf16 as DDP's flat gradients): exact
+    sums, nothing written outside the range, bit-identical across ranks, graph-replayable."""
+    rc, res, logs = run_ranks("peer_inplace", world, "1", dtype)
     assert rc == 0, "\n".join(logs)
     assert all(r is not None for r in res), "\n".join(logs)
     assert all(r["sums"] == res[0]["sums"] for r in res), "results differ across ranks"
