@@ -46,7 +46,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "pde_peer.h"
@@ -119,11 +121,13 @@ class PeerAllReduce {
   int ip_vpt_ = 2;                              // one-shot vectors per thread (PDE_PEER_IP_VPT; 2 measured best)
   struct Reg {
     uint8_t* base[kPeerMaxRanks] = {};          // every rank's registered buffer, mapped here ([rank] = own)
-    uint8_t* mapped[kPeerMaxRanks] = {};        // what hipIpcOpenMemHandle returned (closed in close())
     int64_t bytes = 0;
     bool open = false;
   };
   std::vector<Reg> regs_;
+  // peer allocations opened for registrations, by (peer, IPC handle bytes): two registered buffers in
+  // one peer allocation (one caching-allocator segment) share a single mapping, closed once
+  std::map<std::pair<int, std::string>, uint8_t*> ipc_open_;
   bool opened_ = false;
   int64_t timeout_ticks_ = 10LL * 100000000;   // 10 s
   int64_t one_shot_max_ = 256 * 1024;

@@ -580,9 +580,9 @@ void PeerAllReduce::close() {
     if (peers_[p] != nullptr) (void)hipIpcCloseMemHandle(peers_[p]);
     if (peer_flags_[p] != nullptr) (void)hipIpcCloseMemHandle(peer_flags_[p]);
     if (peer_ipflags_[p] != nullptr) (void)hipIpcCloseMemHandle(peer_ipflags_[p]);
-    for (auto& r : regs_)
-      if (r.mapped[p] != nullptr) (void)hipIpcCloseMemHandle(r.mapped[p]);
   }
+  for (auto& kv : ipc_open_) (void)hipIpcCloseMemHandle(kv.second);
+  ipc_open_.clear();
   regs_.clear();
   for (auto& q : peers_) q = nullptr;
   for (auto& q : peer_flags_) q = nullptr;
@@ -763,10 +763,14 @@ void PeerAllReduce::open_registered(int id, const std::vector<std::string>& hand
     std::memcpy(&bytes, s.data() + kHandle + 8, 8);
     if (bytes != r.bytes) throw std::invalid_argument("registered buffers differ in size across ranks");
     if (off & 15) throw std::invalid_argument("a peer's registered buffer is not 16-byte aligned");
-    void* m = nullptr;
-    hip_check(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(registered)");
-    r.mapped[p] = static_cast<uint8_t*>(m);
-    r.base[p] = static_cast<uint8_t*>(m) + off;
+    const auto key = std::make_pair(p, std::string(s.data(), kHandle));
+    auto it = ipc_open_.find(key);
+    if (it == ipc_open_.end()) {
+      void* m = nullptr;
+      hip_check(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(registered)");
+      it = ipc_open_.emplace(key, static_cast<uint8_t*>(m)).first;
+    }
+    r.base[p] = it->second + off;
   }
   r.open = true;
 }

@@ -510,6 +510,15 @@ def case_peer_allreduce(graph="1"):
             for k, t in enumerate(xs):
                 want = float(sum(r + 1 + k for r in range(W)))
                 assert torch.all(t == want), (rep, k, t[:3])
+    # two registrations inside ONE allocation (one caching-allocator segment): one peer mapping, shared
+    pair = torch.zeros(2 * 65_536, device=dev, dtype=dt)
+    assert p.register(pair[:65_536]) and p.register(pair[65_536:]), p.reg_reason
+    for k, half in enumerate((pair[:65_536], pair[65_536:])):
+        half.fill_(float(R + 1 + k))
+        p.all_reduce_(half, "peer2")
+    torch.cuda.synchronize()
+    assert torch.all(pair[:65_536] == float(sum(r + 1 for r in range(W))))
+    assert torch.all(pair[65_536:] == float(sum(r + 2 for r in range(W))))
     assert p.error() == 0
     emit({"rank": R, "sums": sums})
     p.close()
@@ -566,6 +575,15 @@ def case_peer_inplace(graph="1", dtype="f32"):
             assert torch.all(a == float(sum(r + 1 + rep for r in range(W)))), (rep, a[:3])
             assert torch.allclose(b.float(), torch.full_like(b, sum(2 * r + rep for r in range(W)) / W).float(),
                                   atol=1e-2 if dt == torch.bfloat16 else 1e-6), (rep, b[:3])
+    # two registrations inside ONE allocation (one caching-allocator segment): one peer mapping, shared
+    pair = torch.zeros(2 * 65_536, device=dev, dtype=dt)
+    assert p.register(pair[:65_536]) and p.register(pair[65_536:]), p.reg_reason
+    for k, half in enumerate((pair[:65_536], pair[65_536:])):
+        half.fill_(float(R + 1 + k))
+        p.all_reduce_(half, "peer2")
+    torch.cuda.synchronize()
+    assert torch.all(pair[:65_536] == float(sum(r + 1 for r in range(W))))
+    assert torch.all(pair[65_536:] == float(sum(r + 2 for r in range(W))))
     assert p.error() == 0
     emit({"rank": R, "sums": sums})
     p.close()
