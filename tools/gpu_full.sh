@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/${1:-r4_full}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 180 --timeout-method thread > $O/pytest_gpu.txt 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 170 --timeout-method thread > $O/pytest_gpu.txt 2>&1
 TRC=$?
 if [ $TRC -gt 1 ]; then tail -40 $O/pytest_gpu.txt; exit $TRC; fi
 grep -E "^(FAILED|ERROR)" $O/pytest_gpu.txt | cut -c1-300; tail -2 $O/pytest_gpu.txt
