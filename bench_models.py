@@ -18,7 +18,10 @@ import sys
 import time
 
 
-def _setup():
+def _setup(shared_gpu: bool = False):
+    """(torch, dist, rank, world, device).  ``shared_gpu``: the one-GPU rehearsal of the N > 1 path --
+    every rank on cuda:0, a gloo control group, DDP's bucket all-reduces and buffer broadcasts on the
+    xGMI peer kernel (in place over the registered flat gradients)."""
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -26,13 +29,14 @@ def _setup():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
     torch.cuda.set_device(local_rank)
     if world > 1 and not dist.is_initialized():
         with stdout_to_stderr():                  # RCCL's init banner must not precede the JSON line
-            dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world)
+            dist.init_process_group("gloo" if shared_gpu else "nccl", init_method="env://", rank=rank,
+                                    world_size=world)
             dist.barrier()
     return torch, dist, rank, world, torch.device("cuda", local_rank)
 
@@ -75,7 +79,10 @@ def _tune(ddp, step, world, args, restore=None) -> dict:
     from pytorch_distributed_example_amd.parallel import tune_bucket_cap
     out = {}
     if str(args.bucket_mb) == "auto":
-        timings, best = tune_bucket_cap(ddp, step, restore=restore)
+        # shared-GPU rehearsal: only the peer route is device-side (gloo host collectives cannot be
+        # captured into the step graph)
+        routes = ["peer"] if getattr(args, "shared_gpu", False) else None
+        timings, best = tune_bucket_cap(ddp, step, routes=routes, restore=restore)
         out.update(bucket_mb=best, bucket_sweep_ms_per_step=timings)
     else:
         out["bucket_mb"] = float(args.bucket_mb)
@@ -213,7 +220,7 @@ def _gpt2_run(args, torch, dist, rank, world, dev, comm):
 
 
 def bench_gpt2(args):
-    torch, dist, rank, world, dev = _setup()
+    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False))
     r = _gpt2_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
     B, T = r["B"], r["T"]
     tps = args.steps * B * T * world / r["elapsed"]

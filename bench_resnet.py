@@ -72,7 +72,7 @@ def _resnet_run(args, torch, dist, rank, world, dev, comm):
 
 
 def bench_resnet18(args):
-    torch, dist, rank, world, dev = _setup()
+    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False))
     r = _resnet_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
     B = r["B"]
     ips = args.steps * B * world / r["elapsed"]
