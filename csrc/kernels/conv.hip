@@ -32,6 +32,8 @@
 #include "pde_kernels.h"
 #include "pde_lds.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace pde_lds;
@@ -438,6 +440,7 @@ struct WgradArgs {
   int Bn, IH, IW, C, OH, OW, N, S, stride, pad, T;
   int P, stages_per_split, mtiles, ntiles;
   float inv_hw, inv_w;
+  int incr;             // 1: walk the B rows' (b, oh, ow) incrementally (64 / OW + 1 < 2 OH, host-checked)
 };
 
 template <int BM, int BN, int NST>
@@ -476,6 +479,22 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
     xs_[v] = tap % a.S - a.pad;
   }
   const rsrc_t dyr = make_rsrc(a.dY, a.dy_bytes), xr = make_rsrc(a.X, a.x_bytes);
+  // B rows: the output pixel of this lane's row in each of its BI instructions, decomposed once into
+  // (b, oh, ow) and then advanced by 64 pixels per issued stage -- ow by 64 % OW, oh by 64 / OW, with at
+  // most one carry into oh and two into b (a.incr) -- instead of two reciprocal divisions per row and
+  // stage: ~10 fewer VALU per instruction in a loop that was VALU-bound (11 VALU per MFMA, PMC)
+  const int dq64 = 64 / a.OW, dr64 = 64 - dq64 * a.OW;
+  int pb[BI], poh[BI], pow_[BI];
+  if (a.incr) {
+#pragma unroll
+    for (int v = 0; v < BI; ++v) {
+      const int p = pbeg + 8 * ((4 * v + w) & 7) + lrow;
+      const int b = p / (a.OH * a.OW), r2 = p - b * (a.OH * a.OW);
+      pb[v] = b;
+      poh[v] = r2 / a.OW;
+      pow_[v] = r2 - poh[v] * a.OW;
+    }
+  }
   auto issue = [&](int kt, int buf) {
     const int p0 = pbeg + kt * 64;
     const char* Ai = smem + buf * STAGE;
@@ -489,9 +508,25 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
       const int q = 4 * v + w, p = p0 + 8 * (q & 7) + lrow;
-      const int pp = min(p, a.P - 1);
-      const int b = fdiv(pp, a.OH * a.OW, a.inv_hw), r2 = pp - b * (a.OH * a.OW);
-      const int oh = fdiv(r2, a.OW, a.inv_w), ow = r2 - oh * a.OW;
+      int b, oh, ow;
+      if (a.incr) {                    // rows past P are masked below: their (b, oh, ow) may run on
+        b = pb[v];
+        oh = poh[v];
+        ow = pow_[v];
+        int nw = ow + dr64, nh = oh + dq64, nb = b;
+        if (nw >= a.OW) { nw -= a.OW; ++nh; }
+        if (nh >= a.OH) { nh -= a.OH; ++nb; }
+        if (nh >= a.OH) { nh -= a.OH; ++nb; }
+        pb[v] = nb;
+        poh[v] = nh;
+        pow_[v] = nw;
+      } else {
+        const int pp = min(p, a.P - 1);
+        b = fdiv(pp, a.OH * a.OW, a.inv_hw);
+        const int r2 = pp - b * (a.OH * a.OW);
+        oh = fdiv(r2, a.OW, a.inv_w);
+        ow = r2 - oh * a.OW;
+      }
       const int ih = oh * a.stride + xr_[v], iw = ow * a.stride + xs_[v];
       const bool ok = p < pend && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
       const uint32_t off = (uint32_t)(((b * a.IH + ih) * a.IW + iw) * a.C + xc_[v]) * 2u;
@@ -1490,6 +1525,13 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   a.P = Bn * OH * OW;
   a.inv_hw = 1.0f / (float)(OH * OW);
   a.inv_w = 1.0f / (float)OW;
+  {
+    static const bool incr_env = [] {
+      const char* e = getenv("PDE_WGRAD_INCR");
+      return e == nullptr || e[0] != '0';
+    }();
+    a.incr = incr_env && (64 / OW + 1 < 2 * OH) ? 1 : 0;   // <= 2 carries of oh into b per 64-pixel step
+  }
   const int stages = (a.P + 63) / 64;
   a.stages_per_split = (stages + splits - 1) / splits;
   const int TC = a.T * C;
