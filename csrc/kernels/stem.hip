@@ -15,6 +15,9 @@
 // each wave walks its row in 32-pixel quarters with a 32 x 64 accumulator pair; epilogue rounds to
 // bf16, emits per-channel (sum, sum of squares) partials of the rounded output in the [block][2][64]
 // format of the BatchNorm finalize (no BN statistics pass), and stores 16-byte rows via LDS.
+#include <type_traits>
+
+#include "pde_act.h"
 #include "pde_bf16.h"
 #include "pde_hip.h"
 #include "pde_kernels.h"
@@ -56,19 +59,31 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const bf16_t* __restrict__ X, 
     *reinterpret_cast<uint4*>(wp + n * kSWStride * 2 + ch * 16) = reinterpret_cast<const uint4*>(Wp)[e];
   }
   // software pipeline over this block's row groups: the next group's 13 input rows are loaded into
-  // registers while the current group computes from LDS
+  // registers while the current group computes from LDS.  A thread's staged pixels e = t + 256 j sit at
+  // the same (row r_j, column) of every group, so their row / column split (a division), the column
+  // bounds and the in-row element offset are fixed once per block; a group adds one row base
   const int ncols = 2 * OW + 6;
   constexpr int kPF = (kSInRows * kSInCols + 255) / 256;    // staged pixels per thread (<= 12)
   uint2 pf[kPF];
+  int pr[kPF], poff[kPF];
+  uint32_t pcol = 0;                                          // bit j: column of pixel j inside the image
+#pragma unroll
+  for (int j = 0; j < kPF; ++j) {
+    const int e = t + 256 * j, r = e / ncols, col = e - r * ncols, iw = col - 3;
+    pr[j] = r < kSInRows ? r : (1 << 20);                     // past the staged rows: never loaded
+    poff[j] = r * Wd * 3 + iw * 3;
+    pcol |= (iw >= 0 && iw < Wd) ? (1u << j) : 0u;
+  }
   const int gbeg = blockIdx.x * ngroups, gend = min(gbeg + ngroups, total_groups);
   auto prefetch = [&](int grp) {
     const int b = grp / rgroups, ih0 = 2 * (grp - b * rgroups) * kSRows - 3;
+    const bf16_t* base = X + ((ptrdiff_t)b * H + ih0) * Wd * 3;   // (row ih0, column 0) of image b
 #pragma unroll
     for (int j = 0; j < kPF; ++j) {
-      const int e = t + 256 * j, r = e / ncols, col = e - r * ncols, ih = ih0 + r, iw = col - 3;
+      const int ih = ih0 + pr[j];
       pf[j] = make_uint2(0u, 0u);
-      if (r < kSInRows && ih >= 0 && ih < H && iw >= 0 && iw < Wd) {
-        const bf16_t* src = X + (((size_t)b * H + ih) * Wd + iw) * 3;
+      if (((pcol >> j) & 1u) && (unsigned)ih < (unsigned)H) {
+        const bf16_t* src = base + poff[j];
         pf[j].x = (uint32_t)src[0] | ((uint32_t)src[1] << 16);
         pf[j].y = (uint32_t)src[2];
       }
@@ -106,20 +121,31 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const bf16_t* __restrict__ X, 
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, acc1, 0, 0, 0);
           }
         }
-        // epilogue: D reg r -> pixel row (r&3) + 8*(r>>2) + 4*g, channel i32 (+32)
+        // epilogue: D reg r -> pixel row (r&3) + 8*(r>>2) + 4*g, channel i32 (+32).  The two channels
+        // of a register pair are rounded by one packed convert and stored as the low / high halves
+        // of that word; the statistics of the rounded values use packed adds / FMAs; only the last,
+        // partial quarter of a row masks pixels
+        auto epi = [&](auto FULL_) {
+          constexpr bool FULL = decltype(FULL_)::value;
+          pde_f2 sacc = {s_lo, s_hi}, qacc = {q_lo, q_hi};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int px = (r & 3) + 8 * (r >> 2) + 4 * g;
-          const bool valid = q0 + px < OW;
-          const bf16_t v0 = f2bf(acc0[r]), v1 = f2bf(acc1[r]);
-          const float f0 = bf2f(v0), f1 = bf2f(v1);
-          if (valid) {
-            s_lo += f0; q_lo += f0 * f0;
-            s_hi += f1; q_hi += f1 * f1;
+          for (int r = 0; r < 16; ++r) {
+            const int px = (r & 3) + 8 * (r >> 2) + 4 * g;
+            const uint32_t pk = pack_bf2(acc0[r], acc1[r]);
+            pde_f2 f = {__uint_as_float(pk << 16), __uint_as_float(pk & 0xffff0000u)};
+            if constexpr (!FULL) {
+              const float m = q0 + px < OW ? 1.f : 0.f;
+              f = f * m;
+            }
+            sacc += f;
+            qacc = f * f + qacc;
+            *reinterpret_cast<uint16_t*>(st + px * 128 + i32 * 2) = (uint16_t)pk;
+            *reinterpret_cast<uint16_t*>(st + px * 128 + (i32 + 32) * 2) = (uint16_t)(pk >> 16);
           }
-          *reinterpret_cast<bf16_t*>(st + px * 128 + i32 * 2) = v0;
-          *reinterpret_cast<bf16_t*>(st + px * 128 + (i32 + 32) * 2) = v1;
-        }
+          s_lo = sacc.x; s_hi = sacc.y; q_lo = qacc.x; q_hi = qacc.y;
+        };
+        if (q0 + 32 <= OW) epi(std::true_type{});
+        else epi(std::false_type{});
         // the stage is private to this wave: wave-level LDS ordering is enough
         __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
