@@ -1058,20 +1058,25 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
   struct Fr {
     s4v a[2][2], b[2][2];
   };
-  // this lane's two K rows advance by 16 pixels per k-step: image (row, column) kept incrementally
-  // (no integer division in the loop); rows past npx read a valid halo row (their dY rows are zero)
-  int kk0 = 0, py0 = 0, px0 = 0, py1 = 0, px1 = 0;
+  // this lane's two K rows advance by 16 pixels per k-step: their image column and halo row index
+  // (py + 1) * (W + 2) + px + 1 are kept incrementally -- a column wrap moves the halo row by the two
+  // padding columns -- so the loop has no division and no per-step multiply (v_mul_lo_u32 is a
+  // quarter-rate op; the K loop was VALU-bound); rows past npx read a valid halo row (their dY is 0)
+  int kk0 = 0, px0 = 0, px1 = 0, hr0 = 0, hr1 = 0;
   auto start = [&]() {
     kk0 = 4 * h2 + q;
-    py0 = kk0 / a.W; px0 = kk0 - py0 * a.W;
-    const int k1 = kk0 + 8;
-    py1 = k1 / a.W; px1 = k1 - py1 * a.W;
+    const int py0 = kk0 / a.W, k1 = kk0 + 8, py1 = k1 / a.W;
+    px0 = kk0 - py0 * a.W;
+    px1 = k1 - py1 * a.W;
+    hr0 = (py0 + 1) * HW2 + px0 + 1;
+    hr1 = (py1 + 1) * HW2 + px1 + 1;
   };
   auto advance = [&]() {
     kk0 += 16;
     px0 += 16; px1 += 16;
-    while (px0 >= a.W) { px0 -= a.W; ++py0; }
-    while (px1 >= a.W) { px1 -= a.W; ++py1; }
+    hr0 += 16; hr1 += 16;
+    while (px0 >= a.W) { px0 -= a.W; hr0 += 2; }
+    while (px1 >= a.W) { px1 -= a.W; hr1 += 2; }
   };
   // dY (A) rows advance by exactly 16 per k-step, which leaves their swizzle unchanged: the four A
   // offsets are per-lane constants plus 2048 * ks
@@ -1083,8 +1088,8 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
   }
   auto load = [&](Fr& f, uint32_t hbase, uint32_t ybase, int npx) {
     const int k0 = kk0, k1 = kk0 + 8;
-    const int r0 = (k0 < npx ? (py0 + 1) * HW2 + px0 + 1 : HW2 + 1) + td;
-    const int r1 = (k1 < npx ? (py1 + 1) * HW2 + px1 + 1 : HW2 + 1) + td;
+    const int r0 = (k0 < npx ? hr0 : HW2 + 1) + td;
+    const int r1 = (k1 < npx ? hr1 : HW2 + 1) + td;
     const uint32_t ya = ybase + 128u * (uint32_t)(kk0 - 4 * h2 - q);     // 2048 * ks
     const uint32_t b0 = hbase + r0 * 128 + 8 * hf, b1 = hbase + r1 * 128 + 8 * hf;
     const int s0 = hsw((r0 >> 1) & 7), s1 = hsw((r1 >> 1) & 7);
