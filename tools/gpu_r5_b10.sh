@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-5 batch 10: route timings as graph-replayed GPU time (default) vs eager launches; peer GPU tests.
+# (The batch also ran a cross-entropy non-temporal A/B whose code was reverted: profiles/r5_gpt2/rejected_xent_nt/.)
 set -o pipefail
 O=gpurun_out/${1:-r5_b10}
 mkdir -p $O
@@ -16,5 +17,3 @@ print(sys.argv[2], "headline", d["ms_per_step"], "| comm", w.get("ms_per_step"),
       "compute", w.get("compute_only_us_per_step"), "routes", json.dumps(w.get("route_us_per_call")))
 PY
 done
-# GPT-2 cross-entropy: non-temporal dlogits stores / logits loads (PDE_XENT_NT bits), same box
-bash tools/gpu_gpt2_ab.sh ${1:-r5_b10}/xent PDE_XENT_NT=0 PDE_XENT_NT=1 PDE_XENT_NT=3
