@@ -482,6 +482,83 @@ __global__ __launch_bounds__(512) void k_bnpool_fwd(const uint4* __restrict__ Y,
   }
 }
 
+// The same fused apply + pool with one thread per 2 x JW block of pooled cells (oh0 + i, ow0 + j) and
+// chunk: the 5 x (2 JW + 1) input patch rows 2 oh0 - 1 .. 2 oh0 + 3, columns 2 ow0 - 1 .. 2 ow0 + 2 JW - 1
+// covers all its windows, so (JW = 2) a thread issues 25 16-byte loads and 25 relu(bn(.)) evaluations
+// for 4 outputs instead of 36 + 36 (JW = 1: 15 for 2).  The patch streams row by row (5 loads in flight); each element updates the windows
+// that contain it in the same (kh, kw) order as k_bnpool_fwd, so ties resolve identically.
+template <int JW>
+__global__ __launch_bounds__(256) void k_bnpool_fwd2(const uint4* __restrict__ Y, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, uint4* __restrict__ P,
+                                                     uint2* __restrict__ Arg, uint4* __restrict__ Ysel, int H, int W,
+                                                     int OH, int OW, int CP, int lgcp) {
+  const int oh0 = 2 * blockIdx.x, n = blockIdx.y, c8 = threadIdx.x & (CP - 1);
+  constexpr int NC = 2 * JW + 1, NQ = 2 * JW;   // patch columns, outputs per thread
+  const int owp = (OW + JW - 1) / JW;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c8 * 8 + e];
+    sf[e] = shift[c8 * 8 + e];
+  }
+  const uint4* yimg = Y + (size_t)n * H * W * CP;
+  for (int idx = threadIdx.x; idx < owp * CP; idx += blockDim.x) {
+    const int ow0 = JW * (idx >> lgcp);
+    float best[NQ][8], ysel[NQ][8];
+    uint32_t arg[NQ][8];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        best[q][e] = -INFINITY;
+        ysel[q][e] = 0.f;
+        arg[q][e] = 0;
+      }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int ih = 2 * oh0 - 1 + r;
+      if (ih < 0 || ih >= H) continue;  // uniform over the block
+      uint4 raw[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) raw[c] = yimg[(ih * W + min(max(2 * ow0 - 1 + c, 0), W - 1)) * CP + c8];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int iw = 2 * ow0 - 1 + c;
+        const bool ok = iw >= 0 && iw < W;
+        float v[8];
+        unpack8(raw[c], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = bf2f(f2bf(fmaxf(v[e] * sc[e] + sf[e], 0.f)));
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            if (r < 2 * i || r > 2 * i + 2) continue;  // compile-time after unrolling
+#pragma unroll
+            for (int j = 0; j < JW; ++j) {
+              if (c < 2 * j || c > 2 * j + 2) continue;
+              const int q = JW * i + j;
+              const bool better = ok && a > best[q][e];
+              best[q][e] = better ? a : best[q][e];
+              ysel[q][e] = better ? v[e] : ysel[q][e];
+              arg[q][e] = better ? (uint32_t)((r - 2 * i) * 3 + c - 2 * j) : arg[q][e];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int oh = oh0 + q / JW, ow = ow0 + q % JW;
+      if (oh >= OH || ow >= OW) continue;
+      const size_t o = ((size_t)(n * OH + oh) * OW + ow) * CP + c8;
+      P[o] = pack8(best[q]);
+      Ysel[o] = pack8(ysel[q]);
+      Arg[o] = make_uint2(arg[q][0] | (arg[q][1] << 8) | (arg[q][2] << 16) | (arg[q][3] << 24),
+                          arg[q][4] | (arg[q][5] << 8) | (arg[q][6] << 16) | (arg[q][7] << 24));
+    }
+  }
+}
+
 // Backward.  The BN partials need only the windows: d is non-zero only where a window took its
 // maximum, so sum d = sum over windows of dP (masked by a > 0) and sum d*y = sum over windows of
 // dP * y[argmax].  The forward stores y[argmax] (Ysel, one pooled map), and the reduce pass is
@@ -751,6 +828,20 @@ hipError_t pde_bnpool_fwd(const void* y, const float* scale, const float* shift,
                           int N, int C, int H, int W, int OH, int OW, hipStream_t st) {
   const int CP = C / 8;
   if (C % 8 || (CP & (CP - 1)) || CP > 64) return hipErrorInvalidValue;
+  // pooled cells per thread: 1, 2 (vertical pair, the default) or 4 (2x2 block); read per call (once
+  // per step) so that a test can compare the variants in one process.  ResNet-18 stem at B = 256
+  // (profiles/r5_models/bnpool_fwd_pairs): 152.4 / 136.4 / 149.0 us -- the 2x2 block needs 164 VGPRs
+  // (3 waves / SIMD), the pair 94 (5 waves)
+  const char* env = getenv("PDE_BNPOOL_FWD");
+  const int variant = env ? atoi(env) : 2;
+  if (variant == 2 || variant == 4) {
+    const int jw = variant / 2, cells = (OW + jw - 1) / jw * CP;
+    const int threads = min(256, (cells + 63) / 64 * 64);
+    auto kern = jw == 2 ? k_bnpool_fwd2<2> : k_bnpool_fwd2<1>;
+    hipLaunchKernelGGL(kern, dim3((OH + 1) / 2, N), dim3(threads), 0, st, (const uint4*)y, scale, shift, (uint4*)p,
+                       (uint2*)arg, (uint4*)ysel, H, W, OH, OW, CP, ilog2(CP));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_bnpool_fwd, dim3(OH, N), dim3(bnpool_threads(OW * CP)), 0, st, (const uint4*)y, scale, shift,
                      (uint4*)p, (uint2*)arg, (uint4*)ysel, H, W, OH, OW, CP, ilog2(CP));
   return hipGetLastError();

@@ -362,6 +362,31 @@ def test_bn_relu_maxpool_fused(shape):
     assert rel_err(dgf, gr.grad) < 3e-2 and rel_err(dbf, br.grad) < 3e-2
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 64, 9, 7), (3, 16, 6, 6), (2, 32, 11, 13)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_bn_relu_maxpool_fwd_variants_identical(shape, ties, monkeypatch):
+    """The 1-, 2- and 4-cells-per-thread pooling forwards (PDE_BNPOOL_FWD, read per call) produce
+    bit-identical pooled maps, argmax codes and y-at-argmax maps, ties included (integer-valued y
+    makes most windows tie)."""
+    from pytorch_distributed_example_amd.models.resnet import BN
+    from pytorch_distributed_example_amd.ops.resnet import bn_relu_maxpool
+    torch.manual_seed(12)
+    N, C, H, W = shape
+    y0 = torch.randint(-2, 3, (N, C, H, W)).float() if ties else torch.randn(N, C, H, W) * 1.3 + 0.2
+    y0 = y0.to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    yf = y0.float().permute(0, 2, 3, 1).reshape(-1, C)
+    stats = (torch.cat([yf.sum(0), (yf * yf).sum(0)]).contiguous(), 1)
+    got = []
+    for variant in ("1", "2", "4"):
+        monkeypatch.setenv("PDE_BNPOOL_FWD", variant)
+        bn = BN(C).to(dev).to(torch.bfloat16)
+        p = bn_relu_maxpool(y0.clone().requires_grad_(), stats, bn)
+        saved = p.grad_fn.saved_tensors
+        got.append((p.detach(), saved[6], saved[7]))     # pooled, arg, ysel
+    for p, a, s in got[1:]:
+        assert torch.equal(p, got[0][0]) and torch.equal(a, got[0][1]) and torch.equal(s, got[0][2])
+
+
 def test_resnet18_grads_land_in_flat_buffer():
     """After the optimizer binds the flat buffers, conv weights stay channels-last and every
     gradient of a step is written in place into the flat gradient buffer (no per-parameter copy)."""
