@@ -650,7 +650,7 @@ __device__ __forceinline__ bf16x8 halo_frag(const char* halo, int row, int chunk
 // channel chunk that lane l loads for halo group g (parity gpar = g & 1; groups are 8 rows)
 __device__ __forceinline__ int halo_dma_chunk(int l, int gpar) { return (l & 7) ^ hsw((4 * gpar + (l >> 4)) & 7); }
 
-template <int BM, int BN>
+template <int BM, int BN, int V>
 __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   constexpr int WN = BN / 64, WM = 4 / WN;
   static_assert(WM * 64 == BM, "wave grid must tile BM x BN with 64x64 wave tiles");
@@ -736,27 +736,68 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
       }
     }
     issue_b(0, c0, 0);
-    for (int tp = 0; tp < 9; ++tp) {
-      wait_vm<0>();
-      __builtin_amdgcn_s_barrier();
-      if (tp + 1 < 9) issue_b(tp + 1, c0, (tp + 1) & 1);
-      const int pk = a.tap[tp];
-      const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
-      const char* Bi = bimg + (tp & 1) * BBYTES;
-      int hp[2];
+    if constexpr (V == 0) {
+      for (int tp = 0; tp < 9; ++tp) {
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (tp + 1 < 9) issue_b(tp + 1, c0, (tp + 1) & 1);
+        const int pk = a.tap[tp];
+        const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+        const char* Bi = bimg + (tp & 1) * BBYTES;
+        int hp[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) hp[i] = hbase[i] + td;
+        for (int i = 0; i < 2; ++i) hp[i] = hbase[i] + td;
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        bf16x8 fa[2], fb[2];
+        for (int s4 = 0; s4 < 4; ++s4) {
+          bf16x8 fa[2], fb[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[i] = halo_frag(halo, hp[i], 2 * s4 + lh);
+          for (int i = 0; i < 2; ++i) fa[i] = halo_frag(halo, hp[i], 2 * s4 + lh);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, wn * 64 + j * 32 + lr, 2 * s4 + lh);
+          for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, wn * 64 + j * 32 + lr, 2 * s4 + lh);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+        }
+      }
+    } else {
+      // V = 1 (default): the A-fragment row bases pass through an opaque register move at every tap,
+      // so the compiler cannot hoist all 9 taps x 8 fragment addresses out of the channel loop (V = 0:
+      // 72 VGPRs at the 256-register cap, leaving 12 for fragments and an lgkmcnt wait in front of
+      // nearly every MFMA; V = 1: 217 VGPRs, 72 instead of 108 waits per chunk, ~33 more VALU per tap).
+      // l2 / l3 convs 3-5 % faster, ResNet-18 step +0.7 % (profiles/r5_models/hconv_tap_addresses/).
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (tp + 1 < 9) issue_b(tp + 1, c0, (tp + 1) & 1);
+        const int pk = a.tap[tp];
+        const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+        const char* Bi = bimg + (tp & 1) * BBYTES;
+        // halo_frag(halo, row, 2 s4 + lh) = halo + (row * 128 + 16 (lh ^ key)) ^ 32 s4: one XOR per
+        // fragment address once the s4 = 0 address is formed
+        int ha[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          int row = hbase[i];
+          asm volatile("" : "+v"(row));
+          row += td;
+          ha[i] = row * 128 + 16 * (lh ^ hsw((row >> 1) & 7));
+        }
+        bf16x8 fa[4][2], fb[4][2];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) fa[s4][i] = *reinterpret_cast<const bf16x8*>(halo + (ha[i] ^ (32 * s4)));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fb[s4][j] = row_frag(Bi, wn * 64 + j * 32 + lr, 2 * s4 + lh);
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(fa[s4][i], fb[s4][j], acc[i][j]);
       }
     }
   }
@@ -1232,12 +1273,15 @@ hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, f
   if (const int g64 = hconv64_grid(Bn, H, W, CA, NC)) {
     a.ntiles = 1;
     hipLaunchKernelGGL(k_hconv64, dim3(g64), dim3(kT64), 0, st, a);
-  } else if (BM == 256) {
-    a.ntiles = NC / 64;
-    hipLaunchKernelGGL((k_hconv<256, 64>), dim3(Bn * rtiles * a.ntiles), dim3(kThreads), 0, st, a);
   } else {
-    a.ntiles = NC / 128;
-    hipLaunchKernelGGL((k_hconv<128, 128>), dim3(Bn * rtiles * a.ntiles), dim3(kThreads), 0, st, a);
+    const char* env = getenv("PDE_HCONV_V");   // tap-loop form (A/B): 0 hoisted addresses, 1 per tap
+    const int v = env ? atoi(env) : 1;
+    a.ntiles = NC / (BM == 256 ? 64 : 128);
+    const dim3 grid(Bn * rtiles * a.ntiles);
+    if (BM == 256)
+      hipLaunchKernelGGL((v == 0 ? k_hconv<256, 64, 0> : k_hconv<256, 64, 1>), grid, dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((v == 0 ? k_hconv<128, 128, 0> : k_hconv<128, 128, 1>), grid, dim3(kThreads), 0, st, a);
   }
   return hipGetLastError();
 }

@@ -77,6 +77,28 @@ def test_conv_exact_integer_data():
     assert torch.equal(w.grad.double().cpu(), wr.grad)
 
 
+@pytest.mark.parametrize("B,C,H,W,N", [(2, 128, 28, 28, 128), (2, 256, 14, 14, 256), (3, 64, 17, 23, 128),
+                                       (2, 128, 20, 15, 64)])
+def test_hconv_tap_loop_forms_identical(B, C, H, W, N, monkeypatch):
+    """k_hconv's two tap-loop forms (PDE_HCONV_V=0: fragment addresses hoisted out of the channel loop;
+    1: formed per tap, the default) run the same MFMA sequence: bit-identical fprop and dgrad, and
+    exact on integer data."""
+    torch.manual_seed(C + W)
+    x = cl(torch.randint(-2, 3, (B, C, H, W), device=dev).to(torch.bfloat16))
+    w = cl(torch.randint(-1, 2, (N, C, 3, 3), device=dev).to(torch.bfloat16))
+    dy = cl(torch.randint(-1, 2, (B, N, H, W), device=dev).to(torch.bfloat16))
+    got = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("PDE_HCONV_V", v)
+        xv = x.clone().requires_grad_()
+        y = conv2d_nhwc(xv, w, 1, 1)
+        y.backward(dy)
+        got.append((y.detach(), xv.grad))
+    assert torch.equal(got[0][0], got[1][0]) and torch.equal(got[0][1], got[1][1])
+    yr = F.conv2d(x.double().cpu(), w.double().cpu(), None, 1, 1)
+    assert torch.equal(got[1][0].double().cpu(), yr)
+
+
 @pytest.mark.parametrize("N", [64, 128])
 @pytest.mark.parametrize("B,H,W", [(3, 10, 9), (2, 12, 20), (2, 9, 56), (24, 56, 56)])
 def test_conv_fprop_bn_stats(N, B, H, W):
