@@ -440,7 +440,8 @@ struct WgradArgs {
   int Bn, IH, IW, C, OH, OW, N, S, stride, pad, T;
   int P, stages_per_split, mtiles, ntiles;
   float inv_hw, inv_w;
-  int incr;             // 1: walk the B rows' (b, oh, ow) incrementally (64 / OW + 1 < 2 OH, host-checked)
+  int incr;             // 1: walk the B rows' (b, oh, ow) incrementally (64 / OW + 1 < 2 OH, host-checked);
+                        // 2: as 1, one walk per row group shared by its two column images
 };
 
 template <int BM, int BN, int NST>
@@ -485,6 +486,13 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
   // stage: ~10 fewer VALU per instruction in a loop that was VALU-bound (11 VALU per MFMA, PMC)
   const int dq64 = 64 / a.OW, dr64 = 64 - dq64 * a.OW;
   int pb[BI], poh[BI], pow_[BI];
+  // incr == 2: instructions v and v + 2 load the same 8 pixel rows ((4 v + w) & 7) for the two 64-column
+  // images, so only NR = 2 walks are kept and each B row's address is rowbase (pixel, shared) + tap
+  // offset (per v): x[b][oh s + dr][ow s + ds][c] = X + (((b IH + oh s) IW + ow s) C + (dr IW + ds) C + c)
+  constexpr int NR = BI >= 2 ? 2 : 1;
+  int toff[BI];
+#pragma unroll
+  for (int v = 0; v < BI; ++v) toff[v] = xr_[v] > -(1 << 19) ? (xr_[v] * a.IW + xs_[v]) * a.C + xc_[v] : 0;
   if (a.incr) {
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
@@ -493,6 +501,20 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
       pb[v] = b;
       poh[v] = r2 / a.OW;
       pow_[v] = r2 - poh[v] * a.OW;
+    }
+  }
+  // incr == 2 keeps, per row group r < NR, (pb, poh, pow_) = (pixel-row element offset of x[b][oh s][ow s][0],
+  // oh s, ow s): the 64-pixel advance adds wd0 (+ wdw on a column wrap, + wdh per row wrap)
+  const int wow = a.OW * a.stride, woh = a.OH * a.stride, wdr = dr64 * a.stride, wdq = dq64 * a.stride;
+  const int wd0 = (dq64 * a.stride * a.IW + dr64 * a.stride) * a.C;
+  const int wdw = (a.stride * a.IW - wow) * a.C, wdh = (a.IH - woh) * a.IW * a.C;
+  if (a.incr == 2) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int ohs = poh[r] * a.stride, ows = pow_[r] * a.stride;
+      pb[r] = ((pb[r] * a.IH + ohs) * a.IW + ows) * a.C;
+      poh[r] = ohs;
+      pow_[r] = ows;
     }
   }
   auto issue = [&](int kt, int buf) {
@@ -504,6 +526,28 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
       const int q = 4 * u + w, p = p0 + 8 * (q & 7) + lrow;
       const uint32_t off = (uint32_t)(p * a.N + n0 + (q >> 3) * 64 + ch * 8) * 2u;
       glds16(dyr, Ai + q * 1024, p < pend ? off : kOOB);
+    }
+    if (a.incr == 2) {
+#pragma unroll
+      for (int v = 0; v < BI; ++v) {
+        const int q = 4 * v + w, r = v % NR;
+        const bool pin = p0 + 8 * ((4 * r + w) & 7) + lrow < pend;
+        const bool ok = pin & ((unsigned)(poh[r] + xr_[v]) < (unsigned)a.IH) &   // & : no short-circuit
+                        ((unsigned)(pow_[r] + xs_[v]) < (unsigned)a.IW);           // exec-mask branches
+        glds16(xr, Bi + q * 1024, ok ? (uint32_t)(pb[r] + toff[v]) * 2u : kOOB);
+      }
+      // advance by 64 pixels: no multiplies (v_mul_lo_u32 is quarter rate), the deltas are uniform
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        int ows = pow_[r] + wdr, ohs = poh[r] + wdq, rb = pb[r] + wd0;
+        if (ows >= wow) { ows -= wow; ohs += a.stride; rb += wdw; }
+        if (ohs >= woh) { ohs -= woh; rb += wdh; }
+        if (ohs >= woh) { ohs -= woh; rb += wdh; }
+        pow_[r] = ows;
+        poh[r] = ohs;
+        pb[r] = rb;
+      }
+      return;
     }
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
@@ -1575,11 +1619,11 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   a.inv_hw = 1.0f / (float)(OH * OW);
   a.inv_w = 1.0f / (float)OW;
   {
-    static const bool incr_env = [] {
+    static const int incr_env = [] {   // PDE_WGRAD_INCR: 0 divisions, 1 a walk per instruction, 2 (default) shared
       const char* e = getenv("PDE_WGRAD_INCR");
-      return e == nullptr || e[0] != '0';
+      return e == nullptr ? 2 : atoi(e);
     }();
-    a.incr = incr_env && (64 / OW + 1 < 2 * OH) ? 1 : 0;   // <= 2 carries of oh into b per 64-pixel step
+    a.incr = (64 / OW + 1 < 2 * OH) ? incr_env : 0;   // <= 2 carries of oh into b per 64-pixel step
   }
   const int stages = (a.P + 63) / 64;
   a.stages_per_split = (stages + splits - 1) / splits;
