@@ -912,6 +912,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
 // remains.  One block per CU (72 KB weights + 2 x 44 KB halos = 160 KB of LDS); the epilogue uses the
 // current halo buffer as its scratch tile.
 constexpr int kT64 = 512;                             // 8 waves: 2 per SIMD to hide LDS / MFMA latency
+template <bool PIPE>
 __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
   constexpr int HG = 44, HU = (HG + 7) / 8, HB = HG * 1024;   // (TH + 2) * (W + 2) <= 352 halo pixels
   constexpr int WB = 9 * 64 * 128;                      // 72 KB weights + 2 x 44 KB halos = 160 KB
@@ -989,18 +990,41 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
     f32x16 acc[1][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[0][j] = f32x16{0.f};
-    for (int tp = 0; tp < 9; ++tp) {
-      const int pk = a.tap[tp];
-      const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
-      const char* Bi = wimg + tp * 8192;
+    if constexpr (PIPE) {
+      // a tap's 12 fragments (4 A from the halo, 8 B from the resident weights) are read before its
+      // 8 MFMAs, so the reads of a tap overlap instead of each MFMA waiting on the read just issued
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        bf16x8 fa, fb[2];
-        fa = halo_frag(halo, hbase[0] + td, 2 * s4 + lh);
+      for (int tp = 0; tp < 9; ++tp) {
+        const int pk = a.tap[tp];
+        const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+        const char* Bi = wimg + tp * 8192;
+        bf16x8 fa[4], fb[4][2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, j * 32 + lr, 2 * s4 + lh);
+        for (int s4 = 0; s4 < 4; ++s4) {
+          fa[s4] = halo_frag(halo, hbase[0] + td, 2 * s4 + lh);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[0][j] = mfma_bf16(fa, fb[j], acc[0][j]);
+          for (int j = 0; j < 2; ++j) fb[s4][j] = row_frag(Bi, j * 32 + lr, 2 * s4 + lh);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[0][j] = mfma_bf16(fa[s4], fb[s4][j], acc[0][j]);
+      }
+    } else {
+      for (int tp = 0; tp < 9; ++tp) {
+        const int pk = a.tap[tp];
+        const int td = (int)(signed char)(pk & 0xff) * HW2 + (int)(signed char)((pk >> 8) & 0xff);
+        const char* Bi = wimg + tp * 8192;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          bf16x8 fa, fb[2];
+          fa = halo_frag(halo, hbase[0] + td, 2 * s4 + lh);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fb[j] = row_frag(Bi, j * 32 + lr, 2 * s4 + lh);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[0][j] = mfma_bf16(fa, fb[j], acc[0][j]);
+        }
       }
     }
     __syncthreads();                                   // every wave is done reading this halo
@@ -1316,7 +1340,11 @@ hipError_t launch_hconv(const void* A, const void* Wm, void* Y, const void* R, f
   for (int k = 0; k < 9; ++k) a.tap[k] = taps[k];
   if (const int g64 = hconv64_grid(Bn, H, W, CA, NC)) {
     a.ntiles = 1;
-    hipLaunchKernelGGL(k_hconv64, dim3(g64), dim3(kT64), 0, st, a);
+    const char* env = getenv("PDE_HC64_PIPE");   // 0: fragment reads interleaved with the MFMAs (A/B)
+    if (env && atoi(env) == 0)
+      hipLaunchKernelGGL(k_hconv64<false>, dim3(g64), dim3(kT64), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_hconv64<true>, dim3(g64), dim3(kT64), 0, st, a);
   } else {
     const char* env = getenv("PDE_HCONV_V");   // tap-loop form (A/B): 0 hoisted addresses, 1 per tap
     const int v = env ? atoi(env) : 1;

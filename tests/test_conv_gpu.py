@@ -99,6 +99,27 @@ def test_hconv_tap_loop_forms_identical(B, C, H, W, N, monkeypatch):
     assert torch.equal(got[1][0].double().cpu(), yr)
 
 
+@pytest.mark.parametrize("B,H,W", [(4, 56, 56), (3, 17, 20)])
+def test_hconv64_read_forms_identical(B, H, W, monkeypatch):
+    """The persistent layer-1 halo conv (k_hconv64) with a tap's fragments read ahead of its MFMAs
+    (default) and interleaved with them (PDE_HC64_PIPE=0): bit-identical fprop and dgrad, exact on
+    integer data."""
+    torch.manual_seed(H + W)
+    x = cl(torch.randint(-2, 3, (B, 64, H, W), device=dev).to(torch.bfloat16))
+    w = cl(torch.randint(-1, 2, (64, 64, 3, 3), device=dev).to(torch.bfloat16))
+    dy = cl(torch.randint(-1, 2, (B, 64, H, W), device=dev).to(torch.bfloat16))
+    got = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("PDE_HC64_PIPE", v)
+        xv = x.clone().requires_grad_()
+        y = conv2d_nhwc(xv, w, 1, 1)
+        y.backward(dy)
+        got.append((y.detach(), xv.grad))
+    assert torch.equal(got[0][0], got[1][0]) and torch.equal(got[0][1], got[1][1])
+    yr = F.conv2d(x.double().cpu(), w.double().cpu(), None, 1, 1)
+    assert torch.equal(got[1][0].double().cpu(), yr)
+
+
 @pytest.mark.parametrize("N", [64, 128])
 @pytest.mark.parametrize("B,H,W", [(3, 10, 9), (2, 12, 20), (2, 9, 56), (24, 56, 56)])
 def test_conv_fprop_bn_stats(N, B, H, W):
