@@ -440,11 +440,10 @@ struct WgradArgs {
   int Bn, IH, IW, C, OH, OW, N, S, stride, pad, T;
   int P, stages_per_split, mtiles, ntiles;
   float inv_hw, inv_w;
-  int incr;             // 1: walk the B rows' (b, oh, ow) incrementally (64 / OW + 1 < 2 OH, host-checked);
-                        // 2: as 1, one walk per row group shared by its two column images
+  int incr;             // unused (the walk is the kernel's INC template flag)
 };
 
-template <int BM, int BN, int NST>
+template <int BM, int BN, int NST, bool INC>
 __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs a) {
   constexpr int WN = (BN / 64 >= 4) ? 4 : BN / 64;   // waves along the (tap, c) columns
   constexpr int WM = 4 / WN;
@@ -455,7 +454,9 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
   constexpr int LPS = AI + BI;
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
 
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  // w through readfirstlane: the compiler then knows it is wave-uniform, so every LDS-DMA destination
+  // (m0) and row-group index derived from it is scalar arithmetic instead of VALU + v_readfirstlane
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int ntile = a.mtiles * a.ntiles;
   const int split = id / ntile, rem = id % ntile;
@@ -480,41 +481,32 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
     xs_[v] = tap % a.S - a.pad;
   }
   const rsrc_t dyr = make_rsrc(a.dY, a.dy_bytes), xr = make_rsrc(a.X, a.x_bytes);
-  // B rows: the output pixel of this lane's row in each of its BI instructions, decomposed once into
-  // (b, oh, ow) and then advanced by 64 pixels per issued stage -- ow by 64 % OW, oh by 64 / OW, with at
-  // most one carry into oh and two into b (a.incr) -- instead of two reciprocal divisions per row and
-  // stage: ~10 fewer VALU per instruction in a loop that was VALU-bound (11 VALU per MFMA, PMC)
+  // B rows (INC, 64 / OW + 1 < 2 OH): instructions v and v + 2 load the same 8 pixel rows ((4 v + w) & 7)
+  // for the two 64-column images, so NR = 2 row walks serve all BI instructions.  A walk keeps
+  // (pb, poh, pow_) = (element offset of x[b][oh s][ow s][0], oh s, ow s) of its lane's row, decomposed
+  // once and advanced by 64 pixels per issued stage with uniform deltas -- wd0, + wdw on a column wrap,
+  // + wdh per row wrap (at most one carry into oh, two into b) -- and an instruction's address is the
+  // walk's offset + its per-lane tap offset toff[v] = (dr IW + ds) C + c.  No divisions and no
+  // multiplies in the loop (v_mul_lo_u32 is quarter rate): the former walk per instruction with a
+  // multiply-formed address cost ~230 VALU per 16 MFMAs (profiles/r5_models/wgrad_shared_walk/).
   const int dq64 = 64 / a.OW, dr64 = 64 - dq64 * a.OW;
-  int pb[BI], poh[BI], pow_[BI];
-  // incr == 2: instructions v and v + 2 load the same 8 pixel rows ((4 v + w) & 7) for the two 64-column
-  // images, so only NR = 2 walks are kept and each B row's address is rowbase (pixel, shared) + tap
-  // offset (per v): x[b][oh s + dr][ow s + ds][c] = X + (((b IH + oh s) IW + ow s) C + (dr IW + ds) C + c)
   constexpr int NR = BI >= 2 ? 2 : 1;
+  int pb[NR], poh[NR], pow_[NR];
   int toff[BI];
 #pragma unroll
   for (int v = 0; v < BI; ++v) toff[v] = xr_[v] > -(1 << 19) ? (xr_[v] * a.IW + xs_[v]) * a.C + xc_[v] : 0;
-  if (a.incr) {
-#pragma unroll
-    for (int v = 0; v < BI; ++v) {
-      const int p = pbeg + 8 * ((4 * v + w) & 7) + lrow;
-      const int b = p / (a.OH * a.OW), r2 = p - b * (a.OH * a.OW);
-      pb[v] = b;
-      poh[v] = r2 / a.OW;
-      pow_[v] = r2 - poh[v] * a.OW;
-    }
-  }
-  // incr == 2 keeps, per row group r < NR, (pb, poh, pow_) = (pixel-row element offset of x[b][oh s][ow s][0],
-  // oh s, ow s): the 64-pixel advance adds wd0 (+ wdw on a column wrap, + wdh per row wrap)
   const int wow = a.OW * a.stride, woh = a.OH * a.stride, wdr = dr64 * a.stride, wdq = dq64 * a.stride;
   const int wd0 = (dq64 * a.stride * a.IW + dr64 * a.stride) * a.C;
   const int wdw = (a.stride * a.IW - wow) * a.C, wdh = (a.IH - woh) * a.IW * a.C;
-  if (a.incr == 2) {
+  if constexpr (INC) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      const int ohs = poh[r] * a.stride, ows = pow_[r] * a.stride;
-      pb[r] = ((pb[r] * a.IH + ohs) * a.IW + ows) * a.C;
-      poh[r] = ohs;
-      pow_[r] = ows;
+      const int p = pbeg + 8 * ((4 * r + w) & 7) + lrow;
+      const int b = p / (a.OH * a.OW), r2 = p - b * (a.OH * a.OW);
+      const int oh = r2 / a.OW, ow = r2 - oh * a.OW;
+      poh[r] = oh * a.stride;
+      pow_[r] = ow * a.stride;
+      pb[r] = ((b * a.IH + poh[r]) * a.IW + pow_[r]) * a.C;
     }
   }
   auto issue = [&](int kt, int buf) {
@@ -527,7 +519,7 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
       const uint32_t off = (uint32_t)(p * a.N + n0 + (q >> 3) * 64 + ch * 8) * 2u;
       glds16(dyr, Ai + q * 1024, p < pend ? off : kOOB);
     }
-    if (a.incr == 2) {
+    if constexpr (INC) {
 #pragma unroll
       for (int v = 0; v < BI; ++v) {
         const int q = 4 * v + w, r = v % NR;
@@ -552,25 +544,11 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_wgrad(WgradArgs 
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
       const int q = 4 * v + w, p = p0 + 8 * (q & 7) + lrow;
-      int b, oh, ow;
-      if (a.incr) {                    // rows past P are masked below: their (b, oh, ow) may run on
-        b = pb[v];
-        oh = poh[v];
-        ow = pow_[v];
-        int nw = ow + dr64, nh = oh + dq64, nb = b;
-        if (nw >= a.OW) { nw -= a.OW; ++nh; }
-        if (nh >= a.OH) { nh -= a.OH; ++nb; }
-        if (nh >= a.OH) { nh -= a.OH; ++nb; }
-        pb[v] = nb;
-        poh[v] = nh;
-        pow_[v] = nw;
-      } else {
-        const int pp = min(p, a.P - 1);
-        b = fdiv(pp, a.OH * a.OW, a.inv_hw);
-        const int r2 = pp - b * (a.OH * a.OW);
-        oh = fdiv(r2, a.OW, a.inv_w);
-        ow = r2 - oh * a.OW;
-      }
+      const int pp = min(p, a.P - 1);  // (walk precondition 64 / OW + 1 < 2 OH fails: tiny images)
+      const int b = fdiv(pp, a.OH * a.OW, a.inv_hw);
+      const int r2 = pp - b * (a.OH * a.OW);
+      const int oh = fdiv(r2, a.OW, a.inv_w);
+      const int ow = r2 - oh * a.OW;
       const int ih = oh * a.stride + xr_[v], iw = ow * a.stride + xs_[v];
       const bool ok = p < pend && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
       const uint32_t off = (uint32_t)(((b * a.IH + ih) * a.IW + iw) * a.C + xc_[v]) * 2u;
@@ -1647,27 +1625,30 @@ hipError_t pde_conv_wgrad(const void* dy, const void* x, float* part, int splits
   a.inv_hw = 1.0f / (float)(OH * OW);
   a.inv_w = 1.0f / (float)OW;
   {
-    static const int incr_env = [] {   // PDE_WGRAD_INCR: 0 divisions, 1 a walk per instruction, 2 (default) shared
+    static const int incr_env = [] {   // PDE_WGRAD_INCR=0: per-stage divisions instead of the row walk
       const char* e = getenv("PDE_WGRAD_INCR");
-      return e == nullptr ? 2 : atoi(e);
+      return e == nullptr ? 1 : atoi(e) != 0;
     }();
     a.incr = (64 / OW + 1 < 2 * OH) ? incr_env : 0;   // <= 2 carries of oh into b per 64-pixel step
   }
   const int stages = (a.P + 63) / 64;
   a.stages_per_split = (stages + splits - 1) / splits;
   const int TC = a.T * C;
+  const bool inc = a.incr != 0;
   if (N % 128 == 0) {
     a.mtiles = N / 128; a.ntiles = (TC + 127) / 128;
+    const dim3 grid(splits * a.mtiles * a.ntiles);
     if (g_conv_nst == 2)
-      hipLaunchKernelGGL((k_wgrad<128, 128, 2>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((inc ? k_wgrad<128, 128, 2, true> : k_wgrad<128, 128, 2, false>), grid, dim3(kThreads), 0, st, a);
     else
-      hipLaunchKernelGGL((k_wgrad<128, 128, 3>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((inc ? k_wgrad<128, 128, 3, true> : k_wgrad<128, 128, 3, false>), grid, dim3(kThreads), 0, st, a);
   } else {
     a.mtiles = N / 64; a.ntiles = (TC + 127) / 128;
+    const dim3 grid(splits * a.mtiles * a.ntiles);
     if (g_conv_nst == 2)
-      hipLaunchKernelGGL((k_wgrad<64, 128, 2>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((inc ? k_wgrad<64, 128, 2, true> : k_wgrad<64, 128, 2, false>), grid, dim3(kThreads), 0, st, a);
     else
-      hipLaunchKernelGGL((k_wgrad<64, 128, 3>), dim3(splits * a.mtiles * a.ntiles), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((inc ? k_wgrad<64, 128, 3, true> : k_wgrad<64, 128, 3, false>), grid, dim3(kThreads), 0, st, a);
   }
   PDE_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)N * TC;
