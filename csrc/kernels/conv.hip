@@ -115,7 +115,7 @@ struct BnbAcc {
   // red[NW][2][BN]; threads < 2 BN write row `row` of part.  Call from every thread of the block.
   template <int CPR, int NW, int BN>
   __device__ __forceinline__ void flush(float* red, const BnbArgs& z, size_t row, int NC, int n0) {
-    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);   // w wave-uniform
 #pragma unroll
     for (int off = CPR; off < 64; off <<= 1)
 #pragma unroll
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
   constexpr int SMEM = NST * STAGE > EPIR ? NST * STAGE : EPIR;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);   // w wave-uniform
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
   // phases interleaved in the block id: each XCD (a contiguous id range, xcd_remap) gets an equal share
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   char* halo = smem;
   char* bimg = smem + HBYTES;
 
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);   // w wave-uniform
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = id % a.ntiles, mt = id / a.ntiles;
   const int b = mt / a.rtiles, rt = mt - b * a.rtiles;
@@ -898,7 +898,7 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
   static_assert(256 * RS + 2 * 8 * 64 * 4 <= HB, "epilogue scratch must fit one halo buffer");
   __shared__ __attribute__((aligned(16))) char smem[WB + 2 * HB];
   char* wimg = smem;
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);   // w wave-uniform
   const int ntile = a.Bn * a.rtiles, HW2 = a.W + 2;
   const int lrow = glds_row(l), ch = glds_chunk(l, w & 1);
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), wr = make_rsrc(a.Wg, a.w_bytes);
@@ -1098,7 +1098,7 @@ __global__ __launch_bounds__(kHwgThreads, 1) void k_hwgrad64(HwgArgs a) {
   constexpr int DG = 32, DB = DG * 1024;               // dY tile: 256 rows
   constexpr int BUF = HB + DB;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);   // w wave-uniform
   const int ntile = a.Bn * a.rtiles, HW2 = a.W + 2;
   const rsrc_t yr = make_rsrc(a.dY, a.dy_bytes), xr = make_rsrc(a.X, a.x_bytes);
   if ((int)blockIdx.x >= ntile) return;
