@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(const bf16_t* __restrict_
                                                      int ldo, float* __restrict__ LSE, int T, int H, float sl2,
                                                      float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5, r = lane & 31;
   int qt, bh;
   attn_block(T / 128, gridDim.x / (T / 128), G, true, qt, bh);   // longest (most keys) tiles first
   const int b = bh / H, hh = bh % H;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(const bf16_t* __restri
                                                         float* __restrict__ Dd, bf16_t* __restrict__ dQ, int T, int H,
                                                         float sl2, float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * 2 * TILE];  // stage: K | V
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5, r = lane & 31;
   int qt, bh;
   attn_block(T / 128, gridDim.x / (T / 128), G, true, qt, bh);   // longest (most keys) tiles first
   const int b = bh / H, hh = bh % H;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkdv(const bf16_t* __rest
                                                           bf16_t* __restrict__ dV, int T, int H, float sl2,
                                                           float scale, int G) {
   __shared__ __attribute__((aligned(16))) char lds[NST * kDkdvStage];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5, r = lane & 31;
   int kb, bh;
   attn_block(T / 128, gridDim.x / (T / 128), G, false, kb, bh);  // key tile 0 sees the most queries
   const int b = bh / H, hh = bh % H;

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const bf16_t* __restrict__ X, 
   char* wp = xin + kSInRows * kSInCols * 8;                  // [64][232] bf16
   char* stage = wp + kSC * kSWStride * 2;                    // [4 waves][32 px][64 ch] bf16
   float* wstats = reinterpret_cast<float*>(stage + 4 * 32 * 128);   // [4 waves][2][64]
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, g = l >> 5, i32 = l & 31;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), g = l >> 5, i32 = l & 31;
   const int rgroups = (OH + kSRows - 1) / kSRows;           // 4-row groups per image
   // packed weights once per block (28 KB), reused by all of its row groups
   for (int e = t; e < kSC * kSK / 8; e += 256) {
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const bf16_t* __restrict__ X
   __shared__ __attribute__((aligned(16))) char smem[kSC * kSPixStride * 2 + 7 * kSInCols * 8];
   char* dyt = smem;                                          // [64][160] bf16 (swizzled)
   char* xin = smem + kSC * kSPixStride * 2;                  // [7][230][4] bf16
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, g = l >> 5, i32 = l & 31;
+  const int t = threadIdx.x, l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), g = l >> 5, i32 = l & 31;
   const int rblocks = (OH + kSWRows - 1) / kSWRows;
   const int b = blockIdx.x / rblocks, oh_lo = (blockIdx.x - b * rblocks) * kSWRows;
   const int oh_hi = min(oh_lo + kSWRows, OH);
