@@ -65,6 +65,13 @@ def _hash_file(path, extra=""):
     return h.hexdigest()[:16]
 
 
+# Per-source extra flags.  attention.hip: no SLP vectorization -- the softmax / dS math sits between
+# MFMAs, where packed f32 ops (v_pk_mul/add/fma_f32, 206 of them from SLP packing adjacent scalar ops)
+# cost more issue time than the two scalar ops they replace (MI355X_MICROARCH.md: an anti-lever beside
+# MFMAs; profiles/r5_gpt2/attention_no_slp/)
+_FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def _targets():
     tdir, tinc, tlib, abi = _torch_paths()
     common_inc = ["-I" + os.path.join(CSRC, "include"), "-I" + _pybind_inc(), "-I" + _py_inc()]
@@ -84,7 +91,8 @@ def _targets():
                   "-l:libamdhip64.so", "-lpthread"] + rpath,
         ),
         "_kernels": dict(
-            sources=[(s, hip_dev) for s in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))]
+            sources=[(s, hip_dev + _FILE_FLAGS.get(os.path.basename(s), []))
+                     for s in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))]
             + [(os.path.join(CSRC, "ops_bindings.cpp"), torch_cpp)]
             + [(s, torch_cpp) for s in sorted(glob.glob(os.path.join(CSRC, "bind_*.cpp")))],
             link=["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-L" + tlib,
