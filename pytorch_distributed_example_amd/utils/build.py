@@ -68,8 +68,9 @@ def _hash_file(path, extra=""):
 # Per-source extra flags.  attention.hip: no SLP vectorization -- the softmax / dS math sits between
 # MFMAs, where packed f32 ops (v_pk_mul/add/fma_f32, 206 of them from SLP packing adjacent scalar ops)
 # cost more issue time than the two scalar ops they replace (MI355X_MICROARCH.md: an anti-lever beside
-# MFMAs; profiles/r5_gpt2/attention_no_slp/)
-_FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+# MFMAs; profiles/r5_gpt2/attention_no_slp/); lenet_v2.hip: the same, -45 VALU in the conv backward
+# loop (profiles/r5_lenet/lenet_no_slp/)
+_FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"], "lenet_v2.hip": ["-fno-slp-vectorize"]}
 
 
 def _targets():
