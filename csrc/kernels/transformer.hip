@@ -352,6 +352,111 @@ __global__ __launch_bounds__(256) void k_xent_bf16_reg(bf16_t* __restrict__ L, c
   }
 }
 
+// One exp per logit instead of ~2.25 (k_xent_bf16_reg: an online max/sum with per-chunk rescaling,
+// then exp(v - lse) again for the gradient; v_exp_f32 is a quarter-rate op and the kernel was
+// VALU-bound above its 3.3 GB HBM floor).  Pass 0 takes the row max M from the register-resident
+// row; pass 1 forms p = exp(v - M) once (raw v_exp_f32 of v log2e - M log2e <= 0), sums it, and keeps
+// it as packed fp16 in the row's registers (p <= 1; the gradient is rounded to bf16 in the end, the
+// fp16 step adds < 1/8 ulp of it); pass 2 writes (p / s) * scale -- no exp -- and the owner of the
+// target column then rewrites that one gradient exactly, exp(x_t - lse) - 1 (no cancellation through
+// the fp16 copy).  No per-element masking: k_xent_pad_fill first sets the vocab padding [V, Vp) of
+// every row to -inf (exp -> 0, ignored by the max), and the launcher requires Vp - V >= 8 so the
+// clamped duplicate loads of lanes past the row end are copies of a fully padded chunk.
+__global__ __launch_bounds__(256) void k_xent_pad_fill(bf16_t* __restrict__ L, int N, int Vp, int V) {
+  const int pad = Vp - V;
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= (int64_t)N * pad) return;
+  const int64_t row = i / pad;
+  L[row * Vp + V + (i - row * pad)] = (bf16_t)0xFF80u;   // -inf
+}
+
+template <int NJ>
+__global__ __launch_bounds__(256, 2) void k_xent_bf16_reg2(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt,
+                                                           int Vp, int V, float scale, float* __restrict__ loss_rows,
+                                                           int write_grad) {
+  __shared__ float shr[4], shx;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint4* Lr = reinterpret_cast<uint4*>(L + (size_t)row * Vp);
+  const int nch = Vp >> 3;
+  const int64_t t = tgt[row];
+  const bool valid = t >= 0 && t < V;
+  const int t32 = valid ? (int)t : -1;
+  const bool owner = valid && (t32 >> 3) % 256 == tid;   // this thread holds the target column
+  uint4 q[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)   // unconditional (see above); 32-bit offsets from the uniform row base
+    q[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(Lr) +
+                                           (uint32_t)min(tid + 256 * j, nch - 1) * 16u);
+  // pass 0: row max
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float v[8];
+    unpack8(q[j], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[e]);
+    __builtin_amdgcn_sched_barrier(0);               // chunk by chunk: the row stays packed (q only)
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) shr[w] = mx;
+  float xt = 0.f;
+  if (owner) {   // the target logit: one (L2-hit) load -- selecting it from q would index q dynamically
+    xt = bf2f(L[(size_t)row * Vp + t32]);                // and push the whole row array to scratch
+    shx = xt;
+  }
+  __syncthreads();
+  const float M = fmaxf(fmaxf(shr[0], shr[1]), fmaxf(shr[2], shr[3]));
+  const float L2E = 1.4426950408889634f, mb = M * L2E;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float v[8];
+    unpack8(q[j], v);
+    float pj[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pj[e] = __builtin_amdgcn_exp2f(fmaf(v[e], L2E, -mb));
+      sum += pj[e];
+    }
+    uint32_t h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      h[k] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(pj[2 * k], pj[2 * k + 1]));
+    q[j] = make_uint4(h[0], h[1], h[2], h[3]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lanes past the row end summed a duplicate of the last (fully padded, p = 0) chunk: no correction
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  __syncthreads();                                   // every wave has read the max from shr
+  if (lane == 0) shr[w] = sum;
+  __syncthreads();
+  const float s = (shr[0] + shr[1]) + (shr[2] + shr[3]);
+  const float lse = M + __logf(s);
+  if (tid == 0) loss_rows[row] = valid ? lse - shx : 0.f;
+  if (!write_grad) return;
+  const float sc = valid ? scale : 0.f, f = sc / s;
+  int tid2 = tid;                                    // opaque copy: the store offsets are recomputed
+  asm volatile("" : "+v"(tid2));                     // here, not kept live (spilled) from the loads
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = tid2 + 256 * j;
+    float g[8];
+    const uint32_t hw[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const auto hv = __builtin_bit_cast(__fp16 __attribute__((ext_vector_type(2))), hw[k]);
+      g[2 * k] = (float)hv[0] * f;
+      g[2 * k + 1] = (float)hv[1] * f;
+    }
+    if (c < nch) Lr[c] = pack8(g);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (owner) L[(size_t)row * Vp + t32] = f2bf((__expf(xt - lse) - 1.f) * sc);   // program order: after its chunk
+}
+
 __global__ __launch_bounds__(256) void k_xent_bf16(bf16_t* __restrict__ L, const int64_t* __restrict__ tgt, int Vp,
                                                    int V, float scale, float* __restrict__ loss_rows,
                                                    int write_grad) {
@@ -805,8 +910,18 @@ hipError_t pde_gelu_bwd(const void* dY, const void* X, void* dX, int64_t n, hipS
 hipError_t pde_xent_bf16(void* logits, const int64_t* tgt, int N, int Vp, int V, float scale, float* loss_rows,
                          int write_grad, hipStream_t st) {
   if ((Vp >> 3) <= 256 * 25 && Vp >= 256 * 8 * 16) {   // wide rows (GPT-2 vocab): one read, one write
-    hipLaunchKernelGGL(k_xent_bf16_reg<25>, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale,
-                       loss_rows, write_grad);
+    const char* env = getenv("PDE_XENT_V");            // 1: the two-exp online-softmax kernel (A/B)
+    // loss-only calls (write_grad = 0) keep the logits unmodified: the old kernel (no padding fill)
+    if ((env && atoi(env) == 1) || Vp - V < 8 || !write_grad)
+      hipLaunchKernelGGL(k_xent_bf16_reg<25>, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale,
+                         loss_rows, write_grad);
+    else {
+      const int64_t np = (int64_t)N * (Vp - V);
+      hipLaunchKernelGGL(k_xent_pad_fill, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, (bf16_t*)logits, N, Vp,
+                         V);
+      hipLaunchKernelGGL(k_xent_bf16_reg2<25>, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale,
+                         loss_rows, write_grad);
+    }
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_xent_bf16, dim3(N), dim3(256), 0, st, (bf16_t*)logits, tgt, Vp, V, scale, loss_rows,

@@ -406,11 +406,14 @@ def test_add_layer_norm_residual_unsupported_raises(case):
         add_layer_norm_residual(x, d, w, torch.zeros_like(w))
 
 
-def test_xent_kernel_matches_torch():
-    """Fused softmax-CE over the padded GPT-2 vocab (the 512-thread register-resident kernel): per-row
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_xent_kernel_matches_torch(variant, monkeypatch):
+    """Fused softmax-CE over the padded GPT-2 vocab (the register-resident kernels: PDE_XENT_V=1 the
+    online-softmax one, 2 = default the single-exp one with the padding pre-filled to -inf): per-row
     loss and the in-place dlogits vs fp32 torch, incl. a target in the last (masked) chunk, target 0
     and an ignored row (-1); padding columns get zero gradient."""
     from pytorch_distributed_example_amd._ext import kernels
+    monkeypatch.setenv("PDE_XENT_V", variant)
     torch.manual_seed(11)
     N, V, Vp = 64, 50257, 50304
     logits = (3 * torch.randn(N, Vp)).to(dev, torch.bfloat16)
