@@ -1010,20 +1010,38 @@ __global__ __launch_bounds__(kT64, 1) void k_hconv64(HconvArgs a) {
     float* sst = reinterpret_cast<float*>(ot + 256 * RS);   // [8][2][64]
     {
       const int i = 0;
+      // statistics only when requested (fprop; the dgrad launches have none) and the row mask only on
+      // the waves whose 32 rows run past npx (wave 7 at W = 56: 224 of 256 rows): both branches are
+      // wave-uniform, so neither costs VALU where it does not apply
+      const bool wfull = wm * 32 + 32 <= npx;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = j * 32 + lr;
-        float s1 = 0.f, s2 = 0.f;
+        bf16_t hv[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int m = wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          const bf16_t hv = f2bf(acc[i][j][q]);
-          *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv;
-          const float fv = m < npx ? bf2f(hv) : 0.f;
-          s1 += fv;
-          s2 += fv * fv;
+          hv[q] = f2bf(acc[i][j][q]);
+          *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv[q];
         }
         if (a.stats) {
+          float s1 = 0.f, s2 = 0.f;
+          if (wfull) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const float fv = bf2f(hv[q]);
+              s1 += fv;
+              s2 += fv * fv;
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const int m = wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+              const float fv = m < npx ? bf2f(hv[q]) : 0.f;
+              s1 += fv;
+              s2 += fv * fv;
+            }
+          }
           s1 += __shfl_xor(s1, 32, 64);
           s2 += __shfl_xor(s2, 32, 64);
           if (lh == 0) { sst[(wm * 2 + 0) * 64 + n] = s1; sst[(wm * 2 + 1) * 64 + n] = s2; }
