@@ -322,17 +322,21 @@ __global__ __launch_bounds__(kThreads, NST == 2 ? 2 : 1) void k_igemm(IgemmArgs 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = wn * 64 + j * 32 + lr;
-      float s1 = 0.f, s2 = 0.f;
+      bf16_t hv[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-        const bf16_t hv = f2bf(acc[i][j][q]);
-        *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv;
-        const float fv = bf2f(hv);
-        s1 += fv;
-        s2 += fv * fv;
+        hv[q] = f2bf(acc[i][j][q]);
+        *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv[q];
       }
-      if (a.stats) {
+      if (a.stats) {   // (rows past Mq are zero: their A rows were zero-filled)
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float fv = bf2f(hv[q]);
+          s1 += fv;
+          s2 += fv * fv;
+        }
         s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 32, 64);
         if (i == 0) {
@@ -829,22 +833,38 @@ __global__ __launch_bounds__(kThreads, 2) void k_hconv(HconvArgs a) {
   if (bnb) za.init(a.bnb, n0 + (t % CPR) * 8);        // lands under the tile conversion below
   char* ot = smem;
   float* sst = reinterpret_cast<float*>(smem + BM * RS);   // [WM][2][BN]
+  // statistics only when requested (the dgrad launches have none), the row mask only where this
+  // 32-row fragment runs past npx: wave-uniform branches (as k_hconv64)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = wn * 64 + j * 32 + lr;
-      float s1 = 0.f, s2 = 0.f;
+      bf16_t hv[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-        const bf16_t hv = f2bf(acc[i][j][q]);
-        *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv;
-        const float fv = m < npx ? bf2f(hv) : 0.f;
-        s1 += fv;
-        s2 += fv * fv;
+        hv[q] = f2bf(acc[i][j][q]);
+        *reinterpret_cast<bf16_t*>(ot + m * RS + n * 2) = hv[q];
       }
       if (a.stats) {
+        float s1 = 0.f, s2 = 0.f;
+        if (wm * 64 + i * 32 + 32 <= npx) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const float fv = bf2f(hv[q]);
+            s1 += fv;
+            s2 += fv * fv;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int m = wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+            const float fv = m < npx ? bf2f(hv[q]) : 0.f;
+            s1 += fv;
+            s2 += fv * fv;
+          }
+        }
         s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 32, 64);
         if (i == 0) {
