@@ -108,17 +108,22 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const bf16_t* __restrict__ X, 
       for (int q0 = 0; q0 < OW; q0 += 32) {
         const int ow = min(q0 + i32, OW - 1);
         f32x16 acc0 = {0.f}, acc1 = {0.f};
+        // a kernel row's 6 fragments (2 image, 4 weight) are read before its 4 MFMAs (counted waits)
 #pragma unroll
         for (int kh = 0; kh < 7; ++kh) {
+          bf16x8 a[2], b0[2], b1[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const bf16x8 a =
-                *reinterpret_cast<const bf16x8*>(xin + ((2 * w + kh) * kSInCols + 2 * ow + 4 * h + 2 * g) * 8);
+            a[h] = *reinterpret_cast<const bf16x8*>(xin + ((2 * w + kh) * kSInCols + 2 * ow + 4 * h + 2 * g) * 8);
             const int koff = (kh * 32 + 16 * h + 8 * g) * 2;
-            const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(wp + i32 * kSWStride * 2 + koff);
-            const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(wp + (i32 + 32) * kSWStride * 2 + koff);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, acc1, 0, 0, 0);
+            b0[h] = *reinterpret_cast<const bf16x8*>(wp + i32 * kSWStride * 2 + koff);
+            b1[h] = *reinterpret_cast<const bf16x8*>(wp + (i32 + 32) * kSWStride * 2 + koff);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[h], b0[h], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[h], b1[h], acc1, 0, 0, 0);
           }
         }
         // epilogue: D reg r -> pixel row (r&3) + 8*(r>>2) + 4*g, channel i32 (+32).  The two channels
