@@ -2131,7 +2131,9 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
     }
     return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
   } else if constexpr (C::V == 7) {
-    constexpr bool ok = !TA && !CS && (EPI == kBf16 || (EPI == kGelu && !TB));
+    // not for a transposed B either: the continuous-stream sibling of cfg 19 showed the same wrong
+    // dgrad tiles (profiles/r5_gemm/rejected_cfg19_dgrad/); such requests run cfg 18
+    constexpr bool ok = !TA && !TB && !CS && (EPI == kBf16 || EPI == kGelu);
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
         hipLaunchKernelGGL((k_gemm8pc<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
@@ -2140,7 +2142,10 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
     }
     return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
   } else if constexpr (C::V == 6) {
-    constexpr bool ok = !TA && !CS && EPI != kSlab;
+    // not for a transposed B (dgrad): the persistent transposed-B path returned wrong values in the
+    // last (ragged) row tile in 2-3 of 5 repeats at M = 9000, and once at M = 16384
+    // (profiles/r5_gemm/rejected_cfg19_dgrad/); dgrad requests for cfg 19 run cfg 18
+    constexpr bool ok = !TA && !TB && !CS && EPI != kSlab;
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && (TB || a.K % 64 == 0)) {
         hipLaunchKernelGGL((k_gemm8pp<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);

@@ -200,15 +200,19 @@ def test_gemm8p_wgrad(T, N, K, splits):
 def test_gemm8pp_persistent_bit_identical(M, N, K):
     """cfg 19, the 8-phase loop in a persistent block per CU (the next tile's prologue DMA issued before
     this tile's stores, the first K-tile's waits counting those stores in flight): bit-identical to
-    cfg 18 over many tiles per block, ragged edges, one- and two-K-tile shapes; fprop (bias, GELU) and
-    dgrad (plain, GELU backward)."""
+    cfg 18 over many tiles per block, ragged edges, one- and two-K-tile shapes; fprop (bias, GELU).
+    dgrad requests for cfg 19 run cfg 18 (the persistent transposed-B path is disabled:
+    profiles/r5_gemm/rejected_cfg19_dgrad/); the dgrad lines check that routing stays exact.  Each
+    fprop form runs 3 times (a race would show as run-to-run differences)."""
     x, w, b = _bf(M, K, seed=50), _bf(N, K, scale=0.03, seed=51), _bf(N, seed=52)
     y = G.fprop(x, w, b, cfg=19)
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
-    assert torch.equal(y, G.fprop(x, w, b, cfg=18))
-    a19, d19 = G.fprop(x, w, b, gelu=True, cfg=19)
+    y18 = G.fprop(x, w, b, cfg=18)
     a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
-    assert torch.equal(a19, a18) and torch.equal(d19, d18)
+    for _ in range(3):
+        assert torch.equal(G.fprop(x, w, b, cfg=19), y18)
+        a19, d19 = G.fprop(x, w, b, gelu=True, cfg=19)
+        assert torch.equal(a19, a18) and torch.equal(d19, d18)
     dy, w2 = _bf(M, K, seed=53), _bf(K, N, scale=0.03, seed=54)
     assert torch.equal(G.dgrad(dy, w2, cfg=19), G.dgrad(dy, w2, cfg=18))
     dg = _bf(M, N, seed=55)
@@ -220,7 +224,9 @@ def test_gemm8pp_persistent_bit_identical(M, N, K):
 def test_gemm8pc_continuous_bit_identical(M, N, K):
     """cfg 20: one K-tile stream per persistent block (the next tile's first K-tiles issued as ordinary
     look-ahead slots), register epilogue merging block pairs across lanes: bit-identical to cfg 18 for
-    fprop (with and without bias, with a scale) and dgrad, over many tiles per block and ragged edges."""
+    fprop (with and without bias), over many tiles per block and ragged edges.  dgrad requests for
+    cfg 20 run cfg 18 (the persistent transposed-B paths are disabled,
+    profiles/r5_gemm/rejected_cfg19_dgrad/); the dgrad lines check that routing stays exact."""
     x, w, b = _bf(M, K, seed=60), _bf(N, K, scale=0.03, seed=61), _bf(N, seed=62)
     y = G.fprop(x, w, b, cfg=20)
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
