@@ -65,6 +65,9 @@ def build_parser():
     ap.add_argument("--force-comm", action="store_true",
                     help="run the W>1 communication path (buckets, routes, split optimizer) even at W=1")
     ap.add_argument("--no-autotune", action="store_true", help="W>1: skip the whole-step schedule autotuning")
+    ap.add_argument("--schedule", default=None,
+                    help="force one communication schedule by its autotuner label, e.g. 'serial 431296:peer1' "
+                         "(no autotuning; traces and A/B runs)")
     ap.add_argument("--autotune-budget-s", type=float, default=60.0,
                     help="wall-clock budget of the schedule autotuner (candidates left untimed past it)")
     ap.add_argument("--prime-replays", type=int, default=3,
@@ -298,7 +301,9 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
             for _ in range(n):
                 eng.step()
 
-    if eng.comm_on and not args.no_autotune:
+    if eng.comm_on and args.schedule:
+        eng.set_schedule(args.schedule)
+    elif eng.comm_on and not args.no_autotune:
         # time every communication schedule (bucket routes x overlap) on whole steps, keep the fastest
         extra["schedule_us_per_step"] = eng.autotune_schedule(graph_steps=S, budget_s=args.autotune_budget_s)
         extra["compute_only_us_per_step"] = eng.compute_only_us   # same step, collectives left out

@@ -612,9 +612,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm2(GemmArgs a) {
 // the output of tile i drains to memory while tile i+1 computes.  Per tile, after the K loop:
 //   acc -> LDS tile (bias / scale, bf16) -> barrier -> this thread's 16-byte chunks into registers
 //   (and, GELU backward, its gelu' chunks from memory) -> barrier -> LDS-DMA of tile i+1's stage 0
-//   -> GELU math + buffer stores of tile i (masked lanes store to an out-of-range offset: the store
-//   count per wave is a compile-time constant) -> tile i+1's K loop, whose first wait leaves those
-//   NSTORE stores in flight (vmcnt counts them in issue order: they are younger than stage 0).
+//   -> GELU math of tile i in registers -> vmcnt(0) (stage 0 landed) -> buffer stores of tile i (masked
+//   lanes store to an out-of-range offset) -> tile i+1's K loop, whose first K-tile needs no wait.  (Round 5
+//   left the stores younger than stage 0 inside a vmcnt(NSTORE) allowance: unsound, k_gemm8pp.)
 // In the one-shot grid every CU wrote its tile and only then started the next block's loads; on the
 // GPT-2 shapes the writes of a round of tiles (25-200 MB) were not overlapped with any MFMA work.
 // NST = 2 stages (64-deep), K-contiguous A (TA = 0), no split-K, no bias gradient.
@@ -721,8 +721,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
     int buf = 0;
     bf16x8 fa[2][TM], fb[2][TN];
     for (int kt = 0; kt < KT; ++kt) {
-      if (kt == 0 && pending) wait_vm<NSTORE>();      // stage 0 landed; the older tile's stores may fly
-      else wait_vm<0>();
+      if (!(kt == 0 && pending)) wait_vm<0>();        // (kt == 0 behind stores: stage 0 landed before they issued)
       __builtin_amdgcn_s_barrier();
       const bool do_issue = kt + 1 < KT;
       const int nb = buf ^ 1;
@@ -812,34 +811,38 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void k_gemm_p(GemmArgs a) {
       setup(m0, n0);
       issue(0, 0);
     }
-    // ---- this tile's epilogue math and stores (NSTORE buffer stores per thread, exactly) ----
+    // ---- this tile's epilogue math (registers, under stage 0's load latency), then a vmcnt(0) that retires
+    // stage 0, then the NSTORE buffer stores: no store is ever younger than a slot a counted wait relies on
+    // (vmcnt counts loads and stores, and a store may retire before an older load; k_gemm8pp) ----
+    v4u o1[CH], o2[EPI == kGelu ? CH : 1];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
-      const uint32_t co = chunk_off(c, tm0, tn0);
       if constexpr (EPI == kBf16) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
+        o1[c] = __builtin_bit_cast(v4u, cv[c]);
       } else if constexpr (EPI == kGelu) {
-        uint32_t ya[4], da[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           pde_f2 d;
           const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
-          ya[e] = pack_bf2(y.x, y.y);
-          da[e] = pack_bf2(d.x, d.y);
+          o1[c][e] = pack_bf2(y.x, y.y);
+          o2[c][e] = pack_bf2(d.x, d.y);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
       } else {
         const uint32_t gw[4] = {gv[c].x, gv[c].y, gv[c].z, gv[c].w};
-        uint32_t r[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const pde_f2 p = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
-          r[e] = pack_bf2(p.x, p.y);
+          o1[c][e] = pack_bf2(p.x, p.y);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
       }
+    }
+    wait_vm<0>();
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const uint32_t co = chunk_off(c, tm0, tn0);
+      __builtin_amdgcn_raw_buffer_store_b128(o1[c], cr, co, 0, 0);
+      if constexpr (EPI == kGelu) __builtin_amdgcn_raw_buffer_store_b128(o2[c], c2r, co, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);                 // keep the next tile's accumulator zeroing below the stores
     if (nid >= ntile) break;
@@ -1433,13 +1436,28 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
 //   (GELU backward: its gelu' chunks loaded now) -> barrier -> the NEXT tile's six prologue slots of
 //   LDS-DMA -> this tile's GELU math + NSTORE buffer stores (masked lanes store to an out-of-range
 //   offset: a compile-time store count per wave) -> the next tile's K loop.
-// vmcnt counts in issue order, so the stores sit between the prologue slots and the loop's first
-// issues: the four phases of the first K-tile wait with NSTORE more in flight (the stores drain under
-// them), from the fifth on the count is k_gemm8p's.  What this buys over the one-shot grid on the
-// short-K GPT-2 fprops (K = 768: 12 K-tiles per tile): the block launch, the first K-tile's load
-// latency and the epilogue's store drain of every tile overlap the neighbouring tiles' MFMAs.
+// vmcnt ordering (round 6).  gfx950 has no separate store counter: vmcnt counts loads AND stores, and a
+// store may complete before an OLDER load (LLVM's SIInsertWaitcnts treats a counter with mixed pending
+// load / store events as out of order).  So a counted wait `vmcnt(n)` proves that a given LDS-DMA slot has
+// landed only if no store younger than that slot is part of the allowance n: younger stores still in
+// flight merely make the wait conservative.  Round 5 waited `vmcnt(VMW + NSTORE)` in the first K-tile,
+// counting this tile's stores (issued after the next tile's prologue) as younger work still in flight --
+// unsound when a store retires before the prologue slot: the phase then reads a slot that has not landed
+// (profiles/r6_gemm/: wrong values in the ragged last row tile of a GELU-backward dgrad, reproduced with
+// MODE 1 and made to fail at will by the MODE 2 construction; never with MODE 0 or 3).
+//   MODE 0 (production): round 5's order -- next tile's prologue, then this tile's epilogue math and stores
+//          (draining under the first K-tile) -- with every wait vmcnt(VMW): exact whatever the retire order.
+//   MODE 1: round 5's allowance (diagnostics).
+//   MODE 2: the construction: MODE 1's waits, this tile's real stores issued and drained BEFORE the
+//          prologue, and NSTORE stores of the same size to an L2-resident 128 KB scratch (C2) in their place,
+//          which retire fast -- the allowance then lets phases read LDS slots whose loads are in flight.
+//   MODE 3: epilogue math under the prologue, vmcnt(0), then the stores (no store younger than any slot;
+//          the first K-tile's waits skipped): sound, measured 2-10 % slower than MODE 0 on the GPT-2 shapes.
+// What persistence buys over the one-shot grid on the short-K GPT-2 shapes (K = 768: 12 K-tiles per
+// tile): the block launch, the first K-tile's load latency and the epilogue's store drain of every tile
+// overlap the neighbouring tiles' work.
 // TA = 0 (K-contiguous A), no split-K, no bias gradient; K % 64 == 0 when TB = 0.
-template <bool TB, int EPI>
+template <bool TB, int EPI, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
   constexpr bool TA = false;
   constexpr int WM = 2, WN = 4, TM = 8, TN = 4, NT = 512;
@@ -1464,7 +1482,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
   const int KT = (a.K + 63) >> 6;
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
   const rsrc_t cr = make_rsrc(a.C, a.c_bytes);
-  const rsrc_t c2r = make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
+  const rsrc_t c2r = MODE == 2 ? make_rsrc(a.C2, 128u << 10)
+                               : make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
   const rsrc_t xr = make_rsrc(EPI == kGeluBwd ? (const void*)a.aux : a.C, EPI == kGeluBwd ? a.c_bytes : 0);
   const uint32_t astep = 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
   const int lrow = glds_row(l);
@@ -1553,8 +1572,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
     bf16x8 fa[4][2], fb[TN][2];
     if (KT > 0) {
       if (KT > 1) {
-        if (pend) wait_vm<VMW + NSTORE>();
-        else wait_vm<VMW>();
+        if (!pend) wait_vm<VMW>();
+        else if constexpr (MODE == 1 || MODE == 2) wait_vm<VMW + NSTORE>();
+        else if constexpr (MODE == 0) wait_vm<VMW>();
+        // MODE 3 with stores pending: every prologue slot landed before they were issued
       } else {
         wait_vm<0>();
       }
@@ -1592,8 +1613,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
         else if constexpr (PH == 3) issue(0, kt + 2);
         else issue(2, kt + 2);
         if (kt + 2 < KT) {
-          if (p0) wait_vm<VMW + NSTORE>();      // the previous tile's stores are still older than this slot
-          else wait_vm<VMW>();
+          if (!p0) {
+            wait_vm<VMW>();
+          } else if constexpr (MODE == 3) {
+            // first K-tile behind the stores: the slot this wait retires was issued 4 (TB: 3) phases
+            // earlier -- a prologue slot, landed before the stores issued -- except TB's phase 4, whose
+            // slot phase 1 issued after the stores (older than it: vmcnt(VMW) is exact)
+            if constexpr (TB && PH == 4) wait_vm<VMW>();
+          } else if constexpr (MODE == 0) {
+            wait_vm<VMW>();                     // this tile's stores, if still in flight, only add to the count
+          } else {
+            wait_vm<VMW + NSTORE>();            // round 5: unsound if a store retires before this slot
+          }
         } else {
           wait_vm<0>();
         }
@@ -1665,6 +1696,52 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
       for (int c = 0; c < CH; ++c) gv[c] = bload16(xr, chunk_off(c, m0, n0));   // before the next tile's DMA
     }
     const int tm0 = m0, tn0 = n0;
+    // ---- this tile's epilogue math (registers; the stores are issued below) ----
+    v4u o1[CH], o2[EPI == kGelu ? CH : 1];
+    auto math = [&]() {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
+        if constexpr (EPI == kBf16) {
+          o1[c] = __builtin_bit_cast(v4u, cv[c]);
+        } else if constexpr (EPI == kGelu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            pde_f2 d;
+            const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
+            o1[c][e] = pack_bf2(y.x, y.y);
+            o2[c][e] = pack_bf2(d.x, d.y);
+          }
+        } else {
+          const uint32_t gw[4] = {gv[c].x, gv[c].y, gv[c].z, gv[c].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
+            o1[c][e] = pack_bf2(pr.x, pr.y);
+          }
+        }
+      }
+    };
+    // NSTORE buffer stores per thread, exactly (masked lanes store to an out-of-range offset); MODE 2's
+    // decoys: the same count into the 128 KB scratch behind C2 (every block the same lines: L2 hits)
+    auto stores = [&](bool decoy) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        if (decoy) {
+          __builtin_amdgcn_raw_buffer_store_b128(o1[c], c2r, (uint32_t)(tv + c * NT) * 16u, 0, 0);
+          continue;
+        }
+        const uint32_t co = chunk_off(c, tm0, tn0);
+        if (EPI == kBf16 && a.ntc) __builtin_amdgcn_raw_buffer_store_b128(o1[c], cr, co, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(o1[c], cr, co, 0, 0);
+        if constexpr (EPI == kGelu) __builtin_amdgcn_raw_buffer_store_b128(o2[c], c2r, co, 0, 0);
+      }
+    };
+    if constexpr (MODE == 2) {                     // construction: the real stores retire before the prologue
+      math();
+      stores(false);
+      wait_vm<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                  // the LDS tile is free: the next tile's slots may land
     const int nid = id + P;
@@ -1673,35 +1750,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
       setup(m0, n0);
       if (KT > 0) prologue();
     }
-    // ---- this tile's epilogue math and stores (NSTORE buffer stores per thread, exactly) ----
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const uint32_t wv[4] = {cv[c].x, cv[c].y, cv[c].z, cv[c].w};
-      const uint32_t co = chunk_off(c, tm0, tn0);
-      if constexpr (EPI == kBf16) {
-        if (a.ntc) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 2);
-        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, cv[c]), cr, co, 0, 0);
-      } else if constexpr (EPI == kGelu) {
-        uint32_t ya[4], da[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pde_f2 d;
-          const pde_f2 y = gelu2_d(pde_f2{bf_lo(wv[e]), bf_hi(wv[e])}, d);
-          ya[e] = pack_bf2(y.x, y.y);
-          da[e] = pack_bf2(d.x, d.y);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{ya[0], ya[1], ya[2], ya[3]}, cr, co, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{da[0], da[1], da[2], da[3]}, c2r, co, 0, 0);
-      } else {
-        const uint32_t gw[4] = {gv[c].x, gv[c].y, gv[c].z, gv[c].w};
-        uint32_t r[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const pde_f2 pr = pde_f2{bf_lo(wv[e]), bf_hi(wv[e])} * pde_f2{bf_lo(gw[e]), bf_hi(gw[e])};
-          r[e] = pack_bf2(pr.x, pr.y);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{r[0], r[1], r[2], r[3]}, cr, co, 0, 0);
-      }
+    if constexpr (MODE == 2) {
+      stores(true);                                // NSTORE decoy stores where round 5 counted the real ones
+    } else {
+      math();                                      // under the prologue's load latency
+      if constexpr (MODE == 3) wait_vm<0>();       // every prologue slot landed: no store is younger than a
+                                                   // slot a later counted wait relies on
+      stores(false);
     }
     __builtin_amdgcn_sched_barrier(0);             // keep the next tile's accumulator zeroing below the stores
     if (nid >= ntile) break;
@@ -1718,9 +1773,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
 // (the stage buffers stay in use): each lane holds four consecutive columns of every 16x16 accumulator,
 // so two horizontally adjacent blocks are merged across the lane pair that holds the other half of each
 // 8-column group (one 64-lane shuffle per 8 bytes) and every lane stores one 16-byte chunk per block pair
-// (bias, scale and GELU applied in registers).  vmcnt counts in issue order: those NS stores sit behind
-// the four look-ahead slots in flight, so the first K-tile of the next tile waits with NS more
-// outstanding and the stores drain under its MFMAs.
+// (bias, scale and GELU applied in registers).  vmcnt ordering as k_gemm8pp (a store never in a counted
+// wait's allowance): MODE 0 waits vmcnt(VMW) everywhere, the NS stores in flight only adding to the
+// count.  MODE 1: round 5's vmcnt(VMW + NS) allowance (diagnostics); MODE 3: outputs computed in registers,
+// the look-ahead slots in flight retired with vmcnt(0), then the stores (the next tile's first waits,
+// which would retire those pre-store slots, skipped but TB's phase 4).
 // TA = 0, no split-K / bias gradient, epilogues bf16 and bias + GELU; K % 128 == 0 (an even K-tile count
 // keeps every tile starting on LDS buffer 0).
 //
@@ -1728,7 +1785,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
 // instructions per wave), B1 = n-block 2 (one); phases 2 and 3 run the single n-block 2 (8 MFMAs); any four
 // consecutive phases still issue one slot of each region, so the counted wait keeps 1 + 2 + 2 + 2 = 7
 // instructions in flight; the third accumulator column has no merge partner and is stored 8 bytes per lane.
-template <bool TB, int EPI, int TN = 4>
+template <bool TB, int EPI, int TN = 4, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
   constexpr bool TA = false;
   constexpr int WM = 2, WN = 4, TM = 8;
@@ -1894,8 +1951,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       else if constexpr (PH == 3) issue(0, jt, kn);
       else issue(2, jt, kn);
       if (gj + c + 2 < total) {
-        if (p0) wait_vm<VMW + NS>();            // the previous tile's stores are older than this slot
-        else wait_vm<VMW>();
+        if (!p0) {
+          wait_vm<VMW>();
+        } else if constexpr (MODE == 3) {
+          if constexpr (TB && PH == 4) wait_vm<VMW>();   // the slot phase 1 issued after the stores
+          // else: retires a look-ahead slot that landed before the stores issued
+        } else if constexpr (MODE == 0) {
+          wait_vm<VMW>();
+        } else {
+          wait_vm<VMW + NS>();                  // round 5: unsound if a store retires before this slot
+        }
       } else {
         wait_vm<0>();                           // end of the stream: fewer slots in flight, drain
       }
@@ -1935,8 +2000,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
       else coords(j + 2, m0e, n0e);
     }
     const int row0 = m0 + wm * WTM + mrow, col0 = n0 + wn * WTN + (pcol & 8);
+    constexpr int NP = TN / 2, NQ = EPI == kGelu ? 2 : 1;
+    v4u ov[TM * NP * NQ];                          // outputs first (registers), stores after the drain
+    uint32_t oo[TM * NP];
+    v2u ol[TN % 2 ? TM * NQ : 1];
+    uint32_t olo[TN % 2 ? TM : 1];
 #pragma unroll
-    for (int jp = 0; jp < TN / 2; ++jp) {
+    for (int jp = 0; jp < NP; ++jp) {
       float bv0[4] = {0.f, 0.f, 0.f, 0.f}, bv1[4] = {0.f, 0.f, 0.f, 0.f};
       const int nb = n0 + wn * WTN + 32 * jp + pcol;
       if (has_bias && nb < a.N) unpack4(*reinterpret_cast<const uint2*>(a.bias + nb), bv0);
@@ -1951,16 +2021,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
           v0[e] = (acc[i][2 * jp][e] + bv0[e]) * sc;
           v1[e] = (acc[i][2 * jp + 1][e] + bv1[e]) * sc;
         }
-        const uint32_t off = (row < a.M && col < a.N) ? (uint32_t)(((size_t)row * a.ldc + col) * 2) : kOOB;
-        auto emit = [&](const uint2 u0, const uint2 u1, rsrc_t rs) {
-          // lower lane: block 2jp (own low half + partner's high half); upper: block 2jp+1
+        oo[jp * TM + i] = (row < a.M && col < a.N) ? (uint32_t)(((size_t)row * a.ldc + col) * 2) : kOOB;
+        // lower lane: block 2jp (own low half + partner's high half); upper: block 2jp+1
+        auto merge = [&](const uint2 u0, const uint2 u1) -> v4u {
           const uint2 send = lower ? u1 : u0;
           const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, XM, 64), (uint32_t)__shfl_xor((int)send.y, XM, 64));
-          const v4u out = lower ? v4u{u0.x, u0.y, recv.x, recv.y} : v4u{recv.x, recv.y, u1.x, u1.y};
-          __builtin_amdgcn_raw_buffer_store_b128(out, rs, off, 0, 0);
+          return lower ? v4u{u0.x, u0.y, recv.x, recv.y} : v4u{recv.x, recv.y, u1.x, u1.y};
         };
         if constexpr (EPI == kBf16) {
-          emit(pack4(v0), pack4(v1), cr);
+          ov[jp * TM + i] = merge(pack4(v0), pack4(v1));
         } else {
           // GELU of the bf16-rounded pre-activation, as the LDS epilogues of cfgs 17-19 compute it
           const uint2 p0 = pack4(v0), p1 = pack4(v1);
@@ -1976,8 +2045,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
             y1[e] = pack_bf2(y.x, y.y);
             d1[e] = pack_bf2(d.x, d.y);
           }
-          emit(make_uint2(y0[0], y0[1]), make_uint2(y1[0], y1[1]), cr);
-          emit(make_uint2(d0[0], d0[1]), make_uint2(d1[0], d1[1]), c2r);
+          ov[2 * (jp * TM + i)] = merge(make_uint2(y0[0], y0[1]), make_uint2(y1[0], y1[1]));
+          ov[2 * (jp * TM + i) + 1] = merge(make_uint2(d0[0], d0[1]), make_uint2(d1[0], d1[1]));
         }
       }
     }
@@ -1992,10 +2061,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = (acc[i][jl][e] + bvl[e]) * sc;
-        const uint32_t off = (row < a.M && nl < a.N) ? (uint32_t)(((size_t)row * a.ldc + nl) * 2) : kOOB;
+        olo[i] = (row < a.M && nl < a.N) ? (uint32_t)(((size_t)row * a.ldc + nl) * 2) : kOOB;
         const uint2 pv = pack4(v);
         if constexpr (EPI == kBf16) {
-          __builtin_amdgcn_raw_buffer_store_b64(v2u{pv.x, pv.y}, cr, off, 0, 0);
+          ol[i] = v2u{pv.x, pv.y};
         } else {
           const uint32_t wv[2] = {pv.x, pv.y};
           uint32_t y[2], d2[2];
@@ -2006,9 +2075,22 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pc(GemmArgs a) {
             y[e] = pack_bf2(yy.x, yy.y);
             d2[e] = pack_bf2(d.x, d.y);
           }
-          __builtin_amdgcn_raw_buffer_store_b64(v2u{y[0], y[1]}, cr, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(v2u{d2[0], d2[1]}, c2r, off, 0, 0);
+          ol[2 * i] = v2u{y[0], y[1]};
+          ol[2 * i + 1] = v2u{d2[0], d2[1]};
         }
+      }
+    }
+    if constexpr (MODE == 3) wait_vm<0>();       // the look-ahead slots in flight land before any store issues
+#pragma unroll
+    for (int q = 0; q < TM * NP; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b128(ov[q * NQ], cr, oo[q], 0, 0);
+      if constexpr (NQ == 2) __builtin_amdgcn_raw_buffer_store_b128(ov[q * NQ + 1], c2r, oo[q], 0, 0);
+    }
+    if constexpr (TN % 2) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __builtin_amdgcn_raw_buffer_store_b64(ol[i * NQ], cr, olo[i], 0, 0);
+        if constexpr (NQ == 2) __builtin_amdgcn_raw_buffer_store_b64(ol[i * NQ + 1], c2r, olo[i], 0, 0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);           // keep the next tile's accumulator zeroing below the stores
@@ -2093,6 +2175,10 @@ template <> struct Cfg<22> { static constexpr int V = 9, TM = 8, TN = 3, WM = 2,
 constexpr int kNumCfg = 23;
 
 int g_num_cu = 0;
+// persistent GEMM store-ordering mode (k_gemm8pp's header) from GemmArgs::dbg bits 8-9: 0 production
+// (exact waits), 1 round 5's allowance, 2 its failure construction (C2: a 128 KB scratch), 3 drain-before-
+// stores (diagnostics / A/B only)
+int gemm_mode(const GemmArgs& a) { return (a.dbg >> 8) & 3; }
 int num_cu() {
   if (g_num_cu == 0) {
     int dev = 0, n = 0;
@@ -2125,30 +2211,48 @@ hipError_t launch_cfg(GemmArgs& a, int splits, hipStream_t st) {
     constexpr bool ok = !TA && !TB && !CS && (EPI == kBf16 || EPI == kGelu);
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
-        hipLaunchKernelGGL((k_gemm8pc<false, EPI, 3>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        const dim3 g(std::min(grid, num_cu()));
+        switch (gemm_mode(a)) {
+          case 1: hipLaunchKernelGGL((k_gemm8pc<false, EPI, 3, 1>), g, dim3(512), 0, st, a); break;
+          case 3: hipLaunchKernelGGL((k_gemm8pc<false, EPI, 3, 3>), g, dim3(512), 0, st, a); break;
+          default: hipLaunchKernelGGL((k_gemm8pc<false, EPI, 3, 0>), g, dim3(512), 0, st, a); break;
+        }
         return hipGetLastError();
       }
     }
     return launch_cfg<16, TA, TB, EPI, CS>(a, splits, st);
   } else if constexpr (C::V == 7) {
-    // not for a transposed B either: the continuous-stream sibling of cfg 19 showed the same wrong
-    // dgrad tiles (profiles/r5_gemm/rejected_cfg19_dgrad/); such requests run cfg 18
-    constexpr bool ok = !TA && !TB && !CS && (EPI == kBf16 || EPI == kGelu);
+    // dgrad (TB) re-enabled in round 6 with the store-ordering fix (k_gemm8pp's header)
+    constexpr bool ok = !TA && !CS && (EPI == kBf16 || EPI == kGelu) && !(TB && EPI == kGelu);
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && a.K % 128 == 0 && a.K >= 128) {
-        hipLaunchKernelGGL((k_gemm8pc<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        const dim3 g(std::min(grid, num_cu()));
+        switch (gemm_mode(a)) {
+          case 1: hipLaunchKernelGGL((k_gemm8pc<TB, EPI, 4, 1>), g, dim3(512), 0, st, a); break;
+          case 3: hipLaunchKernelGGL((k_gemm8pc<TB, EPI, 4, 3>), g, dim3(512), 0, st, a); break;
+          default: hipLaunchKernelGGL((k_gemm8pc<TB, EPI, 4, 0>), g, dim3(512), 0, st, a); break;
+        }
         return hipGetLastError();
       }
     }
     return launch_cfg<19, TA, TB, EPI, CS>(a, splits, st);
   } else if constexpr (C::V == 6) {
-    // not for a transposed B (dgrad): the persistent transposed-B path returned wrong values in the
-    // last (ragged) row tile in 2-3 of 5 repeats at M = 9000, and once at M = 16384
-    // (profiles/r5_gemm/rejected_cfg19_dgrad/); dgrad requests for cfg 19 run cfg 18
-    constexpr bool ok = !TA && !TB && !CS && EPI != kSlab;
+    // dgrad (TB) re-enabled in round 6 with the store-ordering fix (k_gemm8pp's header)
+    constexpr bool ok = !TA && !CS && EPI != kSlab;
     if constexpr (ok) {
       if (splits == 1 && a.c_bytes < kOOB && (TB || a.K % 64 == 0)) {
-        hipLaunchKernelGGL((k_gemm8pp<TB, EPI>), dim3(std::min(grid, num_cu())), dim3(512), 0, st, a);
+        const dim3 g(std::min(grid, num_cu()));
+        switch (gemm_mode(a)) {
+          case 1: hipLaunchKernelGGL((k_gemm8pp<TB, EPI, 1>), g, dim3(512), 0, st, a); break;
+          case 2:
+            if constexpr (EPI == kBf16) {
+              hipLaunchKernelGGL((k_gemm8pp<TB, EPI, 2>), g, dim3(512), 0, st, a);
+              break;
+            }
+            [[fallthrough]];
+          case 3: hipLaunchKernelGGL((k_gemm8pp<TB, EPI, 3>), g, dim3(512), 0, st, a); break;
+          default: hipLaunchKernelGGL((k_gemm8pp<TB, EPI, 0>), g, dim3(512), 0, st, a); break;
+        }
         return hipGetLastError();
       }
     }

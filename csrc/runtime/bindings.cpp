@@ -251,5 +251,6 @@ PYBIND11_MODULE(_runtime, m) {
       .def("set_timeout_ms", &PeerAllReduce::set_timeout_ms)
       .def("set_one_shot_max_bytes", &PeerAllReduce::set_one_shot_max_bytes)
       .def("set_max_blocks", &PeerAllReduce::set_max_blocks)
+      .def("set_ip_block_cap", &PeerAllReduce::set_ip_block_cap)
       .def("close", &PeerAllReduce::close, py::call_guard<py::gil_scoped_release>());
 }

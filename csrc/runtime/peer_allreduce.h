@@ -89,6 +89,11 @@ class PeerAllReduce {
   void set_timeout_ms(int64_t ms) { timeout_ticks_ = ms * 100000; }   // s_memrealtime runs at 100 MHz
   void set_one_shot_max_bytes(int64_t b) { one_shot_max_ = b; }
   void set_max_blocks(int b) { max_blocks_ = b < 1 ? 1 : (b > kPeerMaxBlocks ? kPeerMaxBlocks : b); }
+  // in-place one-shot grid cap: ranks time-sharing ONE GPU need every rank's spinning grid co-resident
+  // (a grid that cannot be placed until another rank's spinning blocks exit deadlocks until the barrier
+  // time-out), so dist/peer.py sets 256 / (ranks on this device) there; a call that does not fit runs
+  // two-shot (same fixed rank order: bit-identical results)
+  void set_ip_block_cap(int b) { ip_block_cap_ = b < 1 ? 1 : (b > kPeerMaxBlocks ? kPeerMaxBlocks : b); }
   // In-place registered form.  register_buffer returns the bytes (IPC handle of the allocation's base |
   // int64 offset of `ptr` in it) peers pass to open_registered; returns the registration id through
   // `id` (the same on every rank when every rank registers in the same order).
@@ -132,6 +137,7 @@ class PeerAllReduce {
   int64_t timeout_ticks_ = 10LL * 100000000;   // 10 s
   int64_t one_shot_max_ = 256 * 1024;
   int max_blocks_ = 64;
+  int ip_block_cap_ = kPeerMaxBlocks;
   int debug_skip_stage_ = 0;
 };
 

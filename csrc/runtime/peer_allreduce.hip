@@ -385,7 +385,17 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
   const bool tail_lane = blockIdx.x == 0 && threadIdx.x < a.tail;
   float tail_sum = 0.f;
 
-  ip_barrier<W, false, true>(a, 0, target, failed, &s_bad);   // A: every rank's buffer holds its input
+  // A: every rank's buffer holds its input.  No release is needed in front of the signal: the input was
+  // written by EARLIER kernels of this stream, and the kernel boundary between them and this launch is
+  // at least an agent-scope release -- on gfx950 `buffer_wbl2 sc1`, which writes every XCD L2's dirty
+  // lines back to memory (the eight XCD L2s are not coherent with each other, so agent scope already
+  // means memory-side visibility: MI355X_MICROARCH.md, inter-workgroup visibility).  Peers read with
+  // sc0 sc1 (system-coherent) loads that are served from memory / MALL over xGMI, never from this
+  // rank's L2.  (A fence here would only write back the XCD this block runs on, not the producer's.)
+  // The results are plain stores: their readers are this rank's own later kernels, and the peers read
+  // this range again only after the next call's barrier A, behind the same kernel-boundary release.
+  // The registration self-test (dist/peer.py) exercises exactly this producer -> in-place hand-off.
+  ip_barrier<W, false, true>(a, 0, target, failed, &s_bad);
   if (tail_lane) {                                      // trailing elements: read now, written after B
     const int tb = (int)((tail_off + threadIdx.x) * ESZ);
 #pragma unroll
@@ -816,6 +826,7 @@ void PeerAllReduce::all_reduce_registered(int id, int64_t off, int64_t count, in
     if (algo == 1) throw std::invalid_argument("in-place one-shot holds at most 8 MB per call");
     two = true;
   }
+  if (!two && a.n4 > (int64_t)ip_block_cap_ * kThreads * 4) two = true;   // shared-GPU grid cap (header)
   a.chunk4 = two ? (a.n4 + world_ - 1) / world_ : a.n4;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int64_t u = 1, nb;
@@ -826,7 +837,7 @@ void PeerAllReduce::all_reduce_registered(int id, int64_t off, int64_t count, in
     nb = (a.chunk4 + kThreads - 1) / kThreads;
     nb = nb < 1 ? 1 : (nb > max_blocks_ ? max_blocks_ : nb);
   } else {
-    while (u < 4 && (u < u_max || a.n4 > (int64_t)kPeerMaxBlocks * kThreads * u)) u *= 2;
+    while (u < 4 && (u < u_max || a.n4 > (int64_t)ip_block_cap_ * kThreads * u)) u *= 2;
     nb = (a.n4 + kThreads * u - 1) / (kThreads * u);
     nb = nb < 1 ? 1 : nb;
   }

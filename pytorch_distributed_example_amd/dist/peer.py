@@ -73,6 +73,7 @@ class PeerAllReduce:
         self.reason = ""
         self.reg_reason = ""
         self._regs = []          # (data_ptr, numel, registration id, tensor kept alive)
+        self.shared = 1
         _SEQ[0] += 1
         key = f"{group.prefix}/peer_ar/{_SEQ[0]}"
         err = ""
@@ -99,6 +100,13 @@ class PeerAllReduce:
                     if d != me and not torch.cuda.can_device_access_peer(me, d):
                         raise RuntimeError(f"cuda:{me} cannot access peer cuda:{d}")
                 self.native.open(handles)
+                self.shared = devs.count(me)       # ranks time-sharing this GPU (1 on a real node)
+                if self.shared > 1:
+                    # every sharing rank's spinning grid must be co-resident (else a rank's kernel waits
+                    # for CUs that another rank's blocks hold while they wait for it: a deadlock until
+                    # the barrier time-out -- seen with 8 ranks on one GPU)
+                    self.native.set_max_blocks(max(1, min(64, 256 // self.shared)))
+                    self.native.set_ip_block_cap(max(1, 256 // self.shared))
             except Exception as e:   # noqa: BLE001
                 err = f"open: {e}"
         ok = _host_allreduce_min(group, 0 if err else 1)
@@ -187,6 +195,9 @@ class PeerAllReduce:
             return (((i * 7 + c * 13 + rank * 5) % 17) - 8).to(buf.dtype)
 
         s = torch.cuda.current_stream(self.device)
+        # the test runs on the live buffer (the registration covers exactly it): whatever it holds --
+        # e.g. gradients accumulated before a DDP wrapper was built -- is restored afterwards
+        saved = buf.detach().clone()
         for n in sorted({1, 5, 4099, min(n_all, 70001), n_all - (n_all % per)}):
             if n <= 0 or n > n_all:
                 continue
@@ -205,7 +216,9 @@ class PeerAllReduce:
                     if not torch.equal(buf[off:off + n], want):
                         bad = int((buf[off:off + n] != want).sum())
                         raise RuntimeError(f"algo {algo} n={n} off={off} call {c}: {bad} wrong elements")
-        buf.zero_()
+        buf.copy_(saved)
+        torch.cuda.synchronize(self.device)
+        del saved
 
     @property
     def capacity_bytes(self) -> int:

@@ -562,6 +562,18 @@ class LeNetTrainStep:
             pack_conv2_weight(self.p["conv2.weight"], self.Wt2)
 
     # ------------------------------------------------------------------ schedule autotuning (W > 1)
+    def set_schedule(self, label: str):
+        """Force one schedule by its autotuner label, e.g. ``"serial 431296:peer1"`` or
+        ``"overlap2 25664:peer1,405632:rccl"`` (mode, then bucket numel:route pairs); identically on
+        every rank (traces / A/B runs)."""
+        mode, _, rest = label.strip().partition(" ")
+        routes = {int(n): r for n, r in (kv.split(":") for kv in rest.split(",") if kv)}
+        if mode not in ("overlap", "overlap2", "flat", "serial", "fused", "none"):
+            raise ValueError(f"unknown schedule mode {mode!r}")
+        self.mode = mode
+        self.comm.routes = routes
+        self.graphs.clear()
+
     def schedule_candidates(self):
         """(mode, {bucket numel: route}) pairs the comm path can run: bucketed + overlapped with the
         conv backward (one route per bucket), or one all-reduce after backward on the comm stream

@@ -75,7 +75,7 @@ def _loss_fn(output, label):
 
 class Trainer(object):
     def __init__(self, net, optimizer, train_loader, test_loader, device, distributed, do_eval,
-                 manual_average: bool = False):
+                 manual_average: bool = False, autocast_dtype=None):
         self.net = net
         self.optimizer = optimizer
         self.train_loader = train_loader
@@ -84,7 +84,19 @@ class Trainer(object):
         self.distributed = distributed
         self.do_eval = do_eval
         self.manual_average = manual_average    # reference path: per-parameter all-reduce after backward
+        # mixed precision (``--dtype bf16``): forward + loss under torch.autocast, fp32 parameters,
+        # gradients and optimizer state (the loss itself is computed from fp32 logits)
+        self.autocast_dtype = autocast_dtype
         self.printer = print
+
+    def _forward(self, data, label):
+        if self.autocast_dtype is None:
+            output = self.net(data)
+            return output, _loss_fn(output, label)
+        with torch.autocast(device_type=self.device.type, dtype=self.autocast_dtype):
+            output = self.net(data)
+        output = output.float()
+        return output, _loss_fn(output, label)
 
     def fit(self, epochs, start_epoch: int = 0):
         """Epochs ``start_epoch+1 .. epochs`` (a resumed run passes the checkpoint's epoch, so the
@@ -114,8 +126,7 @@ class Trainer(object):
             label = label.to(self.device)
 
             with prof.range("forward"):
-                output = self.net(data)
-                loss = _loss_fn(output, label)
+                output, loss = self._forward(data, label)
 
             self.optimizer.zero_grad()
             with prof.range("backward"):
@@ -142,8 +153,7 @@ class Trainer(object):
                 data = data.to(self.device)
                 label = label.to(self.device)
 
-                output = self.net(data)
-                loss = _loss_fn(output, label)
+                output, loss = self._forward(data, label)
 
                 test_loss.update(loss, data.size(0))
                 test_acc.update(output, label)

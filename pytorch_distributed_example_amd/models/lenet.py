@@ -6,12 +6,16 @@ Parameter names, shapes, registration order and initialisation are identical to 
 Execution:
 * GPU input  -> one fused HIP autograd Function (``ops.LeNetFunction``: 4 forward launches, 3 backward)
 * CPU input  -> the layer-by-layer ATen CPU path (the reference's ``--no-cuda`` mode)
+* ``net.aten = True`` -> the same layer-by-layer path through ``torch.nn.functional`` on any device,
+  which ``torch.autocast`` can lower to bf16 (``scripts/mnist.py --dtype bf16``: the framework's
+  toy-CNN kernels are fp32, the reference's dtype)
 The high-throughput trainer (``engine.LeNetTrainStep``) runs the same kernels without autograd
 and fuses the loss and the optimizer into the step.
 """
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn as tnn
 
 from .. import ops
@@ -37,8 +41,14 @@ class Net(tnn.Module):
         self.conv2 = Conv2d(20, 50, 5, 1)
         self.fc1 = Linear(4 * 4 * 50, 500)
         self.fc2 = Linear(500, 10)
+        self.aten = False
 
     def forward(self, x):
+        if self.aten:
+            x = F.max_pool2d(F.relu(F.conv2d(x, self.conv1.weight, self.conv1.bias)), 2, 2)
+            x = F.max_pool2d(F.relu(F.conv2d(x, self.conv2.weight, self.conv2.bias)), 2, 2)
+            x = F.relu(F.linear(x.reshape(-1, 4 * 4 * 50), self.fc1.weight, self.fc1.bias))
+            return F.log_softmax(F.linear(x, self.fc2.weight, self.fc2.bias), dim=1)
         if x.is_cuda:
             return ops.lenet_forward(x, self)
         x = ops.relu(self.conv1(x))

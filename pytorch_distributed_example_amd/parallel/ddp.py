@@ -130,6 +130,7 @@ class DistributedDataParallel(nn.Module):
         self._stage = None
         self._bcast = None
         self._peer = None
+        self.peer_algo = {}            # bucket numel -> 1 (one-shot) / 2 (two-shot) for the in-place route
         self.peer_inplace = False
         self.peer_reason = ""
         want_peer = (reduce_route in ("auto", "peer") and self.comm_on and self.device.type == "cuda"
@@ -330,9 +331,14 @@ class DistributedDataParallel(nn.Module):
         if reg is not None:
             rid, off = reg
             n, scale = view.numel(), 1.0 / self.world_size
+            # one- / two-shot per bucket size: a tuned choice (peer_algo[numel] = 1 / 2, e.g. from
+            # dist.peer.tune_routes), else one-shot (one barrier pair, W reads per element) for buckets
+            # up to 256 KB -- at most 32 blocks, so its spinning blocks never crowd out a co-resident
+            # kernel of a rank sharing the GPU -- and two-shot (64-block cap) above
+            algo = self.peer_algo.get(n, 1 if n * esz <= (256 << 10) else 2)
 
             def fn_ip(stream):
-                pk.native.all_reduce_registered(rid, off, n, esz, scale, 2, stream)
+                pk.native.all_reduce_registered(rid, off, n, esz, scale, algo, stream)
             return dist.gpu_launch(self.process_group, [view], fn_ip, async_op=True, what="ddp peer all-reduce")
         chunk = max(8, (pk.capacity_bytes // esz) // 8 * 8)
         n = view.numel()

@@ -14,7 +14,10 @@ Additive flags: --engine {auto,fused,autograd}, --ddp {on,off} (off = the refere
 ``average_gradients``), --model {net,mlp}, --optimizer {adam,sgd}, --seed, --train-size,
 --test-size, --save/--resume (state_dict compatible), --cprofile PATH (default ./stats, like the
 reference's always-on cProfile wrapper; --no-cprofile turns it off), --metrics PATH (JSONL),
---log-rank0-only, --no-graph, --set-epoch.
+--log-rank0-only, --no-graph, --set-epoch, --bucket-mb (DDP gradient bucket cap, autograd engine),
+--dtype {fp32,bf16} (bf16: torch.autocast mixed precision over the ATen layer path with fp32
+parameters, gradients and optimizer state; the fused engine and the framework's toy-CNN kernels are
+fp32, the reference's dtype).
 """
 import argparse
 import cProfile
@@ -106,6 +109,11 @@ def run(args):
 
     distributed = False if world == 1 else True
     engine = args.engine
+    if args.dtype == "bf16":
+        if engine == "fused":
+            raise SystemExit("--dtype bf16 needs --engine autograd (the fused toy-CNN engine is fp32)")
+        engine = "autograd"
+        net.aten = True                  # the layer path through torch.nn.functional, autocast to bf16
     if engine == "auto":
         engine = "fused" if (device.type == "cuda" and args.model == "net" and
                              (not distributed or dist.get_backend() in ("nccl", "rccl"))) else "autograd"
@@ -133,14 +141,15 @@ def run(args):
     else:
         model = net
         if distributed and args.ddp == "on":
-            model = DistributedDataParallel(net, init_sync=False)
+            model = DistributedDataParallel(net, init_sync=False, bucket_cap_mb=args.bucket_mb)
         params = model.parameters()
         optimizer = (Adam(params, lr=args.learning_rate) if args.optimizer == "adam"
                      else SGD(params, lr=args.learning_rate, momentum=0.9))
         if payload is not None and "optimizer" in payload:
             optimizer.load_state_dict(payload["optimizer"])
         trainer = Trainer(model, optimizer, train_loader, test_loader, device, distributed, args.eval,
-                          manual_average=(args.ddp == "off"))
+                          manual_average=(args.ddp == "off"),
+                          autocast_dtype=torch.bfloat16 if args.dtype == "bf16" else None)
         trainer.set_epoch = args.set_epoch
         opt_state = optimizer.state_dict
     trainer.printer = printer
@@ -194,6 +203,11 @@ def build_parser():
     parser.add_argument('--log-rank0-only', action='store_true')
     parser.add_argument('--no-graph', action='store_true', help='fused engine: launch eagerly (no hipGraph)')
     parser.add_argument('--set-epoch', action='store_true', help='reshuffle shards every epoch')
+    parser.add_argument('--bucket-mb', type=float, default=25.0,
+                        help='DDP gradient bucket cap in MB (autograd engine; the fused engine times its '
+                             'own one- / two-bucket schedules)')
+    parser.add_argument('--dtype', choices=['fp32', 'bf16'], default='fp32',
+                        help='compute dtype: bf16 = autocast mixed precision (fp32 params / grads / Adam state)')
     return parser
 
 

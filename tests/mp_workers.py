@@ -647,15 +647,18 @@ def case_peer_engine(steps="6", mode="eager", overlap="1", autotune="0"):
     dist.destroy_process_group()
 
 
-def case_engine_w2_equiv(steps="8"):
+def case_engine_w2_equiv(steps="8", opt="adam"):
     """Verdict r4 item 6: the fused engine at W ranks (B=64 each, sharing one GPU, peer all-reduce)
     trains exactly like ONE rank at B=64*W on the concatenated shards: same per-step global loss and
-    the same parameters, up to fp32 reassociation; every W-rank replica bit-identical."""
+    the same parameters, up to fp32 reassociation; every W-rank replica bit-identical.  ``opt`` sgd
+    (lr 0.05, momentum 0.9: the update is linear in the gradient, so a wrong gradient scale or a
+    dropped / doubled shard shows at full size) or adam (the reference's optimizer)."""
     from pytorch_distributed_example_amd.data import synthetic_mnist, DistributedSampler
     from pytorch_distributed_example_amd.engine import LeNetTrainStep
     from pytorch_distributed_example_amd.models import build_net
 
     n_steps, b = int(steps), 64
+    kw = dict(optimizer="sgd", lr=0.05, momentum=0.9) if opt == "sgd" else {}
     dev = _shared_gpu_init()
     ds = synthetic_mnist(2048, seed=0, device=dev)
     shards = [DistributedSampler(ds, num_replicas=W, rank=r, shuffle=True, seed=0).indices_tensor()
@@ -672,8 +675,9 @@ def case_engine_w2_equiv(steps="8"):
         return out
 
     net = build_net(seed=3, device=dev)
+    net0 = [p.detach().clone() for p in net.parameters()]
     comm = dist.engine_comm(allow_host_only=True)
-    eng = LeNetTrainStep(net, batch_size=b, comm=comm, force_comm=True)
+    eng = LeNetTrainStep(net, batch_size=b, comm=comm, force_comm=True, **kw)
     mine = train(eng, shards[R], b)
     torch.cuda.synchronize()
     assert comm.health() == "", comm.health()
@@ -685,9 +689,15 @@ def case_engine_w2_equiv(steps="8"):
     if R == 0:
         cat = torch.cat([torch.cat([shards[r][k * b:(k + 1) * b] for r in range(W)]) for k in range(n_steps)])
         ref_net = build_net(seed=3, device=dev)
-        ref = LeNetTrainStep(ref_net, batch_size=b * W)
+        ref = LeNetTrainStep(ref_net, batch_size=b * W, **kw)
         res["one_loss"] = [x / (b * W) for x in train(ref, cat, b * W)]
         res["one_params"] = [p.detach().double().sum().item() for p in ref_net.parameters()]
+        # element-wise: |w - one| against the size of the training update |one - init| of each tensor
+        res["max_abs_diff"] = [float((p.double() - q.double()).abs().max()) for p, q in
+                               zip(net.parameters(), ref_net.parameters())]
+        res["max_update"] = [float((q.double() - p0.double()).abs().max()) for q, p0 in
+                             zip(ref_net.parameters(), net0)]
+        res["max_param"] = [float(q.double().abs().max()) for q in ref_net.parameters()]
     emit(res)
     dist.destroy_process_group()
 

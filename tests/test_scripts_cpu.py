@@ -64,6 +64,7 @@ def test_mnist_single_process_golden():
     assert lines[0].startswith("Namespace(backend='nccl', init_method='tcp://127.0.0.1:23456', rank=None, "
                                "world_size=1, epochs=2, no_cuda=True, learning_rate=0.001, root='data', "
                                "batch_size=128, eval=False")
+    assert "bucket_mb=25.0, dtype='fp32'" in lines[0]              # additive flags and defaults
     assert lines[1:4] == ["device = cpu", "Getting data loader with root = data", "obtained data_loader"]
     ep = [EPOCH_LINE.match(l) for l in lines[4:]]
     assert all(ep) and len(ep) == 2
@@ -80,6 +81,32 @@ def test_mnist_gloo_two_ranks(ddp):
     # test metrics identical across ranks (replicas in sync)
     last = [m for m in ep if m.group(1) == "2"]
     assert last[0].group(5) == last[1].group(5) and last[0].group(6) == last[1].group(6)
+
+
+def test_mnist_bucket_mb_reaches_ddp():
+    """--bucket-mb re-cuts DDP's gradient buckets: 0.05 MB splits the toy CNN's 1.72 MB of gradients into
+    several buckets (fc1.weight alone is 1.6 MB), and the replicas' printed metrics are identical to the
+    default single-bucket run (a bucket boundary does not change the elementwise 2-rank sum)."""
+    from pytorch_distributed_example_amd.models import build_net
+    from pytorch_distributed_example_amd.parallel.ddp import reverse_order_buckets
+    shapes = [(n, tuple(p.shape)) for n, p in build_net(seed=0).named_parameters()]
+    assert len(reverse_order_buckets(shapes, int(0.05 * (1 << 20)), 4)) > 2
+    assert len(reverse_order_buckets(shapes, int(25.0 * (1 << 20)), 4)) == 1
+    common = ["--backend", "gloo", "--eval", "--epochs", "1", "--log-rank0-only"]
+    small = [l for l in _mnist(common + ["--bucket-mb", "0.05"], n=2) if EPOCH_LINE.match(l)]
+    default = [l for l in _mnist(common, n=2) if EPOCH_LINE.match(l)]
+    assert small == default and len(small) == 1
+
+
+def test_mnist_dtype_bf16_autocast():
+    """--dtype bf16: the forward runs under torch.autocast (bf16 matmuls / convs) with fp32 parameters and
+    optimizer state; it trains (loss decreases) and differs from the fp32 run (bf16 is really in use)."""
+    lines = _mnist(["-s", "1", "--dtype", "bf16", "--epochs", "2"])
+    assert "dtype='bf16'" in lines[0]
+    ep = [m for m in map(EPOCH_LINE.match, lines) if m]
+    assert len(ep) == 2 and float(ep[1].group(3)) < float(ep[0].group(3))
+    fp = [m for m in map(EPOCH_LINE.match, _mnist(["-s", "1", "--epochs", "2"])) if m]
+    assert ep[0].group(3) != fp[0].group(3)
 
 
 def test_config1_mlp_gloo_two_ranks(tmp_path):
