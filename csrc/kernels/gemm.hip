@@ -1449,8 +1449,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm8p(GemmArgs a) {
 //          (draining under the first K-tile) -- with every wait vmcnt(VMW): exact whatever the retire order.
 //   MODE 1: round 5's allowance (diagnostics).
 //   MODE 2: the construction: MODE 1's waits, this tile's real stores issued and drained BEFORE the
-//          prologue, and NSTORE stores of the same size to an L2-resident 128 KB scratch (C2) in their place,
-//          which retire fast -- the allowance then lets phases read LDS slots whose loads are in flight.
+//          prologue, and NSTORE decoy stores of the same size in their place (each block rewriting its own
+//          L2-resident 128 KB of a C-sized scratch, C2) -- if a store acknowledgement can overtake an older
+//          load, the allowance lets phases read LDS slots whose loads are still in flight.
 //   MODE 3: epilogue math under the prologue, vmcnt(0), then the stores (no store younger than any slot;
 //          the first K-tile's waits skipped): sound, measured 2-10 % slower than MODE 0 on the GPT-2 shapes.
 // What persistence buys over the one-shot grid on the short-K GPT-2 shapes (K = 768: 12 K-tiles per
@@ -1482,7 +1483,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
   const int KT = (a.K + 63) >> 6;
   const rsrc_t ar = make_rsrc(a.A, a.a_bytes), br = make_rsrc(a.B, a.b_bytes);
   const rsrc_t cr = make_rsrc(a.C, a.c_bytes);
-  const rsrc_t c2r = MODE == 2 ? make_rsrc(a.C2, 128u << 10)
+  const rsrc_t c2r = MODE == 2 ? make_rsrc(a.C2, a.c_bytes)
                                : make_rsrc(EPI == kGelu ? (const void*)a.C2 : a.C, EPI == kGelu ? a.c_bytes : 0);
   const rsrc_t xr = make_rsrc(EPI == kGeluBwd ? (const void*)a.aux : a.C, EPI == kGeluBwd ? a.c_bytes : 0);
   const uint32_t astep = 128u, bstep = TB ? (uint32_t)a.ldb * 128u : 128u;
@@ -1723,12 +1724,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm8pp(GemmArgs a) {
       }
     };
     // NSTORE buffer stores per thread, exactly (masked lanes store to an out-of-range offset); MODE 2's
-    // decoys: the same count into the 128 KB scratch behind C2 (every block the same lines: L2 hits)
+    // decoys: the same count into a scratch as large as C (C2), each block rewriting its own 128 KB
+    // (lines spread over every L2 channel and resident after the first tile: fast write acknowledgements)
+    const uint32_t nreg = a.c_bytes >> 17, dbase = nreg ? (blockIdx.x % nreg) << 17 : 0u;
     auto stores = [&](bool decoy) {
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
         if (decoy) {
-          __builtin_amdgcn_raw_buffer_store_b128(o1[c], c2r, (uint32_t)(tv + c * NT) * 16u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(o1[c], c2r, dbase + (uint32_t)(tv + c * NT) * 16u, 0, 0);
           continue;
         }
         const uint32_t co = chunk_off(c, tm0, tn0);

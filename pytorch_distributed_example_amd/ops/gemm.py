@@ -21,9 +21,9 @@ on the v2 main loop (32-deep sub-stages, fragments of the next sub-stage read ac
 (one block per CU walking the tiles, each tile's output stores draining under the next tile's K loop;
 fprop / dgrad only -- wgrad calls with these ids run 9 / 11); 16 / 17 = 256x192 / 256x256 on
 v_mfma_f32_16x16x32_bf16 (every operand layout: fprop, dgrad, split-K wgrad); 18 = the 8-phase
-256x256 loop (every layout); 19 = 18 in a persistent block per CU (fprop; dgrad and other calls run 18);
-20 = 18 as one continuous K-tile stream per persistent block with a register epilogue (bias fprop,
-K % 128 == 0; other calls run 19, dgrad 18); 21 = 20 at 256x192 (fprop; other calls run 16); 22 = 18 at 256x192 (fprop; other calls run 16).
+256x256 loop (every layout); 19 = 18 in a persistent block per CU (fprop / dgrad; wgrad and other calls
+run 18); 20 = 18 as one continuous K-tile stream per persistent block with a register epilogue (bias
+fprop, plain dgrad, K % 128 == 0; other calls run 19); 21 = 20 at 256x192 (fprop; other calls run 16); 22 = 18 at 256x192 (fprop; other calls run 16).
 ``_CFG`` holds the per-shape choices measured on MI355X (``tools/gemm_own_bench.py`` ->
 ``profiles/r2_gemm/``); other shapes use the wave-quantisation heuristic of ``pick``.
 """
@@ -59,10 +59,11 @@ _CFG: Dict[Tuple[str, int, int], Tuple[int, int]] = {
     # of logits non-temporally: within 3 % of hipBLASLt, 12 % faster than plain stores)
     ("fprop", 2304, 768): (16, 1), ("fprop", 768, 768): (22, 1), ("fprop", 3072, 768): (19, 1),
     ("fprop", 768, 3072): (22, 1), ("fprop", 50304, 768): (19, 1),
-    # dgrad on cfg 18, not the persistent 19: its transposed-B path returned wrong values in ragged
-    # last tiles in repeats (profiles/r5_gemm/rejected_cfg19_dgrad/; a cfg-19 dgrad request runs 18)
+    # dgrad: the persistent cfg 19 again for the GELU-backward and LM-head dgrads (round 6: its tile-
+    # boundary waits no longer count stores as in flight, profiles/r6_gemm/; 90.5 vs 95.1 us and
+    # 1021 vs 1140 us against cfg 18), cfg 18 for the plain mlp dgrad (74.3 vs 76.9 us)
     ("dgrad", 768, 2304): (9, 1), ("dgrad", 768, 768): (9, 1), ("dgrad", 768, 3072): (18, 1),
-    ("dgrad", 3072, 768): (18, 1), ("dgrad", 768, 50304): (18, 1),
+    ("dgrad", 3072, 768): (19, 1), ("dgrad", 768, 50304): (19, 1),
     # split counts that bring tiles x splits closest to the 256 CUs (profiles/r3_gemm/; 256x256 tiles
     # for cfg 18: 36 tiles x 7, 27 x 9)
     ("wgrad", 2304, 768): (18, 9), ("wgrad", 768, 768): (9, 16), ("wgrad", 3072, 768): (18, 7),

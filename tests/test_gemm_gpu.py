@@ -199,24 +199,40 @@ def test_gemm8p_wgrad(T, N, K, splits):
                                    (20000, 2056, 128)])
 def test_gemm8pp_persistent_bit_identical(M, N, K):
     """cfg 19, the 8-phase loop in a persistent block per CU (the next tile's prologue DMA issued before
-    this tile's stores, the first K-tile's waits counting those stores in flight): bit-identical to
-    cfg 18 over many tiles per block, ragged edges, one- and two-K-tile shapes; fprop (bias, GELU).
-    dgrad requests for cfg 19 run cfg 18 (the persistent transposed-B path is disabled:
-    profiles/r5_gemm/rejected_cfg19_dgrad/); the dgrad lines check that routing stays exact.  Each
-    fprop form runs 3 times (a race would show as run-to-run differences)."""
+    this tile's stores; round 6: the first K-tile's counted waits no longer treat those stores as still
+    in flight, profiles/r6_gemm/): bit-identical to cfg 18 over many tiles per block, ragged edges, one-
+    and two-K-tile shapes; fprop (bias, GELU) and dgrad (plain, GELU backward).  Each form runs 3 times
+    (a race shows as run-to-run differences)."""
     x, w, b = _bf(M, K, seed=50), _bf(N, K, scale=0.03, seed=51), _bf(N, seed=52)
     y = G.fprop(x, w, b, cfg=19)
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
     y18 = G.fprop(x, w, b, cfg=18)
     a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
+    dy, w2 = _bf(M, K, seed=53), _bf(K, N, scale=0.03, seed=54)
+    dg = _bf(M, N, seed=55)
+    x18, xg18 = G.dgrad(dy, w2, cfg=18), G.dgrad(dy, w2, dgelu=dg, cfg=18)
     for _ in range(3):
         assert torch.equal(G.fprop(x, w, b, cfg=19), y18)
         a19, d19 = G.fprop(x, w, b, gelu=True, cfg=19)
         assert torch.equal(a19, a18) and torch.equal(d19, d18)
-    dy, w2 = _bf(M, K, seed=53), _bf(K, N, scale=0.03, seed=54)
-    assert torch.equal(G.dgrad(dy, w2, cfg=19), G.dgrad(dy, w2, cfg=18))
-    dg = _bf(M, N, seed=55)
-    assert torch.equal(G.dgrad(dy, w2, dgelu=dg, cfg=19), G.dgrad(dy, w2, dgelu=dg, cfg=18))
+        assert torch.equal(G.dgrad(dy, w2, cfg=19), x18)
+        assert torch.equal(G.dgrad(dy, w2, dgelu=dg, cfg=19), xg18)
+
+
+@pytest.mark.parametrize("cfg", [19, 20])
+def test_persistent_dgrad_ragged_rows_regression(cfg):
+    """The round-5 failure: cfg 19 (and 20) dgrad at M = 9000 (a ragged last row tile, the blocks' second
+    tile) returned wrong values in that tile in 2-4 of 5 repeats; reproduced in round 6 with the old
+    tile-boundary wait (tools/gemm_store_order.py mode 1).  10 repeats, plain and (cfg 19) GELU-backward,
+    bit-identical to cfg 18."""
+    M, N, K = 9000, 3072, 768
+    dy, w2 = _bf(M, K, seed=56), _bf(K, N, scale=0.03, seed=57)
+    dg = _bf(M, N, seed=58)
+    ref, refg = G.dgrad(dy, w2, cfg=18), G.dgrad(dy, w2, dgelu=dg, cfg=18)
+    for _ in range(10):
+        assert torch.equal(G.dgrad(dy, w2, cfg=cfg), ref)
+        if cfg == 19:
+            assert torch.equal(G.dgrad(dy, w2, dgelu=dg, cfg=cfg), refg)
 
 
 @pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (9000, 3072, 768), (4100, 776, 1536), (20000, 2056, 128),
@@ -224,21 +240,24 @@ def test_gemm8pp_persistent_bit_identical(M, N, K):
 def test_gemm8pc_continuous_bit_identical(M, N, K):
     """cfg 20: one K-tile stream per persistent block (the next tile's first K-tiles issued as ordinary
     look-ahead slots), register epilogue merging block pairs across lanes: bit-identical to cfg 18 for
-    fprop (with and without bias), over many tiles per block and ragged edges.  dgrad requests for
-    cfg 20 run cfg 18 (the persistent transposed-B paths are disabled,
-    profiles/r5_gemm/rejected_cfg19_dgrad/); the dgrad lines check that routing stays exact."""
+    fprop (with and without bias) and plain dgrad (also with a loss-gradient scale), over many tiles
+    per block and ragged edges; every form twice."""
     x, w, b = _bf(M, K, seed=60), _bf(N, K, scale=0.03, seed=61), _bf(N, seed=62)
     y = G.fprop(x, w, b, cfg=20)
     assert rel_err(y, F.linear(x.float(), w.float(), b.float())) < 1e-2
-    assert torch.equal(y, G.fprop(x, w, b, cfg=18))
-    assert torch.equal(G.fprop(x, w, None, cfg=20), G.fprop(x, w, None, cfg=18))
-    a20, d20 = G.fprop(x, w, b, gelu=True, cfg=20)
+    y18 = G.fprop(x, w, b, cfg=18)
+    n18 = G.fprop(x, w, None, cfg=18)
     a18, d18 = G.fprop(x, w, b, gelu=True, cfg=18)
-    assert torch.equal(a20, a18) and torch.equal(d20, d18)
     dy, w2 = _bf(M, K, seed=63), _bf(K, N, scale=0.03, seed=64)
-    assert torch.equal(G.dgrad(dy, w2, cfg=20), G.dgrad(dy, w2, cfg=18))
     s = torch.tensor([0.37], device=dev)
-    assert torch.equal(G.dgrad(dy, w2, cfg=20, scale=s), G.dgrad(dy, w2, cfg=18, scale=s))
+    x18, xs18 = G.dgrad(dy, w2, cfg=18), G.dgrad(dy, w2, cfg=18, scale=s)
+    for _ in range(2):
+        assert torch.equal(G.fprop(x, w, b, cfg=20), y18)
+        assert torch.equal(G.fprop(x, w, None, cfg=20), n18)
+        a20, d20 = G.fprop(x, w, b, gelu=True, cfg=20)
+        assert torch.equal(a20, a18) and torch.equal(d20, d18)
+        assert torch.equal(G.dgrad(dy, w2, cfg=20), x18)
+        assert torch.equal(G.dgrad(dy, w2, cfg=20, scale=s), xs18)
 
 
 @pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (16384, 2304, 768), (5000, 776, 256), (300, 200, 128)])

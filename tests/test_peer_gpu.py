@@ -168,6 +168,9 @@ def test_engine_w2_matches_w1_on_concatenated_shards(opt):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (w, one)
     assert min(w) > 0.2, w
     r = res[0]
+    print("loss rel diff max", max(abs(a - b) / max(1.0, abs(b)) for a, b in zip(w, one)))
+    print("param max |diff| / max|param| per tensor", [d / pm for d, pm in zip(r["max_abs_diff"], r["max_param"])])
+    print("param-sum rel diff per tensor", [abs(a - b) / max(1.0, abs(b)) for a, b in zip(r["w_params"], r["one_params"])])
     if opt == "sgd":
         for d, up, pm in zip(r["max_abs_diff"], r["max_update"], r["max_param"]):
             assert d <= 1e-5 * pm, (r["max_abs_diff"], r["max_param"])

@@ -437,6 +437,35 @@ def test_xent_kernel_matches_torch(variant, monkeypatch):
     assert got[2].abs().max().item() == 0.0                # ignored row
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_xent_small_probabilities_elementwise(variant, monkeypatch):
+    """softmax-CE gradients of tiny probabilities (a near-uniform row, p ~ 2e-5 over the
+    GPT-2 vocab, and rows with one dominant logit, p ~ 1e-6 elsewhere) match fp32 torch ELEMENTWISE on
+    the non-target columns -- below fp16's normal range the single-exp kernel's packed probabilities
+    would lose their precision (the kernel keeps 2^15 p)."""
+    from pytorch_distributed_example_amd._ext import kernels
+    monkeypatch.setenv("PDE_XENT_V", variant)
+    torch.manual_seed(13)
+    N, V, Vp = 16, 50257, 50304
+    logits = 0.01 * torch.randn(N, Vp)
+    logits[8:, 7] = 14.0                                   # rows 8..15: dominant logit, tails ~ 8e-7
+    logits = logits.to(dev, torch.bfloat16)
+    tg = torch.randint(0, V, (N,), device=dev)
+    ref = logits.float()[:, :V]
+    rows = torch.empty(N, device=dev)
+    L = logits.clone()
+    kernels().xent_bf16(L, tg, V, 1.0, rows, True)
+    g = torch.softmax(ref, 1)
+    g[torch.arange(N, device=dev), tg] -= 1
+    got = L.float()[:, :V]
+    mask = torch.ones_like(g, dtype=torch.bool)
+    mask[torch.arange(N, device=dev), tg] = False
+    rel = ((got - g).abs() / g.abs().clamp_min(1e-30))[mask]
+    assert rel.max().item() < 1.6e-2, rel.max().item()      # bf16 output rounding (2^-8) plus fp32 math
+    lse = torch.logsumexp(ref, 1)
+    assert (rows - (lse - ref.gather(1, tg[:, None])[:, 0])).abs().max().item() < 2e-3
+
+
 def test_scale_bf16_matches_torch():
     """In-place bf16 scale by a device scalar (LM-head dgrad loss-gradient scale): matches the fp32
     product rounded once to bf16, over a grid-stride tail (n8 not a multiple of the block)."""
