@@ -2338,7 +2338,7 @@ void pde_gemm_tile(int cfg, int* bm, int* bn) {
 // See the file header for the operand conventions.  epi: 0 bf16 (+bias), 1 bias+GELU (C = act,
 // C2 = gelu'(pre)), 2 GELU backward (aux = gelu'(pre)), 3 fp32 split-K slabs (C = float [splits][M][ldc]).
 // colsum (wgrad only): fp32 [splits][M] bias-gradient partials.  Supported combinations:
-// (ta, tb) = (0, 0) with epi 0/1, (0, 1) with epi 0/2, (1, 1) with epi 0/3 (+colsum).
+// (ta, tb) = (0, 0) with epi 0/1, (0, 1) with epi 0/2/3, (1, 1) with epi 0/3 (+colsum).
 int g_gemm_dbg = 0;   // pde_gemm_set_dbg: ablation flags of the v1 main loop (benchmarks only)
 
 void pde_gemm_set_dbg(int d) { g_gemm_dbg = d; }
@@ -2384,6 +2384,9 @@ hipError_t pde_gemm(const void* A, const void* B, void* C, void* C2, const void*
   } else if (!ta && tb) {
     if (epi == kBf16) return launch_any<false, true, kBf16, false>(cfg, a, splits, st);
     if (epi == kGeluBwd) return launch_any<false, true, kGeluBwd, false>(cfg, a, splits, st);
+    // split-K dgrad (a deep reduction over few output tiles, e.g. the LM head's 50304-deep dgrad onto
+    // 64 x 3 tiles): fp32 slabs, folded by pde_gemm_reduce
+    if (epi == kSlab) return launch_any<false, true, kSlab, false>(cfg, a, splits, st);
   } else if (ta && tb) {
     if (epi == kSlab) {
       return colsum ? launch_any<true, true, kSlab, true>(cfg, a, splits, st)

@@ -152,16 +152,26 @@ def fprop(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def dgrad(dy2: torch.Tensor, w: torch.Tensor, dgelu: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
-          scale: Optional[torch.Tensor] = None):
+          scale: Optional[torch.Tensor] = None, splits: Optional[int] = None):
     """dy2 [M, N] . w [N, K] -> dx [M, K]; with ``dgelu`` ([M, K], gelu'(pre) from ``fprop(gelu=True)``)
     returns dx * dgelu; ``scale`` (a one-element fp32 device tensor, e.g. the loss gradient) multiplies
-    the result in the epilogue."""
+    the result in the epilogue.  ``splits`` > 1 (no ``dgelu``): split-K over the reduction into fp32 slabs
+    folded by one reduction kernel -- for deep reductions onto too few output tiles to fill the chip (the
+    LM head: 50304-deep onto 64 x 3 tiles of 256 x 256)."""
     _chk(dy2, "dy")
     _chk(w, "w")
     M, Nk = dy2.shape                  # reduction over the weight's rows
     Kout = w.shape[1]
-    c = pick("dgrad", M, Kout, Nk)[0] if cfg is None else cfg
+    c0, s0 = pick("dgrad", M, Kout, Nk)
+    c = c0 if cfg is None else cfg
+    S = s0 if splits is None else splits
+    S = kernels().gemm_splits(Nk, S) if dgelu is None else 1
     dx = torch.empty(M, Kout, device=dy2.device, dtype=torch.bfloat16)
+    if S > 1:
+        part = _scratch(dy2.device, S * M * Kout, "slab")
+        kernels().gemm_bf16(dy2, w, part, 0, 1, EPI_SLAB, M, Kout, Nk, Nk, Kout, Kout, S, c)
+        kernels().gemm_reduce(part, S, M, Kout, dx, None, None, scale)
+        return dx
     if dgelu is not None:
         kernels().gemm_bf16(dy2, w, dx, 0, 1, EPI_GELU_BWD, M, Kout, Nk, Nk, Kout, Kout, 1, c, aux=dgelu)
     else:

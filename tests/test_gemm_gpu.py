@@ -72,6 +72,19 @@ def test_dgrad(cfg, M, N, K):
     assert rel_err(dxg, dx.float() * dgelu.float()) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [9, 16, 17, 18, 19])
+@pytest.mark.parametrize("splits", [2, 4])
+def test_dgrad_split_k(cfg, splits):
+    """Split-K dgrad (fp32 slabs + the reduction kernel, with the loss-gradient scale folded there):
+    the LM-head form, a deep reduction onto few output tiles; ragged M / N and a K % 64 tail."""
+    M, N, K = 1000, 392, 5000
+    dy, w = _bf(M, K, seed=80), _bf(K, N, scale=0.02, seed=81)
+    s = torch.tensor([0.37], device=dev)
+    ref = dy.float() @ w.float()
+    assert rel_err(G.dgrad(dy, w, cfg=cfg, splits=splits), ref) < 1e-2
+    assert rel_err(G.dgrad(dy, w, cfg=cfg, splits=splits, scale=s), ref * 0.37) < 1e-2
+
+
 @pytest.mark.parametrize("cfg", CFGS)
 @pytest.mark.parametrize("splits", [1, 3, 8])
 def test_wgrad_split_bias(cfg, splits):

@@ -74,7 +74,11 @@ def main():
             lib = timeit(lambda: torch.matmul(dy, w), a.iters)
             res = {}
             for cfg in CFGS:
-                res[cfg] = timeit(lambda: G.dgrad(dy, w, dgelu=pre, cfg=cfg), a.iters)
+                res[cfg] = timeit(lambda: G.dgrad(dy, w, dgelu=pre, cfg=cfg, splits=1), a.iters)
+            if pre is None and fin * T <= 768 * 16384 and out >= 3072:   # deep reductions onto few tiles
+                for cfg in (18, 9, 16):
+                    for s in (2, 3, 4, 6):
+                        res[f"{cfg}/{s}"] = timeit(lambda: G.dgrad(dy, w, cfg=cfg, splits=s), a.iters)
             best = min(res, key=res.get)
             lines.append({"gemm": f"{name}.dgrad", "M": T, "N": fin, "K": out,
                           "epilogue": "gelu_bwd" if pre is not None else "none",
