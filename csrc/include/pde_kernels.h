@@ -76,6 +76,14 @@ struct PdeLenetBwdOpt {
                             // 2 (ext): slabs + per-image conv1 partials, folded by pde_lenet_conv_grad_fold
   float* c1img;             // ext: [B][520] per-image conv1 partials
 };
+// ext-mode fold fused with the in-place one-shot (two = 0) or two-shot (two = 1) all-reduce of the
+// registered flat gradient buffer
+// (ipdev: PeerIpDev bytes of that registration; [lo, hi) the conv range the fold writes; sync: two
+// zero-initialised device counters, left zero by every launch).  hipErrorInvalidValue when the buffer
+// does not fit one one-shot grid (the grid cap of ranks sharing a GPU).
+hipError_t pde_lenet_conv_fold_ar(const void* ipdev, const float* slab, const float* c1img, int B, long long c1w,
+                                 long long c1b, long long c2w, long long c2b, long long n, long long lo, long long hi,
+                                 unsigned* sync, float scale, int two, hipStream_t st);
 hipError_t pde_lenet_conv_grad_fold(const float* slab, const float* c1img, int B, float* g, long long c1w, long long c1b,
                                     long long c2w, long long c2b, hipStream_t st);
 hipError_t pde_lenet_conv_bwd2(const float* Xb, const float* P1, const uint8_t* A1, const float* dP2m,

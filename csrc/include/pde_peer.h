@@ -26,4 +26,23 @@ struct PeerDev {
   int32_t world;
 };
 
+// The in-place (registered-buffer) protocol's view of one registration, for kernels that run the
+// in-place one-shot all-reduce inside their own launch (the LeNet engine's fused conv-gradient fold +
+// all-reduce): every rank's registered buffer and in-place flag region mapped here, the shared
+// time-out latch, and the one-shot grid cap.  Produced by PeerAllReduce::registered_device_args(id).
+// Flag slots and per-slot call counting are exactly peer_inplace_kernel's (peer_allreduce.hip), so
+// fused and standalone in-place calls interleave freely.
+struct PeerIpDev {
+  uint8_t* data[kPeerMaxRanks];
+  uint8_t* flags[kPeerMaxRanks];
+  uint32_t* errc;       // the staged protocol's ctrl: [2] = time-out count (shared latch)
+  uint32_t* err_host;
+  int64_t bytes;        // registered bytes
+  int64_t timeout;      // s_memrealtime ticks (100 MHz)
+  int32_t rank;
+  int32_t world;
+  int32_t block_cap;    // in-place one-shot grid cap (ranks sharing one GPU)
+  int32_t pad;
+};
+
 }  // namespace pde

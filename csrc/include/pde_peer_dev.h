@@ -165,4 +165,68 @@ __device__ bool peer_ar_f32_vblock(const PeerDev& d, const float* in_f, float* o
   return completed;
 }
 
+
+// ---- in-place (registered buffer) one-shot inside another kernel ------------------------------------
+// Exactly peer_inplace_kernel's protocol (peer_allreduce.hip) with the rank count at run time: virtual
+// block vb of every rank owns the same vectors; the arrival signal is an atomic add into this rank's
+// phase-0 slot of every rank's flag region (the add on the own region returns the calls so far of slot
+// vb: per-slot call numbers agree across ranks because every rank makes the same calls); barrier B
+// (phase 1) publishes the call number once every buffer has been read.  Inputs must be in memory
+// (earlier kernels, or system-scope write-through stores drained before the arrival).
+__device__ __forceinline__ uint32_t* ipd_flag(uint8_t* region, int phase, int vb, int src) {
+  return reinterpret_cast<uint32_t*>(region) + (phase * kPeerMaxBlocks + vb) * kPeerMaxRanks + src;
+}
+
+// lanes t < world: arrival add on this rank's slot in rank t's region; *s_call (LDS) <- calls so far
+__device__ __forceinline__ void ipd_arrive(const PeerIpDev& d, int vb, uint32_t* s_call) {
+  const int t = threadIdx.x;
+  if (t < d.world) {
+    uint32_t* slot = ipd_flag(d.flags[t], 0, vb, d.rank);
+    const uint32_t old = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == d.rank) *s_call = old;
+  }
+}
+
+// wait (and with SIGNAL first publish `target` into every rank's slot for this rank) until every rank's
+// slot in the own region holds `target`; skip_own: the own slot is known to hold it (arrival add)
+template <bool SIGNAL>
+__device__ __forceinline__ void ipd_barrier(const PeerIpDev& d, int phase, int vb, uint32_t target, bool failed,
+                                            bool skip_own, uint32_t* bad) {
+  if constexpr (SIGNAL) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int t = threadIdx.x;
+  if (t < d.world && !(skip_own && t == d.rank)) {
+    if constexpr (SIGNAL)
+      __hip_atomic_store(ipd_flag(d.flags[t], phase, vb, d.rank), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = ipd_flag(d.flags[d.rank], phase, vb, t);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int spins = 0;
+    while (!failed && __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == 256) {
+        spins = 0;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > d.timeout) {
+          __hip_atomic_fetch_add(d.errc + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(d.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          *bad = 1u;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// 16-byte system-coherent (sc0 sc1) load / store through a buffer resource: served from memory, never
+// from this CU's or XCD's caches (peers' data arrives over xGMI; own write-through stores land there)
+constexpr int kIpdAuxSys = 1 | 16;
+__device__ __forceinline__ peer_vec_t ipd_ld(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __builtin_bit_cast(peer_vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, kIpdAuxSys));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ipd_rsrc(const uint8_t* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 }  // namespace pde

@@ -1078,6 +1078,238 @@ __global__ __launch_bounds__(256) void k_conv_grad_fold(const float* __restrict_
   }
 }
 
+// Ext-mode fold FUSED with the in-place one-shot all-reduce of the whole flat gradient buffer (the
+// W > 1 "serial ...:pfold" schedule: one launch where there were two, k_conv_grad_fold + the standalone
+// peer_inplace_kernel).  Blocks [0, nfold) are k_conv_grad_fold's fold blocks at 512 threads (the same
+// per-output summation order, so the canonical conv gradients are bit-identical), writing with
+// system-scope write-through stores, then bumping sync[0].  Blocks [nfold, grid) are virtual blocks
+// vb = 0.. of the in-place one-shot over the registered buffer (peer_inplace_kernel's vector map,
+// flag slots and per-slot call counting, pde_peer_dev.h): a block whose vectors touch the conv range
+// first waits until every fold block is done -- it has a higher block id than every fold block, so
+// those are already dispatched and never wait on anything -- and the last such block resets the
+// counters for the next launch (graph replays).  The sum is in fixed rank order: replicas stay
+// bit-identical.
+constexpr int kFoldC2w = (kSlab + 511) / 512;       // 49 conv2 fold blocks of 512
+constexpr int kFoldC1w = (kC1Img + 31) / 32;        // 17 conv1 fold blocks (32 outputs x 16 parts)
+constexpr int kFoldNw = kFoldC2w + kFoldC1w;
+
+struct FoldArArgs {
+  pde::PeerIpDev d;
+  const float* slab;
+  const float* c1img;
+  int B;
+  long long c1w, c1b, c2w, c2b;   // element offsets of the conv slots in the registered buffer
+  long long n4;                   // 16-byte vectors all-reduced: [0, n4) of the registered buffer
+  long long lo4, hi4;             // vectors the fold writes (the conv range)
+  unsigned* sync;                 // [0] fold blocks done, [1] waiting blocks past their wait
+  int nwait;                      // AR blocks whose vectors touch [lo4, hi4)
+  float scale;
+};
+
+// one fold block (k_conv_grad_fold's summation order at 512 threads; write-through stores), then its
+// arrival on sync[0]
+__device__ __forceinline__ void fold_ar_fold_block(const FoldArArgs& a, float (*red)[33]) {
+  const int t = threadIdx.x;
+  const pde::PeerIpDev& d = a.d;
+  const __amdgpu_buffer_rsrc_t ro = pde::ipd_rsrc(d.data[d.rank], d.bytes);
+  auto st_sys = [&](long long e, float v) {   // write-through: in memory once drained (peers read it there)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, (int)(e * 4), 0, pde::kIpdAuxSys);
+  };
+  if ((int)blockIdx.x < kFoldC2w) {
+    const int i = blockIdx.x * 512 + t;
+    const int ic = min(i, kSlab - 1);
+    float q[kNIG];
+#pragma unroll
+    for (int r = 0; r < kNIG; ++r) q[r] = a.slab[(size_t)r * kSlab + ic];
+    float sum = q[0];
+#pragma unroll
+    for (int r = 1; r < kNIG; ++r) sum += q[r];
+    if (i < 25000) st_sys(a.c2w + i, sum);
+    else if (i >= kSlabBias && i < kSlabBias + 50) st_sys(a.c2b + (i - kSlabBias), sum);
+  } else {
+    const int o = ((int)blockIdx.x - kFoldC2w) * 32 + (t & 31), part = t >> 5, oc = min(o, kC1Img - 1);
+    float sum = 0.f;
+    constexpr int kMaxPer = 8;
+    float q[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k) q[k] = a.c1img[(size_t)min(part + 16 * k, a.B - 1) * kC1Img + oc];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k)
+      if (part + 16 * k < a.B) sum += q[k];
+    red[part][t & 31] = sum;
+    __syncthreads();
+    if (t < 32 && o < kC1Img) {
+      float acc = red[0][t];
+#pragma unroll
+      for (int p = 1; p < 16; ++p) acc += red[p][t];
+      const int hh = o / 260, rem = o - hh * 260, c = rem / 26, tap = rem - c * 26, ch = 10 * hh + c;
+      if (tap < 25) st_sys(a.c1w + ch * 25 + tap, acc);
+      else st_sys(a.c1b + ch, acc);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's write-through stores acknowledged
+  __syncthreads();
+  if (t == 0) __hip_atomic_fetch_add(a.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// an all-reduce block that reads conv-range data: wait until every fold block has arrived (their ids are
+// lower, so they are all dispatched already and wait on nothing); *s_bad <- 1 on a (never expected) time-out
+__device__ __forceinline__ void fold_ar_wait(const FoldArArgs& a, uint32_t* s_bad) {
+  if (threadIdx.x == 0) {
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(a.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)kFoldNw) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((int64_t)(__builtin_amdgcn_s_memrealtime() - w0) > a.d.timeout) { *s_bad = 1u; break; }
+    }
+  }
+  __syncthreads();
+}
+
+// the last waiting block resets the counters for the next launch
+__device__ __forceinline__ void fold_ar_exit(const FoldArArgs& a) {
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)a.nwait - 1u) {
+      __hip_atomic_store(a.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(512) void k_conv_fold_ar(FoldArArgs a) {
+  __shared__ float red[16][33];
+  __shared__ uint32_t s_call, s_bad;
+  const int t = threadIdx.x;
+  const pde::PeerIpDev& d = a.d;
+  float* own = reinterpret_cast<float*>(d.data[d.rank]);
+  if ((int)blockIdx.x < kFoldNw) {
+    fold_ar_fold_block(a, red);
+    return;
+  }
+  // ---- in-place one-shot, virtual block vb ----
+  const int vb = (int)blockIdx.x - kFoldNw, nvb = (int)gridDim.x - kFoldNw;
+  const long long stride = (long long)nvb * 512, t0 = (long long)vb * 512 + t;
+  bool waits = false;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long b0 = (long long)vb * 512 + u * stride;
+    waits = waits || (b0 < a.hi4 && b0 + 512 > a.lo4);
+  }
+  if (t == 0) s_bad = 0u;
+  __syncthreads();
+  if (waits) fold_ar_wait(a, &s_bad);
+  pde::ipd_arrive(d, vb, &s_call);
+  if (t == 64 && __hip_atomic_load(d.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) s_bad = 1u;
+  __syncthreads();
+  const uint32_t target = s_call + 1u;
+  const bool failed = s_bad != 0;
+  __amdgpu_buffer_rsrc_t rs[pde::kPeerMaxRanks];
+#pragma unroll
+  for (int p = 0; p < pde::kPeerMaxRanks; ++p) rs[p] = pde::ipd_rsrc(p < d.world ? d.data[p] : d.data[d.rank], d.bytes);
+  pde::ipd_barrier<false>(d, 0, vb, target, failed, true, &s_bad);   // A: every rank's buffer holds its input
+  pde::peer_vec_t v[U][pde::kPeerMaxRanks];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = t0 + u * stride, ic = i < a.n4 ? i : 0;
+#pragma unroll
+    for (int p = 0; p < pde::kPeerMaxRanks; ++p)
+      if (p < d.world) v[u][p] = pde::ipd_ld(rs[p], ic);
+  }
+  pde::peer_vec_t res[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) res[u] = pde::peer_sum(v[u], d.world, a.scale);   // fixed rank order
+  pde::ipd_barrier<true>(d, 1, vb, target, failed, false, &s_bad);   // B: every rank has read every buffer
+  const bool bad = s_bad != 0;
+  const pde::peer_vec_t nanv = {0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = t0 + u * stride;
+    if (i < a.n4) reinterpret_cast<pde::peer_vec_t*>(own)[i] = bad ? nanv : res[u];
+  }
+  if (waits) fold_ar_exit(a);
+}
+
+// The two-shot form (W > 2 over real links: each rank reduces one 1/W chunk from every rank, then gathers
+// the others' chunks -- 2 (W-1)/W of the buffer over the links instead of W-1 times it).  Every
+// all-reduce block waits for the fold (a peer's block reads this rank's conv vectors in any chunk), then
+// peer_inplace_kernel's two-shot path: barrier A, reduce-scatter (write-through), barrier B, all-gather,
+// barrier C.  R: vectors per thread per iteration (R x W system loads in flight).
+template <int R>
+__global__ __launch_bounds__(512) void k_conv_fold_ar2(FoldArArgs a) {
+  __shared__ float red[16][33];
+  __shared__ uint32_t s_call, s_bad;
+  const int t = threadIdx.x;
+  const pde::PeerIpDev& d = a.d;
+  float* own = reinterpret_cast<float*>(d.data[d.rank]);
+  if ((int)blockIdx.x < kFoldNw) {
+    fold_ar_fold_block(a, red);
+    return;
+  }
+  const int vb = (int)blockIdx.x - kFoldNw, nvb = (int)gridDim.x - kFoldNw;
+  const long long stride = (long long)nvb * 512, t0 = (long long)vb * 512 + t;
+  if (t == 0) s_bad = 0u;
+  __syncthreads();
+  fold_ar_wait(a, &s_bad);
+  pde::ipd_arrive(d, vb, &s_call);
+  if (t == 64 && __hip_atomic_load(d.errc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) s_bad = 1u;
+  __syncthreads();
+  const uint32_t target = s_call + 1u;
+  const bool failed = s_bad != 0;
+  const int W = d.world;
+  __amdgpu_buffer_rsrc_t rs[pde::kPeerMaxRanks];
+#pragma unroll
+  for (int p = 0; p < pde::kPeerMaxRanks; ++p) rs[p] = pde::ipd_rsrc(p < W ? d.data[p] : d.data[d.rank], d.bytes);
+  const __amdgpu_buffer_rsrc_t ro = rs[d.rank];
+  const long long chunk4 = (a.n4 + W - 1) / W, lo = (long long)d.rank * chunk4;
+  const long long len = lo + chunk4 <= a.n4 ? chunk4 : (a.n4 > lo ? a.n4 - lo : 0);
+  pde::ipd_barrier<false>(d, 0, vb, target, failed, true, &s_bad);   // A: every rank's buffer holds its input
+  const pde::peer_vec_t nanv = {0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u};
+  for (long long i0 = t0; i0 < len; i0 += R * stride) {           // reduce-scatter: my chunk
+    pde::peer_vec_t v[R][pde::kPeerMaxRanks];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long long i = i0 + r * stride;
+#pragma unroll
+      for (int p = 0; p < pde::kPeerMaxRanks; ++p)
+        if (p < W) v[r][p] = pde::ipd_ld(rs[p], lo + (i < len ? i : i0));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long long i = i0 + r * stride;
+      const pde::peer_vec_t o = s_bad ? nanv : pde::peer_sum(v[r], W, a.scale);
+      if (i < len) __builtin_amdgcn_raw_buffer_store_b128(o, ro, (int)((lo + i) * 16), 0, pde::kIpdAuxSys);
+    }
+  }
+  pde::ipd_barrier<true>(d, 1, vb, target, failed, false, &s_bad);  // B: every chunk reduced, every input read
+  const bool bad = s_bad != 0;
+  const long long last = a.n4 - 1;
+  for (long long i0 = t0; i0 < chunk4; i0 += R * stride) {        // all-gather: chunk q from its owner q
+    pde::peer_vec_t v[R][pde::kPeerMaxRanks];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long long i = i0 + r * stride;
+#pragma unroll
+      for (int q = 0; q < pde::kPeerMaxRanks; ++q) {
+        const long long gq = (long long)q * chunk4 + i;
+        if (q < W && q != d.rank) v[r][q] = pde::ipd_ld(rs[q], gq < last ? gq : last);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long long i = i0 + r * stride;
+#pragma unroll
+      for (int q = 0; q < pde::kPeerMaxRanks; ++q) {
+        const long long gq = (long long)q * chunk4 + i;
+        if (q < W && q != d.rank && i < chunk4 && gq <= last)
+          reinterpret_cast<pde::peer_vec_t*>(own)[gq] = bad ? nanv : v[r][q];
+      }
+    }
+  }
+  pde::ipd_barrier<true>(d, 2, vb, target, failed, false, &s_bad);  // C: every rank has gathered
+  fold_ar_exit(a);
+}
+
 __global__ void k_pack_w2_v2(const float* __restrict__ w2, float* __restrict__ dst) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < 25000) dst[pde_lenet_wp_index(e)] = w2[e];
@@ -1165,6 +1397,55 @@ hipError_t pde_lenet_conv_grad_fold(const float* slab, const float* c1img, int B
                                     long long c2w, long long c2b, hipStream_t st) {
   if (B < 1 || B > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_conv_grad_fold, dim3(kFoldC2 + kFoldC1), dim3(256), 0, st, slab, c1img, B, g, c1w, c1b, c2w, c2b);
+  return hipGetLastError();
+}
+
+hipError_t pde_lenet_conv_fold_ar(const void* ipdev, const float* slab, const float* c1img, int B, long long c1w,
+                                 long long c1b, long long c2w, long long c2b, long long n, long long lo, long long hi,
+                                 unsigned* sync, float scale, int two, hipStream_t st) {
+  if (B < 1 || B > 128 || n <= 0 || (n & 3) || (lo & 3) || (hi & 3) || lo < 0 || hi > n || lo >= hi)
+    return hipErrorInvalidValue;
+  FoldArArgs a{};
+  std::memcpy(&a.d, ipdev, sizeof(a.d));
+  if (n * 4 > a.d.bytes || c1w < lo || c1b + 20 > hi || c2w < lo || c2b + 50 > hi) return hipErrorInvalidValue;
+  a.slab = slab; a.c1img = c1img; a.B = B;
+  a.c1w = c1w; a.c1b = c1b; a.c2w = c2w; a.c2b = c2b;
+  a.n4 = n / 4; a.lo4 = lo / 4; a.hi4 = hi / 4;
+  a.sync = sync;
+  a.scale = scale;
+  if (two) {
+    // the standalone two-shot's grid: one thread per chunk vector, at most 64 blocks (fewer when ranks
+    // share a GPU); R x W system loads in flight per thread
+    const int W = a.d.world;
+    const long long chunk4 = (a.n4 + W - 1) / W;
+    const long long nvb = std::max(1LL, std::min<long long>(std::min(64, a.d.block_cap), (chunk4 + 511) / 512));
+    a.nwait = (int)nvb;
+    const dim3 grid((unsigned)(kFoldNw + nvb));
+    if (W <= 2) hipLaunchKernelGGL(k_conv_fold_ar2<4>, grid, dim3(512), 0, st, a);
+    else if (W <= 4) hipLaunchKernelGGL(k_conv_fold_ar2<2>, grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(k_conv_fold_ar2<1>, grid, dim3(512), 0, st, a);
+    return hipGetLastError();
+  }
+  // vectors per thread: 2 (the standalone one-shot's measured best), more only to fit the grid cap
+  const int cap = std::min(a.d.block_cap, (int)pde::kPeerMaxBlocks);
+  int U = 2;
+  while (U < 4 && (a.n4 + 512LL * U - 1) / (512LL * U) > cap) U *= 2;
+  const long long nvb = (a.n4 + 512LL * U - 1) / (512LL * U);
+  if (nvb > cap) return hipErrorInvalidValue;                       // does not fit one-shot: no fused route
+  const long long stride = nvb * 512;
+  int nwait = 0;
+  for (long long vb = 0; vb < nvb; ++vb) {
+    bool w = false;
+    for (int u = 0; u < U; ++u) {
+      const long long b0 = vb * 512 + u * stride;
+      w = w || (b0 < a.hi4 && b0 + 512 > a.lo4);
+    }
+    nwait += w ? 1 : 0;
+  }
+  a.nwait = nwait;
+  const dim3 grid((unsigned)(kFoldNw + nvb));
+  if (U == 2) hipLaunchKernelGGL(k_conv_fold_ar<2>, grid, dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(k_conv_fold_ar<4>, grid, dim3(512), 0, st, a);
   return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 #include <c10/hip/HIPGuard.h>
 
 #include <cmath>
+#include <cstring>
 #include <optional>
 
 #include "pde_kernels.h"
@@ -342,6 +343,25 @@ void lenet_conv_grad_fold(const at::Tensor& slab, const at::Tensor& c1img, int64
             "lenet_conv_grad_fold");
 }
 
+void lenet_conv_fold_ar(const at::Tensor& ipdev, const at::Tensor& slab, const at::Tensor& c1img, int64_t B,
+                        const at::Tensor& g, int64_t c1w, int64_t c1b, int64_t c2w, int64_t c2b, int64_t lo, int64_t hi,
+                        const at::Tensor& sync, double scale, int64_t two) {
+  TORCH_CHECK(B >= 1 && B <= 128, "conv_fold_ar: batch must be in [1, 128]");
+  TORCH_CHECK(ipdev.device().is_cpu() && ipdev.scalar_type() == at::kByte && ipdev.numel() == sizeof(pde::PeerIpDev),
+              "conv_fold_ar: ipdev must be the bytes of PeerAllReduce.registered_device_args()");
+  check_cuda(slab, "slab", F32, 16 * 25088);
+  check_cuda(c1img, "c1img", F32, B * 520);
+  check_cuda(g, "grads", F32);
+  check_cuda(sync, "sync", at::kInt, 2);
+  pde::PeerIpDev d;
+  std::memcpy(&d, ipdev.data_ptr(), sizeof(d));
+  TORCH_CHECK(d.data[d.rank] == g.data_ptr(), "conv_fold_ar: g must be the registered buffer (from its start)");
+  hip_check(pde_lenet_conv_fold_ar(ipdev.data_ptr(), ptr<float>(slab), ptr<float>(c1img), (int)B, c1w, c1b, c2w, c2b,
+                                   g.numel(), lo, hi, reinterpret_cast<unsigned*>(sync.data_ptr()), (float)scale,
+                                   (int)two, cur_stream()),
+            "lenet_conv_fold_ar");
+}
+
 void lenet_conv_bwd2(const at::Tensor& Xb, const at::Tensor& P1, const at::Tensor& A1, const at::Tensor& dP2m,
                      const at::Tensor& A2, const at::Tensor& W2c, int64_t B, const at::Tensor& slab,
                      const at::Tensor& c1rep, const at::Tensor& c1part, const at::Tensor& tick, const at::Tensor& g, int64_t c1w, int64_t c1b,
@@ -619,6 +639,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_conv_fwd2", &lenet_conv_fwd2, py::arg("Xb"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("Wp"),
         py::arg("b2"), py::arg("P1"), py::arg("A1"), py::arg("P2"), py::arg("A2"), py::arg("zero") = py::none());
   m.def("lenet_conv_grad_fold", &lenet_conv_grad_fold);
+  m.def("lenet_conv_fold_ar", &lenet_conv_fold_ar);
   m.def("lenet_conv_bwd2", &lenet_conv_bwd2, py::arg("Xb"), py::arg("P1"), py::arg("A1"), py::arg("dP2m"),
         py::arg("A2"), py::arg("W2c"), py::arg("B"), py::arg("slab"), py::arg("c1rep"), py::arg("c1part"), py::arg("tick"),
         py::arg("g"),

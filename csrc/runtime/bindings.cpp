@@ -244,6 +244,8 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("count"), py::arg("esz"), py::arg("scale"), py::arg("algo"), py::arg("stream"),
            py::call_guard<py::gil_scoped_release>())
       .def("registered_bytes", &PeerAllReduce::registered_bytes)
+      .def("registered_device_args",
+           [](PeerAllReduce& p, int id) { return py::bytes(p.registered_device_args(id)); })
       .def("debug_skip_stage", &PeerAllReduce::debug_skip_stage)
       .def("error", &PeerAllReduce::error, py::call_guard<py::gil_scoped_release>())
       .def("error_async", &PeerAllReduce::error_async)

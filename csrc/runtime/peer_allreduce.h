@@ -105,6 +105,9 @@ class PeerAllReduce {
   void all_reduce_registered(int id, int64_t off, int64_t count, int esz, float scale, int algo, uintptr_t stream);
   void all_reduce_registered_f32(int id, int64_t off, int64_t count, float scale, int algo, uintptr_t stream);
   int64_t registered_bytes(int id) const;
+  // Raw bytes of a PeerIpDev (pde_peer.h) for registration `id`: kernels that run the in-place one-shot
+  // protocol in their own launch (csrc/kernels/lenet_v2.hip: k_conv_fold_ar).
+  std::string registered_device_args(int id) const;
   void close();
 
  private:

@@ -734,6 +734,24 @@ void PeerAllReduce::device_probe_f32(uintptr_t in, uintptr_t out, int64_t count,
   hip_check(hipGetLastError(), "peer device-path probe launch");
 }
 
+std::string PeerAllReduce::registered_device_args(int id) const {
+  if (id < 0 || id >= (int)regs_.size() || !regs_[id].open) throw std::runtime_error("registration not open");
+  const Reg& r = regs_[id];
+  PeerIpDev d{};
+  for (int p = 0; p < kPeerMaxRanks; ++p) {
+    d.data[p] = p < world_ ? r.base[p] : nullptr;
+    d.flags[p] = p < world_ ? peer_ipflags_[p] : nullptr;
+  }
+  d.errc = ctrl_;
+  d.err_host = err_dev_;
+  d.bytes = r.bytes;
+  d.timeout = timeout_ticks_;
+  d.rank = rank_;
+  d.world = world_;
+  d.block_cap = ip_block_cap_;
+  return std::string(reinterpret_cast<const char*>(&d), sizeof(d));
+}
+
 std::string PeerAllReduce::register_buffer(uintptr_t ptr, int64_t bytes, int* id) {
   if (ptr & 15) throw std::invalid_argument("registered buffers must be 16-byte aligned");
   if (bytes <= 0 || bytes > 0x7fffffffLL) throw std::invalid_argument("registered buffer size must be in (0, 2 GB)");

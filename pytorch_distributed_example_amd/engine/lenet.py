@@ -66,6 +66,8 @@ class LeNetTrainStep:
         # conv bucket after it on the compute stream
         self.mode = "overlap" if overlap else "flat"
         self._peer_dev = None
+        self._ipdev = None            # PeerIpDev bytes of the registered flat gradients ("pfold" route)
+        self._fold_sync = None
         self.ar_epoch = torch.full((1,), -1, device=p0.device, dtype=torch.int64)   # fused-Adam all-reduce
         # force_comm: run the comm-stream/event path even at world size 1 (1-GPU testing of the W>1 path)
         self.comm_on = comm is not None and (self.world > 1 or force_comm)
@@ -246,7 +248,37 @@ class LeNetTrainStep:
             K.sgd_flat(self.params[sl], self.grads[sl], self.m[sl], self.lr, self.momentum, 0.0, self.wd, False,
                        scale, self.counters, self.arrive, -1, pack_off, pack, pack_mode=mode, **folds)
 
-    def _conv_bwd2(self, B: int, q: int, fused_fc_route: Optional[str] = None):
+    def _fold_ar(self, B: int, two: bool = False):
+        """The "serial ...:pfold" / "pfold2" routes: the ext-mode conv-gradient fold and the in-place
+        one-shot / two-shot all-reduce of the whole flat gradient buffer in ONE launch
+        (k_conv_fold_ar / k_conv_fold_ar2, lenet_v2.hip)."""
+        if self._ipdev is None:
+            peer = self.comm.peer
+            rid, off = peer.registered_range(self.grads)
+            assert off == 0
+            self._ipdev = torch.frombuffer(bytearray(peer.native.registered_device_args(rid)), dtype=torch.uint8)
+            self._fold_sync = torch.zeros(2, device=self.device, dtype=torch.int32)
+        o = self.off
+        lo, hi = self.bucket_ranges[1]
+        self.K.lenet_conv_fold_ar(self._ipdev, self.slab, self.c1img, B, self.grads, o["conv1.weight"],
+                                  o["conv1.bias"], o["conv2.weight"], o["conv2.bias"], lo, hi, self._fold_sync, 1.0,
+                                  int(two))
+
+    def pfold_ok(self, two: bool = False) -> bool:
+        """The fused fold + all-reduce route is available: v2 ext-mode layout, the flat gradient buffer
+        registered for the in-place peer route, and (one-shot) one grid that fits the peer grid cap."""
+        peer = getattr(self.comm, "peer", None) if self.comm is not None else None
+        if not self.v2 or self.bwd_mode != "ext" or peer is None or peer.native is None:
+            return False
+        reg = peer.registered_range(self.grads)
+        if reg is None or reg[1] != 0 or self.grads.numel() % 4:
+            return False
+        if two:
+            return True
+        n4 = self.grads.numel() // 4
+        return (n4 + 2047) // 2048 <= min(256, 256 // max(1, getattr(peer, "shared", 1)))
+
+    def _conv_bwd2(self, B: int, q: int, fused_fc_route: Optional[str] = None, fold: bool = True):
         """The v2 conv backward (+ the next batch's prefetch and the meters); ``fused_fc_route``
         ('peer1' / 'peer2'): its W blocks also all-reduce the fc bucket across ranks once their own work
         is done."""
@@ -267,7 +299,7 @@ class LeNetTrainStep:
         self.K.lenet_conv_bwd2(self.Xb[q], self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B, self.slab,
                                self.c1rep, self.c1part, self.tick, self.grads, o["conv1.weight"], o["conv1.bias"],
                                o["conv2.weight"], o["conv2.bias"], **kw)
-        if mode == "ext":      # canonical conv gradients (fixed-order sums) for the conv-bucket all-reduce
+        if mode == "ext" and fold:   # canonical conv gradients (fixed-order sums) for the conv-bucket all-reduce
             self.K.lenet_conv_grad_fold(self.slab, self.c1img, B, self.grads, o["conv1.weight"], o["conv1.bias"],
                                         o["conv2.weight"], o["conv2.bias"])
 
@@ -319,8 +351,10 @@ class LeNetTrainStep:
         cur = torch.cuda.current_stream(self.device)
         ev, cs = self._ev, self.comm_stream
         K.lenet_fc_bwd(*fc_args)
+        pfold = (self.comm.routes.get(self.grads.numel()) if self.comm_on and self.mode == "serial" else None)
+        pfold = pfold if pfold in ("pfold", "pfold2") else None
         if self.v2:
-            conv_bwd = lambda: self._conv_bwd2(B, q)
+            conv_bwd = lambda: self._conv_bwd2(B, q, fold=not pfold)
         else:
             conv_args = (self.X, rows, self.P1, self.A1, self.dP2m, self.A2, p["conv2.weight"], B,
                          self.g_c1w_rep, self.g_c1b_rep, g["conv2.weight"], g["conv2.bias"], C1_NREP, C1_STRIDE,
@@ -361,7 +395,10 @@ class LeNetTrainStep:
             self._opt(0, self.params.numel(), True)
             return
         if self.mode == "serial":
-            self.comm.all_reduce_(self.grads)
+            if pfold:
+                self._fold_ar(B, two=pfold == "pfold2")   # fold + all-reduce in one launch
+            else:
+                self.comm.all_reduce_(self.grads)
             self._opt(0, self.params.numel(), True)
             return
         ev["conv"].record(cur)
@@ -585,6 +622,11 @@ class LeNetTrainStep:
         out = [("overlap", {n0: a, n1: b}) for a in routes for b in routes]
         out += [("overlap2", {n0: a, n1: b}) for a in routes for b in routes]
         out += [(m, {nall: a}) for m in ("flat", "serial") for a in routes]
+        if getattr(self.comm, "peer", None) is not None:
+            if self.pfold_ok():
+                out += [("serial", {nall: "pfold"})]     # fold + in-place one-shot in one launch
+            if self.pfold_ok(two=True) and self.world > 1:
+                out += [("serial", {nall: "pfold2"})]    # fold + in-place two-shot in one launch
         if getattr(self.comm, "peer", None) is not None:
             out += [("fused", {n0: a, n1: b}) for a in ("peer1", "peer2") for b in routes]
             if self.optimizer == "adam":         # last: a failing candidate poisons the peer protocol
