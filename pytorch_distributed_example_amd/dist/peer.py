@@ -57,6 +57,13 @@ def _host_allreduce_max_f64(group, vals) -> list:
     return t.tolist()
 
 
+def _device_uuid(device: torch.device) -> str:
+    try:
+        return str(torch.cuda.get_device_properties(device).uuid)
+    except Exception:   # noqa: BLE001 - older torch: fall back to the index (the rank's own view)
+        return f"index-{torch.device(device).index}"
+
+
 class PeerAllReduce:
     """Collective constructor; see the module docstring.  ``ok`` says whether the path is usable."""
 
@@ -85,12 +92,15 @@ class PeerAllReduce:
             self.native.set_timeout_ms(int(timeout_ms))
             group.store.set(f"{key}/h{self.rank}", self.native.handle())
             group.store.set(f"{key}/dev{self.rank}", str(self.device.index).encode())
+            group.store.set(f"{key}/uuid{self.rank}", _device_uuid(self.device).encode())
         except Exception as e:   # noqa: BLE001 - any failure means "no peer path"
             err = f"setup: {e}"
             group.store.set(f"{key}/h{self.rank}", b"")
             group.store.set(f"{key}/dev{self.rank}", b"-1")
+            group.store.set(f"{key}/uuid{self.rank}", f"none-{self.rank}".encode())
         handles = [group.store.get(f"{key}/h{r}") for r in range(self.world)]
         devs = [int(group.store.get(f"{key}/dev{r}")) for r in range(self.world)]
+        uuids = [group.store.get(f"{key}/uuid{r}").decode() for r in range(self.world)]
         if not err:
             try:
                 if any(len(h) == 0 for h in handles):
@@ -100,7 +110,9 @@ class PeerAllReduce:
                     if d != me and not torch.cuda.can_device_access_peer(me, d):
                         raise RuntimeError(f"cuda:{me} cannot access peer cuda:{d}")
                 self.native.open(handles)
-                self.shared = devs.count(me)       # ranks time-sharing this GPU (1 on a real node)
+                # ranks time-sharing this GPU (1 on a real node), by physical device (a per-rank
+                # HIP_VISIBLE_DEVICES makes every rank's index 0)
+                self.shared = uuids.count(uuids[self.rank])
                 if self.shared > 1:
                     # every sharing rank's spinning grid must be co-resident (else a rank's kernel waits
                     # for CUs that another rank's blocks hold while they wait for it: a deadlock until

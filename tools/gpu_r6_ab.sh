@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round 6: same-box A/B of two builds of the kernel library (ab/kernels_old.so, ab/kernels_new.so; untracked,
+# built in-tree before the call), swapped in place between runs: LeNet GPU tests on the new build, then the
+# toy-CNN headline (driver flags, 5 interleaved reps) and the 2000-step run (2 reps).
+set -o pipefail
+O=gpurun_out/${1:-r6_ab}
+mkdir -p $O
+export TMPDIR=/tmp
+LIB=pytorch_distributed_example_amd/_lib/_kernels.cpython-310-x86_64-linux-gnu.so
+cp ab/kernels_new.so $LIB
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lenet_gpu.py > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+tail -1 $O/pytest.txt
+for r in 1 2 3 4 5; do
+  for v in old new; do
+    cp ab/kernels_$v.so $LIB
+    timeout -k 10 200 python bench.py --steps 20 --warmup 5 --comm-figure off > $O/w20_${v}_$r.json 2>> $O/err.txt || exit 1
+  done
+done
+for r in 1 2; do
+  for v in old new; do
+    cp ab/kernels_$v.so $LIB
+    timeout -k 10 200 python bench.py --steps 2000 --warmup 200 --comm-figure off > $O/w2000_${v}_$r.json 2>> $O/err.txt || exit 1
+  done
+done
+cp ab/kernels_new.so $LIB
+python3 - $O <<'PY'
+import json, sys, glob, statistics
+o = sys.argv[1]
+for w in ("w20", "w2000"):
+    for v in ("old", "new"):
+        xs = [json.load(open(f))["ms_per_step"] * 1000 for f in sorted(glob.glob(f"{o}/{w}_{v}_*.json"))]
+        print(w, v, [round(x, 2) for x in xs], "median", round(statistics.median(xs), 2))
+PY
