@@ -961,13 +961,19 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ H1, int
     const float* a3 = &pv[3][c >> 2].x;
     z[c] = (a0[c & 3] + a1[c & 3]) + (a2[c & 3] + a3[c & 3]) + bias[c];
   }
+  // log_softmax once: the model's log_softmax followed by cross_entropy's is the same function
+  // (log_softmax is idempotent: logsumexp(log_softmax(z)) = 0), so CE(log_softmax(z)) = -lp[y] and
+  // dlogits = softmax(z) - onehot(y) exactly; p reuses the exponentials of the sum
   float m = z[0];
 #pragma unroll
   for (int c = 1; c < kCls; ++c) m = fmaxf(m, z[c]);
-  float se = 0.f;
+  float ez[kCls], se = 0.f;
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) se += expf(z[c] - m);
-  const float lse = logf(se);
+  for (int c = 0; c < kCls; ++c) {
+    ez[c] = expf(z[c] - m);
+    se += ez[c];
+  }
+  const float lse = logf(se), rse = 1.f / se;
   float lp[kCls];
 #pragma unroll
   for (int c = 0; c < kCls; ++c) lp[c] = z[c] - m - lse;
@@ -977,13 +983,9 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ H1, int
   for (int c = 1; c < kCls; ++c) {
     if (lp[c] > m2) { m2 = lp[c]; pred = c; }
   }
-  float se2 = 0.f;
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) se2 += expf(lp[c] - m2);
-  const float lse2 = logf(se2);
   float lpy = 0.f;
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) lpy = (c == y) ? lp[c] - m2 - lse2 : lpy;
+  for (int c = 0; c < kCls; ++c) lpy = (c == y) ? lp[c] : lpy;
   const float loss = -lpy;
   const int hit = pred == y ? 1 : 0;
   if (t == 0) {
@@ -1002,15 +1004,9 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ H1, int
     logp_out[(size_t)row * kCls + t] = v;
   }
   if (!dZ1) return;
-  float dz[kCls], sdl = 0.f;
+  float dz[kCls];
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) {
-    const float dl = (expf(lp[c] - m2 - lse2) - (c == y ? 1.f : 0.f)) * inv_b;
-    dz[c] = dl;
-    sdl += dl;
-  }
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) dz[c] = dz[c] - expf(lp[c]) * sdl;
+  for (int c = 0; c < kCls; ++c) dz[c] = (ez[c] * rse - (c == y ? 1.f : 0.f)) * inv_b;
   if (t < kCls) {
     float v = 0.f;
 #pragma unroll
