@@ -51,7 +51,8 @@ constexpr int kL_TOT = kL_W1 + 528;          // 23904 floats = 93 KB
 #define PMARK(ph)                                                                             \
   do {                                                                                        \
     if constexpr (PROF) {                                                                     \
-      if (threadIdx.x == 0) prof[(size_t)blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+      if (threadIdx.x == 0)                                                                   \
+        prof[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                                         \
   } while (0)
 

@@ -60,6 +60,14 @@ def analyse(buf):
         if k == 0:
             rec["phases_p50"] = [round(float(np.median(rows[:, p] - st)) * tick, 2) for p in range(1, 8)
                                  if (rows[:, p] > 0).all()]
+            idx = np.nonzero(live)[0]
+            half = (idx.max() + 1) // 2       # 2-D grid (B, 2) flattened: [0, B) co-half / block column 0
+            for c, sel in (("ct0", idx < half), ("ct1", idx >= half)):
+                r = rows[sel]
+                if len(r):
+                    rec[f"phases_p50_{c}"] = [round(float(np.median(r[:, p] - r[:, 0])) * tick, 2)
+                                              for p in range(1, 8) if (r[:, p] > 0).all()]
+                    rec[f"end_max_{c}"] = round((r[:, 1:8].max(axis=1).max() - t0) * tick, 2)
         if k in ROLES:
             roles = {}
             for rid, rname in ROLES[k].items():
