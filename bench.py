@@ -119,6 +119,7 @@ class _Job:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = 0 if args.shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
         self.spin_wait = False
+        self.numa = None
 
 
 def _comm_info(dist, comm, eng):
@@ -481,6 +482,7 @@ def lenet_main(job: _Job):
             "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
             "grad_allreduce": "none" if not eng.comm_on else eng.mode,
             "host_wait": "spin" if job.spin_wait else "runtime default",
+            "host_cpus": f"NUMA node of GPU {job.numa}" if job.numa else "unpinned",
             **_comm_info(dist, comm, eng),
             **extra,
         },
@@ -562,6 +564,10 @@ def main(argv=None):
             print(json.dumps(_error_line(args, job.world, f"--gpus {args.gpus} but WORLD_SIZE={job.world}")),
                   flush=True)
         sys.exit(2)
+    if os.environ.get("PDE_BENCH_NUMA", "1") != "0":
+        # before any HIP call: host threads on the GPU's own socket (launch doorbells, sync polling)
+        from pytorch_distributed_example_amd.utils.hipsched import bind_local_numa
+        job.numa = bind_local_numa(job.local_rank)
     if not args.no_spin_wait:
         # before any HIP context exists: spinning host waits keep the graph-launch path fast
         from pytorch_distributed_example_amd.utils.hipsched import set_schedule

@@ -29,3 +29,68 @@ def set_schedule(device: int = 0, flag: int = HIP_DEVICE_SCHEDULE_SPIN) -> bool:
     if lib.hipSetDevice(ctypes.c_int(device)) != 0:
         return False
     return lib.hipSetDeviceFlags(ctypes.c_uint(flag)) == 0
+
+
+def _cpu_list(spec: str):
+    cpus = set()
+    for part in spec.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def gpu_local_cpus(device: int = 0):
+    """(PCI address, CPU set) of the host NUMA node nearest to visible GPU ``device``, read from the
+    KFD topology and sysfs without initialising HIP; None when unavailable.  Visible GPUs are the KFD
+    GPU nodes in node order, filtered by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES when set (the HIP
+    runtime's own enumeration order)."""
+    import glob
+    import os
+    try:
+        nodes = []
+        for path in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            props = {}
+            try:                      # a container may hide other GPUs' nodes (EPERM): not ours
+                with open(path) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        props[k] = v.strip()
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                nodes.append((int(path.split("/")[-2]), props))
+        nodes.sort()
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+            sel = os.environ.get(var)
+            if sel and all(s.strip().isdigit() for s in sel.split(",")):
+                picked = [nodes[int(s)] for s in sel.split(",") if int(s) < len(nodes)]
+                if len(picked) == len(sel.split(",")) and len(nodes) > len(picked):
+                    nodes = picked
+        props = nodes[device][1]
+        loc, dom = int(props["location_id"]), int(props.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+        with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
+            cpus = _cpu_list(f.read())
+        return (bdf, cpus) if cpus else None
+    except Exception:   # noqa: BLE001 - topology not readable: leave the affinity alone
+        return None
+
+
+def bind_local_numa(device: int = 0):
+    """Pin this process to the CPUs of the NUMA node nearest to GPU ``device`` (call before the first
+    HIP call, so the runtime's own threads inherit it): the host side of every launch and of every
+    synchronize (doorbell writes, completion-signal polling) then stays on the GPU's socket.  Returns
+    the GPU's PCI address, or None if nothing was changed."""
+    import os
+    got = gpu_local_cpus(device)
+    if got is None:
+        return None
+    bdf, cpus = got
+    allowed = os.sched_getaffinity(0)
+    use = cpus & allowed
+    if not use or use == allowed:
+        return None
+    os.sched_setaffinity(0, use)
+    return bdf
