@@ -205,3 +205,13 @@ def test_flat_bind_keeps_existing_grads():
     lay.bind(net)
     for n, p in net.named_parameters():
         assert torch.equal(p.grad, before[n])
+
+
+def test_numa_cpu_list_parsing_and_no_gpu_fallback():
+    """bench.py's host pinning: sysfs cpulist syntax, and no change without a readable GPU topology."""
+    from pytorch_distributed_example_amd.utils import hipsched
+    assert hipsched._cpu_list("64-127,192-255\n") == set(range(64, 128)) | set(range(192, 256))
+    assert hipsched._cpu_list("3") == {3}
+    assert hipsched._cpu_list("") == set()
+    if hipsched.gpu_local_cpus(0) is None:           # CPU-only container: nothing to pin
+        assert hipsched.bind_local_numa(0) is None
