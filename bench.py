@@ -247,7 +247,10 @@ def _init_group(job: _Job):
 
     if dist.is_initialized():
         return
-    init = "env://" if "MASTER_PORT" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
+    if "MASTER_PORT" in os.environ:
+        init = "env://"
+    else:   # W = 1: port 0 lets the store bind an ephemeral port (a probed port can be taken meanwhile)
+        init = f"tcp://127.0.0.1:{0 if job.world == 1 else _free_port()}"
     backend = "gloo" if job.args.shared_gpu or os.environ.get("PDE_BENCH_STUB") == "1" else "nccl"
     with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
         dist.init_process_group(backend, init_method=init, rank=job.rank, world_size=job.world)

@@ -188,7 +188,8 @@ __device__ __forceinline__ void ipd_arrive(const PeerIpDev& d, int vb, uint32_t*
 }
 
 // wait (and with SIGNAL first publish `target` into every rank's slot for this rank) until every rank's
-// slot in the own region holds `target`; skip_own: the own slot is known to hold it (arrival add)
+// slot in the own region holds `target`; skip_own: no signal to / poll of the own slot (barrier A: the
+// arrival add already put `target` there; B / C: no other rank reads it, the drain orders own accesses)
 template <bool SIGNAL>
 __device__ __forceinline__ void ipd_barrier(const PeerIpDev& d, int phase, int vb, uint32_t target, bool failed,
                                             bool skip_own, uint32_t* bad) {

@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(512) void k_conv_fold_ar(FoldArArgs a) {
   pde::peer_vec_t res[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) res[u] = pde::peer_sum(v[u], d.world, a.scale);   // fixed rank order
-  pde::ipd_barrier<true>(d, 1, vb, target, failed, false, &s_bad);   // B: every rank has read every buffer
+  pde::ipd_barrier<true>(d, 1, vb, target, failed, true, &s_bad);    // B: every rank has read every buffer
   const bool bad = s_bad != 0;
   const pde::peer_vec_t nanv = {0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u};
 #pragma unroll
@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(512) void k_conv_fold_ar2(FoldArArgs a) {
       if (i < len) __builtin_amdgcn_raw_buffer_store_b128(o, ro, (int)((lo + i) * 16), 0, pde::kIpdAuxSys);
     }
   }
-  pde::ipd_barrier<true>(d, 1, vb, target, failed, false, &s_bad);  // B: every chunk reduced, every input read
+  pde::ipd_barrier<true>(d, 1, vb, target, failed, true, &s_bad);   // B: every chunk reduced, every input read
   const bool bad = s_bad != 0;
   const long long last = a.n4 - 1;
   for (long long i0 = t0; i0 < chunk4; i0 += R * stride) {        // all-gather: chunk q from its owner q
@@ -1303,7 +1303,7 @@ __global__ __launch_bounds__(512) void k_conv_fold_ar2(FoldArArgs a) {
       }
     }
   }
-  pde::ipd_barrier<true>(d, 2, vb, target, failed, false, &s_bad);  // C: every rank has gathered
+  pde::ipd_barrier<true>(d, 2, vb, target, failed, true, &s_bad);   // C: every rank has gathered
   fold_ar_exit(a);
 }
 

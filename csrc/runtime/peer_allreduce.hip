@@ -319,8 +319,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ip_rsrc(const uint8_t* p, int6
 // consumed, write-through stores acknowledged), then lane t < W stores the call number into rank t's
 // slot for this rank and waits for rank t's store into ours (relaxed system-scope accesses to
 // uncached memory).  A time-out poisons the call (NaN results) and latches the error words.
-// SKIP_OWN: this rank's own slot is known to hold `target` already (barrier A's signal is an atomic
-// add whose return value this block waited for) -- no poll of it.
+// SKIP_OWN: no signal to and no poll of this rank's own slot.  Barrier A: the slot already holds
+// `target` (its signal is an atomic add whose return value this block waited for).  Barriers B / C:
+// nobody else reads a rank's own slot, and the drain above already orders this block's own accesses;
+// the store-then-poll round trip on uncached memory was pure latency (-0.54 us per one-shot call and
+// -1.08 us per two-shot call at W = 1, profiles/r6_comm/skip_own_bc/).
 template <int W, bool SIGNAL = true, bool SKIP_OWN = false>
 __device__ __forceinline__ void ip_barrier(const IpArgs& a, int phase, uint32_t target, bool failed, uint32_t* bad) {
   if constexpr (SIGNAL) {
@@ -422,7 +425,7 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
 #pragma unroll
       for (int p = 0; p < W; ++p) Op::add(acc[u], v[u][p]);  // fixed rank order: bit-identical on every rank
     }
-    ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every rank has read every buffer
+    ip_barrier<W, true, true>(a, 1, target, failed, &s_bad);   // B: every rank has read every buffer
     const bool bad = s_bad != 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -457,7 +460,7 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
         if (i < len) __builtin_amdgcn_raw_buffer_store_b128(o, ro, (int)((lo + i) * 16), 0, kAuxSys);
       }
     }
-    ip_barrier<W>(a, 1, target, failed, &s_bad);        // B: every chunk reduced, every input read
+    ip_barrier<W, true, true>(a, 1, target, failed, &s_bad);   // B: every chunk reduced, every input read
     const bool bad = s_bad != 0;
     if (tail_lane) Op::tail_store(own, tail_off + threadIdx.x, bad ? __builtin_nanf("") : tail_sum * a.scale);
     // all-gather: chunk q from its owner q (W-1 loads in flight per lane)
@@ -484,7 +487,7 @@ __global__ void __launch_bounds__(kThreads) peer_inplace_kernel(IpArgs a) {
         }
       }
     }
-    ip_barrier<W>(a, 2, target, failed, &s_bad);        // C: every rank has gathered from every owner
+    ip_barrier<W, true, true>(a, 2, target, failed, &s_bad);   // C: every rank has gathered from every owner
   }
 }
 

@@ -338,6 +338,13 @@ def _rendezvous(init_method: Optional[str], rank: int, world: int, timeout_ms: i
             return server, R.StoreClient(host, port, timeout_ms)
     elif init_method.startswith("tcp://"):
         host, port = _parse_tcp(init_method)
+        if port == 0:
+            # single-process job: the store takes an ephemeral port itself (no free-port probe that
+            # another socket can take between the probe and the bind)
+            if world != 1:
+                raise ValueError(f"init_method {init_method!r}: port 0 needs world_size 1, got {world}")
+            server = R.StoreServer("0.0.0.0", 0)
+            return server, R.StoreClient(host, server.port, timeout_ms)
     else:
         raise ValueError(f"unsupported init_method {init_method!r} (use tcp://host:port or env://)")
     server = R.StoreServer("0.0.0.0", port) if rank == 0 else None
