@@ -448,6 +448,10 @@ def lenet_main(job: _Job):
     stub = os.environ.get("PDE_BENCH_STUB") == "1"
     if not stub:
         torch.cuda.set_device(job.local_rank)
+        if job.numa:
+            from pytorch_distributed_example_amd.utils.hipsched import verify_numa_binding
+            if not verify_numa_binding(job.numa, job.local_rank):
+                job.numa = None           # KFD order is not the runtime's device order: unpinned
     comm_world = world > 1 or args.force_comm
     anchors = None
     if world > 1:

@@ -93,4 +93,27 @@ def bind_local_numa(device: int = 0):
     if not use or use == allowed:
         return None
     os.sched_setaffinity(0, use)
+    _NUMA_PREV[0] = allowed
     return bdf
+
+
+_NUMA_PREV = [None]   # the affinity bind_local_numa replaced
+
+
+def verify_numa_binding(bdf, device: int = 0, props=None) -> bool:
+    """After HIP is up: check that ``bdf`` (bind_local_numa's pick, from KFD node order) is the PCI
+    address the runtime reports for ``device``.  On a mismatch (a runtime that orders GPUs otherwise)
+    the previous affinity is restored and False returned; True when it matches or nothing was bound."""
+    import os
+    if bdf is None:
+        return True
+    if props is None:
+        import torch
+        props = torch.cuda.get_device_properties(device)
+    want = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+    if bdf.lower().startswith(want):
+        return True
+    if _NUMA_PREV[0] is not None:
+        os.sched_setaffinity(0, _NUMA_PREV[0])
+        _NUMA_PREV[0] = None
+    return False

@@ -215,3 +215,26 @@ def test_numa_cpu_list_parsing_and_no_gpu_fallback():
     assert hipsched._cpu_list("") == set()
     if hipsched.gpu_local_cpus(0) is None:           # CPU-only container: nothing to pin
         assert hipsched.bind_local_numa(0) is None
+
+
+def test_numa_binding_verified_against_runtime_pci_address():
+    """bench.py re-checks the KFD-order pick against the runtime's PCI address once HIP is up; on a
+    mismatch the affinity bind_local_numa replaced comes back."""
+    import os
+    from types import SimpleNamespace
+
+    from pytorch_distributed_example_amd.utils import hipsched
+    props = SimpleNamespace(pci_domain_id=0, pci_bus_id=0xA7, pci_device_id=0)
+    assert hipsched.verify_numa_binding(None, 0, props)
+    assert hipsched.verify_numa_binding("0000:a7:00.0", 0, props)
+    before = os.sched_getaffinity(0)
+    one = {min(before)}
+    try:
+        os.sched_setaffinity(0, one)                 # as bind_local_numa would have
+        hipsched._NUMA_PREV[0] = before
+        assert not hipsched.verify_numa_binding("0000:05:00.0", 0, props)
+        assert os.sched_getaffinity(0) == before
+        assert hipsched._NUMA_PREV[0] is None
+    finally:
+        os.sched_setaffinity(0, before)
+        hipsched._NUMA_PREV[0] = None
