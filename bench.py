@@ -76,6 +76,9 @@ def build_parser():
                     help="untimed back-to-back training steps (about this many ms of GPU work) right before the "
                          "W warm-up steps, so the timed window starts at the clock a sustained run holds "
                          "(0 = off; PDE_BENCH_CLOCK_WARM_MS overrides)")
+    ap.add_argument("--lead-steps", type=int, default=int(os.environ.get("PDE_BENCH_LEAD", "1")),
+                    help="graph mode: the first L timed steps replay as 1-step graphs ahead of the multi-step "
+                         "graphs, so the GPU starts while the host still submits the long graph (0 = off)")
     ap.add_argument("--comm-figure", choices=["auto", "on", "off"], default="auto",
                     help="W=1: also time the step with RCCL initialised + the comm path on (auto = on at W=1)")
     ap.add_argument("--train-size", type=int, default=60000)
@@ -108,6 +111,14 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _graph_plan(args, S: int) -> str:
+    """The timed window's replays, e.g. '1 + 19 steps (hipGraphs)' for --steps 20 with one lead step."""
+    L = min(max(args.lead_steps, 0), args.steps)
+    full, r = divmod(args.steps - L, S)
+    parts = ["1"] * L + ([str(S) if full == 1 else f"{S} x{full}"] if full else []) + ([str(r)] if r else [])
+    return f"graph replays of {' + '.join(parts)} steps"
 
 
 class _Job:
@@ -295,12 +306,21 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     Sw = _graph_steps(args, args.warmup) if args.warmup > 0 else 1
     extra = {}
 
-    def run(n, S=S):
+    # timed window: L lead steps (1-step graphs: a short graph starts on the GPU ~10 us sooner than a
+    # 20-step one, and the long graph's submission then overlaps the lead step), then graphs of S steps
+    # and one graph of the remainder (profiles/r6_lenet/lead_step/)
+    L = min(max(args.lead_steps, 0), steps) if args.mode == "graph" else 0
+    r_timed = (steps - L) % S
+
+    def run(n, S=S, lead=0):
         if args.mode == "graph":
-            for _ in range(n // S):
-                eng.replay(steps=S)             # S steps per replay
-            for _ in range(n % S):
+            for _ in range(lead):
                 eng.replay(steps=1)
+            full, r = divmod(n - lead, S)
+            for _ in range(full):
+                eng.replay(steps=S)             # S steps per replay
+            if r:
+                eng.replay(steps=r)             # primed below when it is the timed remainder
         else:
             for _ in range(n):
                 eng.step()
@@ -321,10 +341,10 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
     if args.mode == "graph":
         # both step parities of both graphs are captured and launched once before the warm-up, so no
         # warm-up / step count can make the timed window capture or first-launch a graph
-        eng.prime_graphs(tuple(sorted({S, Sw, 1})), replays=max(1, args.prime_replays))
+        eng.prime_graphs(tuple(sorted({S, Sw, r_timed or 1, 1})), replays=max(1, args.prime_replays))
     _clock_warm(args, eng, run, S)
     try:
-        return _timed_window(job, eng, comm, extra, run, steps, warmup, Sw, max_over_ranks=max_over_ranks)
+        return _timed_window(job, eng, comm, extra, run, steps, warmup, Sw, max_over_ranks=max_over_ranks, lead=L)
     finally:
         if gc_off:
             gc.enable()
@@ -366,7 +386,7 @@ def _device_barrier(comm, dist):
     torch.cuda.synchronize()
 
 
-def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1, max_over_ranks=True):
+def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1, max_over_ranks=True, lead=0):
     """W warm-up steps, then exactly K timed steps bracketed by barrier + device synchronize on both
     sides.  ``max_over_ranks``: the elapsed time is the MAX over ranks (the job's step time); off for
     the per-rank W=1 anchor, whose ranks still start together (host barrier) but time alone."""
@@ -393,7 +413,10 @@ def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1, max_over_rank
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     t0 = time.perf_counter()
-    run(steps)
+    if lead:
+        run(steps, lead=lead)
+    else:
+        run(steps)
     t_launch = time.perf_counter() - t0
     if trace:
         ev1.record()
@@ -486,7 +509,7 @@ def lenet_main(job: _Job):
             "seq_len": None,
             "parallelism": f"dp{world}",
             "optimizer": "Adam(lr=1e-3)",
-            "mode": args.mode if args.mode == "eager" else f"graph x{S} steps",
+            "mode": args.mode if args.mode == "eager" else _graph_plan(args, S),
             "grad_allreduce": "none" if not eng.comm_on else eng.mode,
             "host_wait": "spin" if job.spin_wait else "runtime default",
             "host_cpus": f"NUMA node of GPU {job.numa}" if job.numa else "unpinned",
