@@ -113,6 +113,13 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _replay_plan(n: int, S: int, lead: int = 0) -> list:
+    """Graph lengths replayed for n steps: ``lead`` 1-step graphs, then S-step graphs, then one graph of
+    the remainder."""
+    full, r = divmod(n - lead, S)
+    return [1] * lead + [S] * full + ([r] if r else [])
+
+
 def _graph_plan(args, S: int) -> str:
     """The timed window's replays, e.g. '1 + 19 steps (hipGraphs)' for --steps 20 with one lead step."""
     L = min(max(args.lead_steps, 0), args.steps)
@@ -314,13 +321,8 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
 
     def run(n, S=S, lead=0):
         if args.mode == "graph":
-            for _ in range(lead):
-                eng.replay(steps=1)
-            full, r = divmod(n - lead, S)
-            for _ in range(full):
-                eng.replay(steps=S)             # S steps per replay
-            if r:
-                eng.replay(steps=r)             # primed below when it is the timed remainder
+            for k in _replay_plan(n, S, lead):
+                eng.replay(steps=k)             # every length in the plan is primed below
         else:
             for _ in range(n):
                 eng.step()

@@ -2,6 +2,7 @@
 process groups, launcher failure handling -- W in {2, 3, 4} processes on 127.0.0.1."""
 import threading
 import time
+from types import SimpleNamespace
 
 import pytest
 
@@ -256,3 +257,21 @@ def test_bench_validate_ranks_rules():
     assert "on device 0" in bench.validate_ranks([row(0), row(1, rccl_device=0), row(2), row(3)], 4)
     assert "some ranks only" in bench.validate_ranks([row(0), row(1, peer_ok=False), row(2), row(3)], 4)
     assert "expected 4" in bench.validate_ranks(good[:3], 4)
+
+
+def test_bench_replay_plan():
+    """The timed window's graph replays: exactly n steps, the lead step(s) first, every length primed
+    (the set bench.py captures before the warm-up: S, the warm-up graph, the timed remainder, 1)."""
+    import bench
+    assert bench._replay_plan(20, 20, 1) == [1, 19]
+    assert bench._replay_plan(20, 20, 0) == [20]
+    assert bench._replay_plan(5, 5, 0) == [5]
+    assert bench._replay_plan(2000, 100, 1) == [1] + [100] * 19 + [99]
+    assert bench._replay_plan(1, 1, 1) == [1]
+    for n in (1, 7, 20, 64, 2000):
+        for L in (0, 1, 2):
+            L = min(L, n)
+            S = bench._graph_steps(SimpleNamespace(graph_steps=0, steps=n))
+            plan = bench._replay_plan(n, S, L)
+            assert sum(plan) == n and plan[:L] == [1] * L
+            assert set(plan) <= {S, (n - L) % S or 1, 1}
