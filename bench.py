@@ -599,7 +599,8 @@ def main(argv=None):
     if os.environ.get("PDE_BENCH_NUMA", "1") != "0":
         # before any HIP call: host threads on the GPU's own socket (launch doorbells, sync polling)
         from pytorch_distributed_example_amd.utils.hipsched import bind_local_numa
-        job.numa = bind_local_numa(job.local_rank)
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        job.numa = bind_local_numa(job.local_rank, [0] * lws if args.shared_gpu else list(range(lws)))
     if not args.no_spin_wait:
         # before any HIP context exists: spinning host waits keep the graph-launch path fast
         from pytorch_distributed_example_amd.utils.hipsched import set_schedule

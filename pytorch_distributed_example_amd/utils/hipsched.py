@@ -78,11 +78,14 @@ def gpu_local_cpus(device: int = 0):
         return None
 
 
-def bind_local_numa(device: int = 0):
+def bind_local_numa(device: int = 0, node_devices=None, min_cpus_per_rank: int = 4):
     """Pin this process to the CPUs of the NUMA node nearest to GPU ``device`` (call before the first
     HIP call, so the runtime's own threads inherit it): the host side of every launch and of every
-    synchronize (doorbell writes, completion-signal polling) then stays on the GPU's socket.  Returns
-    the GPU's PCI address, or None if nothing was changed."""
+    synchronize (doorbell writes, completion-signal polling) then stays on the GPU's socket.
+    ``node_devices``: the GPU of every rank on this host; the ranks whose GPU shares this NUMA node
+    share its CPUs, and with fewer than ``min_cpus_per_rank`` each (a container granted few CPUs)
+    nothing is pinned -- spinning host waits of several ranks on a handful of cores would cost more
+    than the socket locality gains.  Returns the GPU's PCI address, or None if nothing was changed."""
     import os
     got = gpu_local_cpus(device)
     if got is None:
@@ -90,7 +93,11 @@ def bind_local_numa(device: int = 0):
     bdf, cpus = got
     allowed = os.sched_getaffinity(0)
     use = cpus & allowed
-    if not use or use == allowed:
+    sharing = 1
+    if node_devices is not None:
+        sharing = max(1, sum(1 for d in node_devices
+                             if d == device or ((g := gpu_local_cpus(d)) is not None and g[1] == cpus)))
+    if not use or use == allowed or len(use) < min_cpus_per_rank * sharing:
         return None
     os.sched_setaffinity(0, use)
     _NUMA_PREV[0] = allowed

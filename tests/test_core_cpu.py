@@ -238,3 +238,24 @@ def test_numa_binding_verified_against_runtime_pci_address():
     finally:
         os.sched_setaffinity(0, before)
         hipsched._NUMA_PREV[0] = None
+
+
+def test_numa_binding_skipped_when_ranks_would_crowd_the_socket(monkeypatch):
+    """Ranks whose GPUs share a NUMA node share its CPUs: with fewer than 4 per rank nothing is pinned."""
+    import os
+
+    from pytorch_distributed_example_amd.utils import hipsched
+    before = os.sched_getaffinity(0)
+    if len(before) < 8:
+        pytest.skip("needs 8 allowed CPUs")
+    low = set(sorted(before)[:4])
+    topo = {0: ("0000:05:00.0", low), 1: ("0000:06:00.0", low), 2: ("0000:85:00.0", set(sorted(before)[4:8]))}
+    monkeypatch.setattr(hipsched, "gpu_local_cpus", lambda d: topo.get(d))
+    try:
+        assert hipsched.bind_local_numa(0, [0, 1, 2]) is None          # 2 ranks on 4 CPUs
+        assert os.sched_getaffinity(0) == before
+        assert hipsched.bind_local_numa(2, [0, 1, 2]) == "0000:85:00.0"  # 1 rank on 4 CPUs
+        assert os.sched_getaffinity(0) == topo[2][1]
+    finally:
+        os.sched_setaffinity(0, before)
+        hipsched._NUMA_PREV[0] = None
