@@ -154,7 +154,10 @@ def test_read_stats(tmp_path):
     _mnist(["-s", "1", "--epochs", "1", "--cprofile", prof])
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/read_stats.py"), prof, "10"],
                          capture_output=True, text=True, timeout=60)
-    assert out.returncode == 0 and "tottime" in out.stdout
+    assert out.returncode == 0 and "tottime" in out.stdout and "internal time" in out.stdout
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts/read_stats.py"), prof, "5", "--sort",
+                          "cumulative"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "cumulative time" in out.stdout
 
 
 def test_toy_via_torchrun():
