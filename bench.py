@@ -608,6 +608,7 @@ def main(argv=None):
     try:
         if args.model != "lenet":
             from bench_models import run_model_bench
+            args.numa_bdf = job.numa
             return run_model_bench(args)
         return lenet_main(job)
     except Exception as e:   # noqa: BLE001 - always one JSON line, then a non-zero exit

@@ -18,7 +18,10 @@ import sys
 import time
 
 
-def _setup(shared_gpu: bool = False):
+_NUMA = [None]   # the PCI address whose NUMA node this process is pinned to (bench.py), once verified
+
+
+def _setup(shared_gpu: bool = False, numa_bdf=None):
     """(torch, dist, rank, world, device).  ``shared_gpu``: the one-GPU rehearsal of the N > 1 path --
     every rank on cuda:0, a gloo control group, DDP's bucket all-reduces and buffer broadcasts on the
     xGMI peer kernel (in place over the registered flat gradients)."""
@@ -33,6 +36,9 @@ def _setup(shared_gpu: bool = False):
     from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
 
     torch.cuda.set_device(local_rank)
+    if numa_bdf:
+        from pytorch_distributed_example_amd.utils.hipsched import verify_numa_binding
+        _NUMA[0] = numa_bdf if verify_numa_binding(numa_bdf, local_rank) else None
     if world > 1 and not dist.is_initialized():
         with stdout_to_stderr():                  # RCCL's init banner must not precede the JSON line
             dist.init_process_group("gloo" if shared_gpu else "nccl", init_method="env://", rank=rank,
@@ -44,14 +50,9 @@ def _setup(shared_gpu: bool = False):
 def _w1_comm_group(dist):
     """A one-rank RCCL process group for the W = 1 rehearsal of the DDP communication path."""
     if not dist.is_initialized():
-        import socket
-
         from pytorch_distributed_example_amd.utils.stdio import stdout_to_stderr
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        with stdout_to_stderr():
-            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        with stdout_to_stderr():    # port 0: the store binds an ephemeral port itself (no probe race)
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:0", rank=0, world_size=1)
 
 
 def _comm_figure_wanted(args, world) -> bool:
@@ -220,7 +221,7 @@ def _gpt2_run(args, torch, dist, rank, world, dev, comm):
 
 
 def bench_gpt2(args):
-    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False))
+    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False), getattr(args, "numa_bdf", None))
     r = _gpt2_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
     B, T = r["B"], r["T"]
     tps = args.steps * B * T * world / r["elapsed"]
@@ -233,6 +234,7 @@ def bench_gpt2(args):
                 "256 per rank sharded by DistributedSampler, reshuffled per epoch, random-init weights",
         "config": {"model": "GPT-2 small 124M (12L, 12H, d768, ctx 1024, vocab 50257->50304)",
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}",
+                   "host_cpus": f"NUMA node of GPU {_NUMA[0]}" if _NUMA[0] else "unpinned",
                    "optimizer": "AdamW(fp32 master, wd 0.1, clip 1.0)", **r["extra"]},
         "model_tflops_per_gpu": round(r["flops_per_token"] * tps / world / 1e12, 1),
         "last_loss": round(r["last_loss"], 4),

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import json
 
+import bench_models
 from bench_models import (_cap, _capture_step, _comm_figure_wanted, _graph_wanted, _setup, _timed, _tune,
                           _w1_comm_group)
 
@@ -72,7 +73,7 @@ def _resnet_run(args, torch, dist, rank, world, dev, comm):
 
 
 def bench_resnet18(args):
-    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False))
+    torch, dist, rank, world, dev = _setup(getattr(args, "shared_gpu", False), getattr(args, "numa_bdf", None))
     r = _resnet_run(args, torch, dist, rank, world, dev, comm=world > 1 or getattr(args, "force_comm", False))
     B = r["B"]
     ips = args.steps * B * world / r["elapsed"]
@@ -85,6 +86,7 @@ def bench_resnet18(args):
                 "sharded by DistributedSampler, random-init weights",
         "config": {"model": "ResNet-18 (11.69M params, torchvision layout)", "global_batch": B * world,
                    "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}",
+                   "host_cpus": f"NUMA node of GPU {bench_models._NUMA[0]}" if bench_models._NUMA[0] else "unpinned",
                    "optimizer": "SGD(0.1, momentum 0.9, wd 5e-5; fp32 master)", **r["extra"],
                    "memory_format": "channels_last"},
         "last_loss": round(r["last_loss"], 4),
