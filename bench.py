@@ -121,7 +121,8 @@ def _replay_plan(n: int, S: int, lead: int = 0) -> list:
 
 
 def _graph_plan(args, S: int) -> str:
-    """The timed window's replays, e.g. '1 + 19 steps (hipGraphs)' for --steps 20 with one lead step."""
+    """The timed window's replays as reported in config.mode, e.g. 'graph replays of 1 + 19 steps'
+    (--steps 20, one lead step) or 'graph replays of 1 + 100 x19 + 99 steps' (--steps 2000)."""
     L = min(max(args.lead_steps, 0), args.steps)
     full, r = divmod(args.steps - L, S)
     parts = ["1"] * L + ([str(S) if full == 1 else f"{S} x{full}"] if full else []) + ([str(r)] if r else [])
@@ -290,7 +291,7 @@ def _run_lenet(job: _Job, force_comm: bool, steps: int, warmup: int, comm_world:
         if comm_world:
             _init_group(job)
         eng = _StubEngine(True if comm_world and world > 1 else None)
-        return _timed_window(job, eng, None, {}, lambda n, S=1: eng.replay(steps=n), steps, warmup,
+        return _timed_window(job, eng, None, {}, lambda n, S=1, lead=0: eng.replay(steps=n), steps, warmup,
                              max_over_ranks=max_over_ranks)
     dev = torch.device("cuda", job.local_rank)
     with stdout_to_stderr():                      # RCCL's init banner must not precede the JSON line
@@ -415,10 +416,7 @@ def _timed_window(job, eng, comm, extra, run, steps, warmup, Sw=1, max_over_rank
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     t0 = time.perf_counter()
-    if lead:
-        run(steps, lead=lead)
-    else:
-        run(steps)
+    run(steps, lead=lead)
     t_launch = time.perf_counter() - t0
     if trace:
         ev1.record()
